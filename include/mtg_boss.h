@@ -1,0 +1,159 @@
+/*
+ * mtg_boss.h -- C ABI of the MI355X BOSS chunk constructor (libmtg_boss.so).
+ *
+ * Drop-in boundary for MetaGraph's in-memory succinct `build` path.  Each entry point replaces
+ * one member of the reference's chunk-constructor interface (paths relative to
+ * /root/reference/metagraph/src):
+ *
+ *   mtg_boss_ctor_create        IBOSSChunkConstructor::initialize
+ *                               graph/representation/succinct/boss_chunk_construct.hpp:18-34,
+ *                               boss_chunk_construct.cpp:1134-1178 (same 9 parameters + device)
+ *   mtg_boss_ctor_add_sequences IBOSSChunkConstructor::add_sequences(vector<pair<string,u64>>&&)
+ *                               boss_chunk_construct.hpp:26-30 (thread-safe, copies the input)
+ *   mtg_boss_ctor_add_sequence  IBOSSChunkConstructor::add_sequence(string_view, u64 count)
+ *   mtg_boss_ctor_build_chunk   IBOSSChunkConstructor::build_chunk -> BOSS::Chunk
+ *                               (boss_chunk.hpp:19-104: W, last, F, weights, k, alph_size = 5)
+ *   mtg_boss_ctor_get_k         IBOSSChunkConstructor::get_k (BOSS k = DBG k - 1)
+ *   mtg_boss_chunk_free / mtg_boss_ctor_destroy   the destructors
+ *   mtg_last_error              logger->error + exit(1) / throw of the reference become
+ *                               negative return codes plus this message
+ *
+ * Beyond the reference's interface, for callers that already hold reads in HBM (benchmarks,
+ * multi-GPU shards): mtg_boss_build_device runs the whole path on a device buffer and leaves
+ * the BOSS arrays in device memory; mtg_boss_last_timings reports per-stage device times.
+ *
+ * No torch types, no C++ types: plain pointers and sizes.  All functions are thread-safe
+ * except that one constructor must not be built and added to at the same time.
+ */
+#ifndef MTG_BOSS_H
+#define MTG_BOSS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTG_BOSS_ABI_VERSION 1
+
+/* container types of the reference (kmer::ContainerType) */
+#define MTG_CONTAINER_VECTOR 0
+#define MTG_CONTAINER_VECTOR_DISK 1
+
+/* return codes */
+#define MTG_OK 0
+#define MTG_ERR_INVALID_K -1        /* k not in [1, 84]      (reference: exit(1)) */
+#define MTG_ERR_COUNT_WIDTH -2      /* bits_per_count > 32   (reference: runtime_error) */
+#define MTG_ERR_UNSUPPORTED -3      /* suffix filter / disk container not on this path */
+#define MTG_ERR_DEVICE -4           /* HIP runtime / kernel failure */
+#define MTG_ERR_ARGUMENT -5
+#define MTG_ERR_NO_DEVICE -6        /* no MI355X visible: the product path never falls back */
+
+typedef struct mtg_boss_params {
+    uint64_t k;                  /* BOSS k (node length) = DBG k - 1, in [1, 84] */
+    int both_strands;            /* canonical mode: add reverse complements */
+    uint8_t bits_per_count;      /* 0 = no weights; else --count-width (<= 32) */
+    const char *filter_suffix;   /* must be NULL or "" on this path */
+    uint64_t num_threads;        /* host threads for input staging */
+    double memory_preallocated;  /* bytes; advisory (HBM is sized from the input) */
+    int container_type;          /* MTG_CONTAINER_VECTOR */
+    const char *swap_dir;        /* unused on the in-memory path */
+    uint64_t disk_cap_bytes;     /* unused on the in-memory path */
+    int device_id;               /* HIP device ordinal */
+} mtg_boss_params;
+
+typedef struct mtg_boss_ctor mtg_boss_ctor;
+
+/* BOSS::Chunk in host memory (arrays of n entries including the leading row 0) */
+typedef struct mtg_boss_chunk {
+    uint64_t k;
+    uint64_t alph_size;          /* 5: $ACGT */
+    uint64_t n;
+    uint8_t *W;                  /* n labels 0..9 (int_vector width 4 in the reference) */
+    uint8_t *last;               /* n flags 0/1 */
+    uint32_t *weights;           /* n weights or NULL (bits_per_count == 0) */
+    uint64_t F[5];
+    uint8_t bits_per_count;
+    uint64_t n_real;             /* real (non-dummy) edges */
+    uint64_t n_dummy;            /* dummy edges incl. the main dummy row */
+} mtg_boss_chunk;
+
+/* BOSS::Chunk left in device memory (owned by the constructor, valid until its next build) */
+typedef struct mtg_boss_device_chunk {
+    uint64_t k;
+    uint64_t n;
+    uint8_t *W;                  /* device pointers */
+    uint8_t *last;
+    uint32_t *weights;
+    uint64_t F[5];
+    uint64_t n_real;
+    uint64_t n_dummy;
+} mtg_boss_device_chunk;
+
+typedef struct mtg_boss_timings {
+    double total_ms;             /* device time of the whole path (events on the build stream) */
+    double extract_ms;           /* K1 */
+    double sort_ms;              /* K2 over the extracted k-mers */
+    double unique_ms;            /* K3 */
+    double rc_ms;                /* K4 incl. its re-sort */
+    double dummy_ms;             /* K5/K6 incl. dummy sort + unique */
+    double merge_ms;             /* K7 */
+    double emit_ms;              /* K8 */
+    double radix_pass_ms;        /* average onesweep pass of the K2 sort */
+    uint64_t radix_passes;       /* onesweep passes of the K2 sort */
+    uint64_t radix_keys;         /* keys of the K2 sort */
+    uint64_t radix_key_bytes;    /* bytes per key (+ payload) moved per pass per key, one way */
+    uint64_t n_positions;        /* window starts offered to the extractor */
+    uint64_t n_extracted;        /* valid k-mers extracted (N) */
+    uint64_t n_unique;           /* distinct k-mers collected (U) */
+    uint64_t n_real;             /* real edges after rc augmentation */
+    uint64_t n_dummy;            /* dummy edges (sinks + all source levels) */
+    uint64_t n_rows;             /* BOSS rows incl. row 0 */
+} mtg_boss_timings;
+
+int mtg_boss_abi_version(void);
+const char *mtg_last_error(void);
+
+mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *params);
+void mtg_boss_ctor_destroy(mtg_boss_ctor *ctor);
+uint64_t mtg_boss_ctor_get_k(const mtg_boss_ctor *ctor);
+
+/* n sequences, seqs[i] of lens[i] bytes, counts[i] (NULL = all 1).  Copies the input. */
+int mtg_boss_ctor_add_sequences(mtg_boss_ctor *ctor, const char *const *seqs,
+                                const uint64_t *lens, const uint64_t *counts, size_t n);
+int mtg_boss_ctor_add_sequence(mtg_boss_ctor *ctor, const char *seq, uint64_t len,
+                               uint64_t count);
+/* one packed buffer: n sequences back to back, offsets[n + 1] */
+int mtg_boss_ctor_add_packed(mtg_boss_ctor *ctor, const char *data, const uint64_t *offsets,
+                             const uint64_t *counts, size_t n);
+
+/* builds from everything added so far, returns host arrays; clears the added input */
+int mtg_boss_ctor_build_chunk(mtg_boss_ctor *ctor, mtg_boss_chunk *out);
+void mtg_boss_chunk_free(mtg_boss_chunk *chunk);
+
+/*
+ * Device-resident input: `d_seq` holds the reads back to back, each followed by at least one
+ * byte outside {A,C,G,T,U,a,c,g,t,u} (so no k-mer spans two reads).  d_read_starts/d_counts
+ * (both NULL, or n_reads entries) give per-read counts for --count-kmers.  `stream` is a
+ * hipStream_t (NULL = the constructor's own stream).  Arrays stay in device memory.
+ */
+int mtg_boss_build_device(mtg_boss_ctor *ctor, const uint8_t *d_seq, uint64_t seq_len,
+                          const uint64_t *d_read_starts, const uint32_t *d_counts,
+                          uint64_t n_reads, void *stream, mtg_boss_device_chunk *out);
+
+int mtg_boss_last_timings(const mtg_boss_ctor *ctor, mtg_boss_timings *out);
+
+/* device-memory helpers for callers without their own HIP runtime (ctypes, cgo, JNI) */
+void *mtg_device_alloc(int device_id, uint64_t bytes);
+int mtg_device_free(void *ptr);
+int mtg_memcpy_h2d(void *dst, const void *src, uint64_t bytes);
+int mtg_memcpy_d2h(void *dst, const void *src, uint64_t bytes);
+int mtg_device_count(void);
+int mtg_device_synchronize(int device_id);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MTG_BOSS_H */

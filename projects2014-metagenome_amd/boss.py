@@ -1,0 +1,246 @@
+"""Host-side mirror of the reference's chunk-constructor interface over libmtg_boss.so.
+
+Same names, argument meaning and error behaviour as
+graph/representation/succinct/boss_chunk_construct.hpp:18-34 (IBOSSChunkConstructor) and
+boss_chunk.hpp:19-104 (BOSS::Chunk), so tests read like the reference's own:
+
+    ctor = IBOSSChunkConstructor.initialize(k, both_strands, bits_per_count)
+    ctor.add_sequences(["ACGT...", ...])
+    chunk = ctor.build_chunk()          # chunk.W, chunk.last, chunk.F, chunk.weights
+
+The constructor runs entirely on the MI355X through the C ABI (include/mtg_boss.h).  There is
+no CPU fallback: a missing library or device raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmtg_boss.so")
+
+CONTAINER_VECTOR = 0
+CONTAINER_VECTOR_DISK = 1
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_uint64), ("both_strands", ctypes.c_int),
+                ("bits_per_count", ctypes.c_uint8), ("filter_suffix", ctypes.c_char_p),
+                ("num_threads", ctypes.c_uint64), ("memory_preallocated", ctypes.c_double),
+                ("container_type", ctypes.c_int), ("swap_dir", ctypes.c_char_p),
+                ("disk_cap_bytes", ctypes.c_uint64), ("device_id", ctypes.c_int)]
+
+
+class _Chunk(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_uint64), ("alph_size", ctypes.c_uint64), ("n", ctypes.c_uint64),
+                ("W", ctypes.POINTER(ctypes.c_uint8)), ("last", ctypes.POINTER(ctypes.c_uint8)),
+                ("weights", ctypes.POINTER(ctypes.c_uint32)), ("F", ctypes.c_uint64 * 5),
+                ("bits_per_count", ctypes.c_uint8), ("n_real", ctypes.c_uint64),
+                ("n_dummy", ctypes.c_uint64)]
+
+
+class _DeviceChunk(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_uint64), ("n", ctypes.c_uint64),
+                ("W", ctypes.c_void_p), ("last", ctypes.c_void_p), ("weights", ctypes.c_void_p),
+                ("F", ctypes.c_uint64 * 5), ("n_real", ctypes.c_uint64),
+                ("n_dummy", ctypes.c_uint64)]
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_double) for name in
+                ("total_ms", "extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms",
+                 "merge_ms", "emit_ms", "radix_pass_ms")] + \
+               [(name, ctypes.c_uint64) for name in
+                ("radix_passes", "radix_keys", "radix_key_bytes", "n_positions", "n_extracted",
+                 "n_unique", "n_real", "n_dummy", "n_rows")]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# exported C-ABI symbols (must match include/mtg_boss.h)
+EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
+           "mtg_boss_ctor_destroy", "mtg_boss_ctor_get_k", "mtg_boss_ctor_add_sequences",
+           "mtg_boss_ctor_add_sequence", "mtg_boss_ctor_add_packed", "mtg_boss_ctor_build_chunk",
+           "mtg_boss_chunk_free", "mtg_boss_build_device", "mtg_boss_last_timings",
+           "mtg_device_alloc", "mtg_device_free", "mtg_memcpy_h2d", "mtg_memcpy_d2h",
+           "mtg_device_count", "mtg_device_synchronize")
+
+_lib = None
+
+
+def lib():
+    """Load libmtg_boss.so (built by __graft_entry__.build()); raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libmtg_boss.so is not built (run __graft_entry__.build()); "
+                               "the BOSS constructor has no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        L.mtg_boss_abi_version.restype = ctypes.c_int
+        L.mtg_last_error.restype = ctypes.c_char_p
+        L.mtg_boss_ctor_create.argtypes = [P(_Params)]
+        L.mtg_boss_ctor_create.restype = ctypes.c_void_p
+        L.mtg_boss_ctor_destroy.argtypes = [ctypes.c_void_p]
+        L.mtg_boss_ctor_get_k.argtypes = [ctypes.c_void_p]
+        L.mtg_boss_ctor_get_k.restype = ctypes.c_uint64
+        L.mtg_boss_ctor_add_sequences.argtypes = [ctypes.c_void_p, P(ctypes.c_char_p),
+                                                  P(ctypes.c_uint64), P(ctypes.c_uint64),
+                                                  ctypes.c_size_t]
+        L.mtg_boss_ctor_add_sequence.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                                 ctypes.c_uint64, ctypes.c_uint64]
+        L.mtg_boss_ctor_add_packed.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                               P(ctypes.c_uint64), P(ctypes.c_uint64),
+                                               ctypes.c_size_t]
+        L.mtg_boss_ctor_build_chunk.argtypes = [ctypes.c_void_p, P(_Chunk)]
+        L.mtg_boss_chunk_free.argtypes = [P(_Chunk)]
+        L.mtg_boss_build_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_void_p, P(_DeviceChunk)]
+        L.mtg_boss_last_timings.argtypes = [ctypes.c_void_p, P(Timings)]
+        L.mtg_device_alloc.argtypes = [ctypes.c_int, ctypes.c_uint64]
+        L.mtg_device_alloc.restype = ctypes.c_void_p
+        L.mtg_device_free.argtypes = [ctypes.c_void_p]
+        L.mtg_memcpy_h2d.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.mtg_memcpy_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.mtg_device_count.restype = ctypes.c_int
+        L.mtg_device_synchronize.argtypes = [ctypes.c_int]
+        for name in EXPORTS:
+            getattr(L, name)
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(lib().mtg_last_error().decode() or "error %d" % rc)
+
+
+class Chunk:
+    """BOSS::Chunk (boss_chunk.hpp:19-104): W (0..9), last (0/1), F[5], weights, k."""
+
+    def __init__(self, k, W, last, F, weights=None, n_real=None, n_dummy=None):
+        self.k = k
+        self.alph_size = 5
+        self.W = W
+        self.last = last
+        self.F = F
+        self.weights = weights
+        self.n_real = n_real
+        self.n_dummy = n_dummy
+
+    def size(self):
+        return len(self.W)
+
+    def extend(self, other):
+        """BOSS::Chunk::extend (boss_chunk.cpp:230-270): append rows after index 0, sum F."""
+        if self.alph_size != other.alph_size or self.k != other.k:
+            raise RuntimeError("ERROR: trying to concatenate incompatible graph chunks")
+        if len(other.W) == 1:
+            return
+        if (self.weights is None) != (other.weights is None):
+            raise RuntimeError("ERROR: trying to concatenate weighted and unweighted blocks")
+        self.W = np.concatenate([self.W, other.W[1:]])
+        self.last = np.concatenate([self.last, other.last[1:]])
+        self.F = self.F + other.F
+        if self.weights is not None:
+            self.weights = np.concatenate([self.weights, other.weights[1:]])
+
+
+class BOSSChunkConstructor:
+    def __init__(self, handle, k, bits_per_count):
+        self._h = handle
+        self._k = k
+        self._bits = bits_per_count
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.mtg_boss_ctor_destroy(h)
+
+    def get_k(self):
+        return lib().mtg_boss_ctor_get_k(self._h)
+
+    def add_sequence(self, seq, count=1):
+        b = seq.encode() if isinstance(seq, str) else bytes(seq)
+        _check(lib().mtg_boss_ctor_add_sequence(self._h, b, len(b), count))
+
+    def add_sequences(self, seqs, counts=None):
+        """add_sequences(vector<string>&&) / add_sequences(vector<pair<string,uint64_t>>&&)."""
+        if len(seqs) and isinstance(seqs[0], tuple):
+            counts = [c for _, c in seqs]
+            seqs = [s for s, _ in seqs]
+        bs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+        if not bs:
+            return
+        offsets = np.zeros(len(bs) + 1, dtype=np.uint64)
+        offsets[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+        cnt = None if counts is None else np.ascontiguousarray(counts, dtype=np.uint64)
+        _check(lib().mtg_boss_ctor_add_packed(
+            self._h, b"".join(bs), offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None,
+            len(bs)))
+
+    def build_chunk(self):
+        c = _Chunk()
+        _check(lib().mtg_boss_ctor_build_chunk(self._h, ctypes.byref(c)))
+        n = c.n
+        W = np.ctypeslib.as_array(c.W, shape=(n,)).copy()
+        last = np.ctypeslib.as_array(c.last, shape=(n,)).copy()
+        weights = np.ctypeslib.as_array(c.weights, shape=(n,)).copy() if c.weights else None
+        F = np.array(list(c.F), dtype=np.uint64)
+        out = Chunk(c.k, W, last, F, weights, c.n_real, c.n_dummy)
+        lib().mtg_boss_chunk_free(ctypes.byref(c))
+        return out
+
+    def build_device(self, d_seq, seq_len, d_read_starts=None, d_counts=None, n_reads=0,
+                     stream=None):
+        """Whole path on a device-resident read buffer; returns the device chunk descriptor."""
+        c = _DeviceChunk()
+        _check(lib().mtg_boss_build_device(self._h, d_seq, seq_len, d_read_starts, d_counts,
+                                           n_reads, stream, ctypes.byref(c)))
+        return c
+
+    def timings(self):
+        t = Timings()
+        _check(lib().mtg_boss_last_timings(self._h, ctypes.byref(t)))
+        return t
+
+
+class IBOSSChunkConstructor:
+    @staticmethod
+    def initialize(k, both_strands=False, bits_per_count=0, filter_suffix="", num_threads=1,
+                   memory_preallocated=0, container_type=CONTAINER_VECTOR, swap_dir="/tmp/",
+                   disk_cap_bytes=int(1e9), device_id=0):
+        """IBOSSChunkConstructor::initialize (boss_chunk_construct.cpp:1134-1178).
+
+        k is the BOSS k (node length, = DBG k - 1).  Invalid k / count width raise like the
+        reference's exit(1) / runtime_error; there is no CPU fallback for other containers.
+        """
+        if k < 1 or k > 84:
+            raise ValueError("For succinct graph, k must be between 2 and 85")
+        if bits_per_count > 32:
+            raise RuntimeError("Error: trying to allocate too many bits per k-mer count")
+        p = _Params(k, int(bool(both_strands)), bits_per_count,
+                    filter_suffix.encode() if filter_suffix else None, num_threads,
+                    float(memory_preallocated), container_type,
+                    swap_dir.encode() if swap_dir else None, int(disk_cap_bytes), device_id)
+        h = lib().mtg_boss_ctor_create(ctypes.byref(p))
+        if not h:
+            raise RuntimeError(lib().mtg_last_error().decode())
+        return BOSSChunkConstructor(h, k, bits_per_count)
+
+
+class BOSSConstructor(BOSSChunkConstructor):
+    """BOSSConstructor (boss_construct.hpp:12-53): (k, canonical, bits_per_count, ...)."""
+
+    def __new__(cls, k, canonical=False, bits_per_count=0, filter_suffix="", num_threads=1,
+                memory_preallocated=0, container_type=CONTAINER_VECTOR):
+        return IBOSSChunkConstructor.initialize(k, canonical, bits_per_count, filter_suffix,
+                                                num_threads, memory_preallocated,
+                                                container_type)
+
+
+def device_count():
+    return lib().mtg_device_count()

@@ -1,0 +1,710 @@
+// boss_pipeline.hip -- host orchestration of the device BOSS construction path and the C ABI
+// declared in include/mtg_boss.h.
+//
+// Stage order follows construct_boss_chunk (boss_chunk_construct.cpp:248-356) preceded by the
+// k-mer collector (kmer_collector.cpp:26-127, sorted_set.cpp:19-48):
+//   K1 extract -> K2 sort -> K3 unique/count -> [K4 rc + sort] -> K5/K6 dummies (+ sort/unique)
+//   -> K7 lift+merge -> K8 W/last/F/weights.
+// Everything runs on one HIP stream; host syncs only to read sizes that size the next stage.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mtg_boss.h"
+#include "boss_kernels.hpp"
+#include "radix_sort.hpp"
+
+namespace mtg {
+
+static thread_local std::string g_last_error;
+
+static void set_error(const std::string &msg) { g_last_error = msg; }
+
+#define HIP_CHECK(x)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess)                                                               \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) +    \
+                                     " at " #x);                                            \
+    } while (0)
+
+// growable device buffers, reused across builds
+class Workspace {
+  public:
+    enum Slot {
+        SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
+        FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, NSLOTS
+    };
+    ~Workspace() {
+        for (auto &b : bufs_)
+            if (b.ptr) (void)hipFree(b.ptr);
+    }
+    void *get(Slot s, size_t bytes, size_t keep = 0, hipStream_t stream = nullptr) {
+        Buf &b = bufs_[s];
+        bytes = std::max<size_t>(bytes, 256);
+        if (b.cap < bytes) {
+            void *p = nullptr;
+            size_t cap = bytes + bytes / 8;
+            HIP_CHECK(hipMalloc(&p, cap));
+            if (keep && b.ptr) HIP_CHECK(hipMemcpyAsync(p, b.ptr, keep, hipMemcpyDeviceToDevice, stream));
+            if (b.ptr) {
+                if (keep) HIP_CHECK(hipStreamSynchronize(stream));
+                HIP_CHECK(hipFree(b.ptr));
+            }
+            b.ptr = p;
+            b.cap = cap;
+        }
+        return b.ptr;
+    }
+    void swap(Slot a, Slot b) { std::swap(bufs_[a], bufs_[b]); }
+
+  private:
+    struct Buf {
+        void *ptr = nullptr;
+        size_t cap = 0;
+    };
+    Buf bufs_[NSLOTS];
+};
+
+struct Small {  // one device word block, zeroed per use
+    unsigned long long total;
+    unsigned long long totals[2];
+    unsigned long long fhist[8];
+    uint32_t counter;
+    uint32_t error;
+};
+
+class EventTimer {
+  public:
+    explicit EventTimer(hipStream_t s) : s_(s) {}
+    ~EventTimer() {
+        for (auto e : evs_) (void)hipEventDestroy(e);
+    }
+    int mark() {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        HIP_CHECK(hipEventRecord(e, s_));
+        evs_.push_back(e);
+        return (int)evs_.size() - 1;
+    }
+    double ms(int a, int b) {
+        float t = 0;
+        HIP_CHECK(hipEventElapsedTime(&t, evs_[a], evs_[b]));
+        return t;
+    }
+
+  private:
+    hipStream_t s_;
+    std::vector<hipEvent_t> evs_;
+};
+
+struct Ctx {
+    Workspace ws;
+    hipStream_t stream = nullptr;
+    Small *small = nullptr;
+    mtg_boss_timings timings{};
+};
+
+static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+static void reset_small(Ctx &c) { HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream)); }
+
+static uint64_t read_u64(Ctx &c, const unsigned long long *p) {
+    unsigned long long v = 0;
+    HIP_CHECK(hipMemcpyAsync(&v, p, sizeof(v), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    return v;
+}
+
+static void check_error_word(Ctx &c) {
+    uint32_t e = 0;
+    HIP_CHECK(hipMemcpyAsync(&e, &c.small->error, sizeof(e), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    if (e) throw std::runtime_error("device look-back timed out (error word set)");
+}
+
+static uint64_t *zeroed_desc(Ctx &c, uint64_t words) {
+    uint64_t *d = (uint64_t *)c.ws.get(Workspace::DESC, words * 8);
+    HIP_CHECK(hipMemsetAsync(d, 0, words * 8, c.stream));
+    return d;
+}
+
+struct SortStats {
+    double pass_ms = 0;
+    uint64_t passes = 0;
+};
+
+// LSD radix sort of keys[0..n) (and vals) over the low nbits; result left in *keys / *vals
+// (pointers swapped with *alt / *valt as passes ping-pong).
+template <int L, bool HAS_VAL>
+static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uint32_t **valt,
+                       uint64_t n, unsigned nbits, SortStats *stats) {
+    if (n < 2) return;
+    const int passes = (int)ceil_div(nbits, 8);
+    auto *hist = (unsigned long long *)c.ws.get(Workspace::HIST, passes * 256 * 8);
+    HIP_CHECK(hipMemsetAsync(hist, 0, passes * 256 * 8, c.stream));
+    const uint64_t hgrid = std::min<uint64_t>(ceil_div(n, 256), 4096);
+    radix_histogram_kernel<L><<<dim3((unsigned)hgrid), dim3(256), 0, c.stream>>>(*keys, n, passes, hist);
+    HIP_CHECK(hipGetLastError());
+    std::vector<unsigned long long> h(passes * 256);
+    HIP_CHECK(hipMemcpyAsync(h.data(), hist, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<uint64_t> starts(passes * 256);
+    std::vector<int> active;
+    for (int p = 0; p < passes; ++p) {
+        uint64_t s = 0;
+        bool trivial = false;
+        for (int d = 0; d < 256; ++d) {
+            starts[p * 256 + d] = s;
+            s += h[p * 256 + d];
+            if (h[p * 256 + d] == n) trivial = true;
+        }
+        if (!trivial) active.push_back(p);
+    }
+    if (active.empty()) return;
+    auto *dstart = (uint64_t *)c.ws.get(Workspace::STARTS_DIGIT, passes * 256 * 8);
+    HIP_CHECK(hipMemcpyAsync(dstart, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, c.stream));
+    constexpr int TILE = SortTraits<L>::TILE;
+    const uint64_t tiles = ceil_div(n, TILE);
+    if (tiles > 0xFFFFFFFFull) throw std::runtime_error("sort too large");
+    EventTimer tm(c.stream);
+    for (int p : active) {
+        uint64_t *desc = zeroed_desc(c, tiles * 256);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        int e0 = tm.mark();
+        onesweep_kernel<L, HAS_VAL><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            *keys, *alt, HAS_VAL ? *vals : nullptr, HAS_VAL ? *valt : nullptr, n, 8u * p,
+            dstart + p * 256, desc, &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        int e1 = tm.mark();
+        (void)e0;
+        (void)e1;
+        std::swap(*keys, *alt);
+        if (HAS_VAL) std::swap(*vals, *valt);
+    }
+    if (stats) {
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        double sum = 0;
+        for (size_t i = 0; i < active.size(); ++i) sum += tm.ms(2 * i, 2 * i + 1);
+        stats->pass_ms = sum / active.size();
+        stats->passes = active.size();
+    }
+}
+
+template <int L>
+static unsigned bucket_bits(uint64_t n, unsigned keybits) {
+    unsigned b = 1;
+    while (b < 22 && (1ull << (b + 2)) < n) ++b;
+    return std::min(b, keybits);
+}
+
+struct BuildInput {
+    const uint8_t *seq;
+    uint64_t seq_len;
+    const uint64_t *read_starts;
+    const uint32_t *read_counts;
+    uint64_t n_reads;
+};
+
+struct BuildOutput {
+    uint8_t *W;
+    uint8_t *last;
+    uint32_t *weights;
+    uint64_t n;
+    uint64_t F[5];
+    uint64_t n_real;
+    uint64_t n_dummy;
+};
+
+template <int L2, int L3, bool COUNTED>
+static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
+                         const BuildInput &in, BuildOutput *out) {
+    using K2 = Key<L2>;
+    using K3 = Key<L3>;
+    const unsigned K = k + 1;
+    const unsigned cbits = bits <= 8 ? 8 : bits <= 16 ? 16 : 32;
+    const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+    const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
+    mtg_boss_timings &T = c.timings;
+    T = mtg_boss_timings{};
+    EventTimer tm(c.stream);
+    const int ev_start = tm.mark();
+
+    // ---- K1 extract
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    T.n_positions = npos;
+    K2 *ka = (K2 *)c.ws.get(Workspace::KA, npos * sizeof(K2));
+    K2 *kb = (K2 *)c.ws.get(Workspace::KB, npos * sizeof(K2));
+    uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, npos * 4) : nullptr;
+    uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, npos * 4) : nullptr;
+    uint64_t N = 0;
+    reset_small(c);
+    if (npos) {
+        constexpr int TILE = ExtractTraits<L2>::TILE;
+        const uint64_t tiles = ceil_div(npos, TILE);
+        uint64_t *desc = zeroed_desc(c, tiles);
+        extract_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts,
+            in.n_reads, cmax, ka, ca, desc, &c.small->counter, &c.small->total, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        N = read_u64(c, &c.small->total);
+    }
+    T.n_extracted = N;
+    const int ev_extract = tm.mark();
+
+    // ---- K2 sort
+    SortStats ss;
+    radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, &ss);
+    T.radix_pass_ms = ss.pass_ms;
+    T.radix_passes = ss.passes;
+    T.radix_keys = N;
+    T.radix_key_bytes = sizeof(K2) + (COUNTED ? 4 : 0);
+    const int ev_sort = tm.mark();
+
+    // ---- K3 unique / saturating count merge: ka -> kb
+    uint64_t U = 0;
+    reset_small(c);
+    if (N) {
+        const uint64_t tiles = ceil_div(N, 2048);
+        uint64_t *desc = zeroed_desc(c, tiles);
+        unsigned long long *sums = nullptr;
+        if (COUNTED) {
+            sums = (unsigned long long *)c.ws.get(Workspace::SUMS, N * 8);
+            HIP_CHECK(hipMemsetAsync(sums, 0, N * 8, c.stream));
+        }
+        unique_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            ka, ca, N, kb, sums, desc, &c.small->counter, &c.small->total, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        U = read_u64(c, &c.small->total);
+        if (COUNTED) {
+            count_clamp_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256), 4096)),
+                                 dim3(256), 0, c.stream>>>(sums, U, cmax, cb);
+            HIP_CHECK(hipGetLastError());
+        }
+    }
+    std::swap(ka, kb);
+    std::swap(ca, cb);
+    T.n_unique = U;
+    const int ev_unique = tm.mark();
+
+    // ---- K4 reverse complements (CANONICAL_ONLY) + re-sort
+    uint64_t R = U;
+    if (canonical && U) {
+        // ka holds U keys; needs room for 2U.  Buffers are the workspace's KA/KB slots in
+        // some order: find which slot ka currently is.
+        const size_t need = 2 * U;
+        // re-acquire with keep (may reallocate); keep the slot mapping in sync
+        void *pa = c.ws.get(Workspace::KA, 0);
+        Workspace::Slot sa = (pa == (void *)ka) ? Workspace::KA : Workspace::KB;
+        Workspace::Slot sb = sa == Workspace::KA ? Workspace::KB : Workspace::KA;
+        ka = (K2 *)c.ws.get(sa, need * sizeof(K2), U * sizeof(K2), c.stream);
+        kb = (K2 *)c.ws.get(sb, need * sizeof(K2));
+        if (COUNTED) {
+            void *pc = c.ws.get(Workspace::CA, 0);
+            Workspace::Slot qa = (pc == (void *)ca) ? Workspace::CA : Workspace::CB;
+            Workspace::Slot qb = qa == Workspace::CA ? Workspace::CB : Workspace::CA;
+            ca = (uint32_t *)c.ws.get(qa, need * 4, U * 4, c.stream);
+            cb = (uint32_t *)c.ws.get(qb, need * 4);
+        }
+        reset_small(c);
+        const uint64_t tiles = ceil_div(U, 1024);
+        uint64_t *desc = zeroed_desc(c, tiles);
+        rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            ka, ca, U, K, cbits, cmax, desc, &c.small->counter, &c.small->total, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        R = U + read_u64(c, &c.small->total);
+        radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, nullptr);
+    }
+    T.n_real = R;
+    const int ev_rc = tm.mark();
+
+    // ---- K5/K6 dummy sinks and sources (all levels), sort + unique
+    uint64_t D = 0;
+    K3 *dk = nullptr;
+    {
+        const unsigned B = bucket_bits<L2>(R, 2 * K);
+        const unsigned bshift = 2 * K - B;
+        const uint64_t nb = 1ull << B;
+        uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nb + 2) * 8);
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
+        bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
+        HIP_CHECK(hipGetLastError());
+        reset_small(c);
+        uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
+        if (R) {
+            dummy_flag_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(R, 256), 8192)),
+                                    dim3(256), 0, c.stream>>>(ka, R, K, bstart, bshift, flags,
+                                                              c.small->totals);
+            HIP_CHECK(hipGetLastError());
+        }
+        unsigned long long tot[2] = {0, 0};
+        HIP_CHECK(hipMemcpyAsync(tot, c.small->totals, sizeof(tot), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        const uint64_t Draw = tot[0] + tot[1] * k;
+        K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
+        K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
+        if (Draw) {
+            reset_small(c);
+            const uint64_t tiles = ceil_div(R, 1024);
+            uint64_t *desc = zeroed_desc(c, tiles);
+            dummy_write_kernel<L2, L3><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+                ka, flags, R, K, da, desc, &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            uint32_t *nv = nullptr;
+            radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, nullptr);
+            reset_small(c);
+            const uint64_t ut = ceil_div(Draw, 2048);
+            uint64_t *udesc = zeroed_desc(c, ut);
+            unique_kernel<L3, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+                da, nullptr, Draw, db, nullptr, udesc, &c.small->counter, &c.small->total,
+                &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            D = read_u64(c, &c.small->total);
+            dk = db;
+        }
+    }
+    T.n_dummy = D + 1;
+    const int ev_dummy = tm.mark();
+
+    // ---- K7 lift + merge -> stream of M = 1 + R + D lifted k-mers
+    const uint64_t M = 1 + R + D;
+    K3 *sk = (K3 *)c.ws.get(Workspace::STREAM, M * sizeof(K3));
+    uint32_t *sc = COUNTED ? (uint32_t *)c.ws.get(Workspace::SCOUNT, M * 4) : nullptr;
+    {
+        const uint64_t threads = ceil_div(R + D, 8);
+        const uint64_t g = std::max<uint64_t>(1, ceil_div(threads, 256));
+        merge_kernel<L2, L3, COUNTED><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(
+            ka, ca, R, dk, D, K, sk, sc);
+        HIP_CHECK(hipGetLastError());
+    }
+    const int ev_merge = tm.mark();
+
+    // ---- K8 W / last / F / weights
+    uint8_t *W = (uint8_t *)c.ws.get(Workspace::OW, M + 1);
+    uint8_t *last = (uint8_t *)c.ws.get(Workspace::OLAST, M + 1);
+    uint32_t *weights = COUNTED ? (uint32_t *)c.ws.get(Workspace::OWEIGHTS, (M + 1) * 4) : nullptr;
+    HIP_CHECK(hipMemsetAsync(W, 0, 1, c.stream));
+    HIP_CHECK(hipMemsetAsync(last, 0, 1, c.stream));
+    if (COUNTED) HIP_CHECK(hipMemsetAsync(weights, 0, 4, c.stream));
+    reset_small(c);
+    uint64_t rows;
+    {
+        const uint64_t tiles = ceil_div(M, 1024);
+        uint64_t *desc = zeroed_desc(c, tiles);
+        emit_kernel<L3, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            sk, sc, M, k, wmax, W, last, weights, c.small->fhist, desc, &c.small->counter,
+            &c.small->total, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        unsigned long long fh[8];
+        HIP_CHECK(hipMemcpyAsync(fh, c.small->fhist, sizeof(fh), hipMemcpyDeviceToHost, c.stream));
+        rows = read_u64(c, &c.small->total);
+        uint64_t s = 0;
+        for (int ch = 0; ch < 5; ++ch) {
+            out->F[ch] = s;
+            s += fh[ch];
+        }
+    }
+    const int ev_emit = tm.mark();
+    check_error_word(c);
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+
+    out->W = W;
+    out->last = last;
+    out->weights = weights;
+    out->n = rows + 1;
+    out->n_real = R;
+    out->n_dummy = rows - R;
+    T.n_rows = rows + 1;
+    T.extract_ms = tm.ms(ev_start, ev_extract);
+    T.sort_ms = tm.ms(ev_extract, ev_sort);
+    T.unique_ms = tm.ms(ev_sort, ev_unique);
+    T.rc_ms = tm.ms(ev_unique, ev_rc);
+    T.dummy_ms = tm.ms(ev_rc, ev_dummy);
+    T.merge_ms = tm.ms(ev_dummy, ev_merge);
+    T.emit_ms = tm.ms(ev_merge, ev_emit);
+    T.total_ms = tm.ms(ev_start, ev_emit);
+}
+
+template <int L2, int L3>
+static void run_counted(Ctx &c, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
+                        BuildOutput *out) {
+    if (bits) run_pipeline<L2, L3, true>(c, k, canonical, bits, in, out);
+    else run_pipeline<L2, L3, false>(c, k, canonical, bits, in, out);
+}
+
+// word choice as boss_chunk_construct.cpp:1068-1079 (2-bit, by (k+1)*2) and :1030-1036
+// (lifted, by (k+1)*3)
+static void run_dispatch(Ctx &c, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
+                         BuildOutput *out) {
+    const unsigned K = k + 1;
+    if (3 * K <= 64) run_counted<1, 1>(c, k, canonical, bits, in, out);
+    else if (2 * K <= 64) run_counted<1, 2>(c, k, canonical, bits, in, out);
+    else if (3 * K <= 128) run_counted<2, 2>(c, k, canonical, bits, in, out);
+    else if (2 * K <= 128) run_counted<2, 4>(c, k, canonical, bits, in, out);
+    else run_counted<4, 4>(c, k, canonical, bits, in, out);
+}
+
+}  // namespace mtg
+
+// ============================================================================ C ABI
+
+struct mtg_boss_ctor {
+    mtg_boss_params params{};
+    std::string suffix;
+    int device = 0;
+    mtg::Ctx ctx;
+    std::mutex mu;
+    std::vector<char> data;          // staged reads, each followed by a '$' separator
+    std::vector<uint64_t> starts;    // start offset of every read in `data`
+    std::vector<uint32_t> counts;    // per-read counts (clamped to u32)
+    bool any_count_not_one = false;
+};
+
+using namespace mtg;
+
+extern "C" {
+
+int mtg_boss_abi_version(void) { return MTG_BOSS_ABI_VERSION; }
+
+const char *mtg_last_error(void) { return g_last_error.c_str(); }
+
+mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
+    if (!p) {
+        set_error("null params");
+        return nullptr;
+    }
+    if (p->k < 1 || p->k > 84) {
+        set_error("For succinct graph, k must be between 2 and 85");
+        return nullptr;
+    }
+    if (p->bits_per_count > 32) {
+        set_error("Error: trying to allocate too many bits per k-mer count");
+        return nullptr;
+    }
+    if ((p->filter_suffix && p->filter_suffix[0]) || p->container_type != MTG_CONTAINER_VECTOR) {
+        set_error("only the in-memory container without a suffix filter runs on the GPU path");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= p->device_id || p->device_id < 0) {
+        set_error("no HIP device " + std::to_string(p->device_id) + " visible");
+        return nullptr;
+    }
+    auto *c = new mtg_boss_ctor();
+    c->params = *p;
+    c->device = p->device_id;
+    try {
+        HIP_CHECK(hipSetDevice(c->device));
+        HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
+        HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void mtg_boss_ctor_destroy(mtg_boss_ctor *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->ctx.stream) (void)hipStreamSynchronize(c->ctx.stream);
+    if (c->ctx.small) (void)hipFree(c->ctx.small);
+    if (c->ctx.stream) (void)hipStreamDestroy(c->ctx.stream);
+    delete c;
+}
+
+uint64_t mtg_boss_ctor_get_k(const mtg_boss_ctor *c) { return c ? c->params.k : 0; }
+
+static void stage_one(mtg_boss_ctor *c, const char *s, uint64_t len, uint64_t count) {
+    c->starts.push_back(c->data.size());
+    c->data.insert(c->data.end(), s, s + len);
+    c->data.push_back('$');
+    uint32_t cnt = count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)count;
+    c->counts.push_back(cnt);
+    if (cnt != 1) c->any_count_not_one = true;
+}
+
+int mtg_boss_ctor_add_sequences(mtg_boss_ctor *c, const char *const *seqs, const uint64_t *lens,
+                                const uint64_t *counts, size_t n) {
+    if (!c || (n && (!seqs || !lens))) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    for (size_t i = 0; i < n; ++i) stage_one(c, seqs[i], lens[i], counts ? counts[i] : 1);
+    return MTG_OK;
+}
+
+int mtg_boss_ctor_add_sequence(mtg_boss_ctor *c, const char *seq, uint64_t len, uint64_t count) {
+    if (!c || (len && !seq)) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    stage_one(c, seq, len, count);
+    return MTG_OK;
+}
+
+int mtg_boss_ctor_add_packed(mtg_boss_ctor *c, const char *data, const uint64_t *offsets,
+                             const uint64_t *counts, size_t n) {
+    if (!c || (n && (!data || !offsets))) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    for (size_t i = 0; i < n; ++i)
+        stage_one(c, data + offsets[i], offsets[i + 1] - offsets[i], counts ? counts[i] : 1);
+    return MTG_OK;
+}
+
+static int run_build(mtg_boss_ctor *c, const BuildInput &in, BuildOutput *out) {
+    try {
+        HIP_CHECK(hipSetDevice(c->device));
+        run_dispatch(c->ctx, (unsigned)c->params.k, c->params.both_strands != 0,
+                     c->params.bits_per_count, in, out);
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_DEVICE;
+    }
+}
+
+int mtg_boss_build_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_len,
+                          const uint64_t *d_read_starts, const uint32_t *d_counts,
+                          uint64_t n_reads, void *stream, mtg_boss_device_chunk *out) {
+    if (!c || !out || (seq_len && !d_seq) || (!d_read_starts != !d_counts)) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    hipStream_t saved = c->ctx.stream;
+    if (stream) c->ctx.stream = (hipStream_t)stream;
+    BuildInput in{d_seq, seq_len, d_read_starts, d_counts, d_counts ? n_reads : 0};
+    BuildOutput o{};
+    int rc = run_build(c, in, &o);
+    c->ctx.stream = saved;
+    if (rc != MTG_OK) return rc;
+    out->k = c->params.k;
+    out->n = o.n;
+    out->W = o.W;
+    out->last = o.last;
+    out->weights = o.weights;
+    std::memcpy(out->F, o.F, sizeof(o.F));
+    out->n_real = o.n_real;
+    out->n_dummy = o.n_dummy;
+    return MTG_OK;
+}
+
+int mtg_boss_ctor_build_chunk(mtg_boss_ctor *c, mtg_boss_chunk *out) {
+    if (!c || !out) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    std::memset(out, 0, sizeof(*out));
+    try {
+        HIP_CHECK(hipSetDevice(c->device));
+        hipStream_t s = c->ctx.stream;
+        const uint64_t len = c->data.size();
+        const uint64_t nr = c->starts.size();
+        uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, len + 1);
+        if (len) HIP_CHECK(hipMemcpyAsync(dseq, c->data.data(), len, hipMemcpyHostToDevice, s));
+        uint64_t *dstarts = nullptr;
+        uint32_t *dcounts = nullptr;
+        const bool per_read = c->params.bits_per_count && c->any_count_not_one && nr;
+        if (per_read) {
+            dstarts = (uint64_t *)c->ctx.ws.get(Workspace::STARTS, nr * 8);
+            dcounts = (uint32_t *)c->ctx.ws.get(Workspace::RCOUNTS, nr * 4);
+            HIP_CHECK(hipMemcpyAsync(dstarts, c->starts.data(), nr * 8, hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipMemcpyAsync(dcounts, c->counts.data(), nr * 4, hipMemcpyHostToDevice, s));
+        }
+        BuildInput in{dseq, len, dstarts, dcounts, per_read ? nr : 0};
+        BuildOutput o{};
+        run_dispatch(c->ctx, (unsigned)c->params.k, c->params.both_strands != 0,
+                     c->params.bits_per_count, in, &o);
+        out->k = c->params.k;
+        out->alph_size = 5;
+        out->n = o.n;
+        out->bits_per_count = c->params.bits_per_count;
+        out->n_real = o.n_real;
+        out->n_dummy = o.n_dummy;
+        std::memcpy(out->F, o.F, sizeof(o.F));
+        out->W = (uint8_t *)std::malloc(o.n);
+        out->last = (uint8_t *)std::malloc(o.n);
+        if (!out->W || !out->last) throw std::runtime_error("host out of memory");
+        HIP_CHECK(hipMemcpyAsync(out->W, o.W, o.n, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(out->last, o.last, o.n, hipMemcpyDeviceToHost, s));
+        if (o.weights) {
+            out->weights = (uint32_t *)std::malloc(o.n * 4);
+            if (!out->weights) throw std::runtime_error("host out of memory");
+            HIP_CHECK(hipMemcpyAsync(out->weights, o.weights, o.n * 4, hipMemcpyDeviceToHost, s));
+        }
+        HIP_CHECK(hipStreamSynchronize(s));
+        c->data.clear();
+        c->starts.clear();
+        c->counts.clear();
+        c->any_count_not_one = false;
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        mtg_boss_chunk_free(out);
+        return MTG_ERR_DEVICE;
+    }
+}
+
+void mtg_boss_chunk_free(mtg_boss_chunk *chunk) {
+    if (!chunk) return;
+    std::free(chunk->W);
+    std::free(chunk->last);
+    std::free(chunk->weights);
+    chunk->W = chunk->last = nullptr;
+    chunk->weights = nullptr;
+    chunk->n = 0;
+}
+
+int mtg_boss_last_timings(const mtg_boss_ctor *c, mtg_boss_timings *out) {
+    if (!c || !out) return MTG_ERR_ARGUMENT;
+    *out = c->ctx.timings;
+    return MTG_OK;
+}
+
+void *mtg_device_alloc(int device_id, uint64_t bytes) {
+    void *p = nullptr;
+    if (hipSetDevice(device_id) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        set_error("hipMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+int mtg_device_free(void *ptr) { return hipFree(ptr) == hipSuccess ? MTG_OK : MTG_ERR_DEVICE; }
+
+int mtg_memcpy_h2d(void *dst, const void *src, uint64_t bytes) {
+    return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
+}
+
+int mtg_memcpy_d2h(void *dst, const void *src, uint64_t bytes) {
+    return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
+}
+
+int mtg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int mtg_device_synchronize(int device_id) {
+    if (hipSetDevice(device_id) != hipSuccess) return MTG_ERR_DEVICE;
+    return hipDeviceSynchronize() == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
+}
+
+}  // extern "C"
