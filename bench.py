@@ -174,7 +174,7 @@ def main():
     # roofline of the dominant kernel: one onesweep radix pass moves every key (+payload) in
     # and out once: 2 * n * bytes per key, algorithmic
     pass_ms = sum(t["radix_pass_ms"] for t in timings) / len(timings)
-    pass_bytes = 2 * last["radix_keys"] * last["radix_key_bytes"]
+    pass_bytes = last["radix_bytes"]
     achieved = pass_bytes / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     traffic = None
     prof = os.path.join(ROOT, "profiles", "onesweep_traffic.json")
@@ -213,7 +213,7 @@ def main():
         "stages_ms": {k2: last[k2] for k2 in ("extract_ms", "sort_ms", "unique_ms", "rc_ms",
                                               "dummy_ms", "merge_ms", "emit_ms", "total_ms")},
         "counts": {k2: last[k2] for k2 in ("n_extracted", "n_unique", "n_real", "n_dummy",
-                                           "n_rows", "radix_passes")},
+                                           "n_rows", "radix_launches")},
     }
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, kb)

@@ -49,10 +49,10 @@ class _DeviceChunk(ctypes.Structure):
 class Timings(ctypes.Structure):
     _fields_ = [(name, ctypes.c_double) for name in
                 ("total_ms", "extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms",
-                 "merge_ms", "emit_ms", "radix_pass_ms")] + \
+                 "merge_ms", "emit_ms", "radix_pass_ms", "radix_bytes")] + \
                [(name, ctypes.c_uint64) for name in
-                ("radix_passes", "radix_keys", "radix_key_bytes", "n_positions", "n_extracted",
-                 "n_unique", "n_real", "n_dummy", "n_rows")]
+                ("radix_launches", "n_positions", "n_extracted", "n_unique", "n_real",
+                 "n_dummy", "n_rows")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

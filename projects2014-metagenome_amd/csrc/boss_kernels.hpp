@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void extract_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts,
     uint64_t n_reads, uint32_t cmax, Key<L> *__restrict__ out_keys,
-    uint32_t *__restrict__ out_counts, uint64_t *desc, uint32_t *tile_counter,
+    uint32_t *__restrict__ out_counts, uint64_t *desc, uint32_t epoch, uint32_t *tile_counter,
     unsigned long long *total_out, uint32_t *error) {
     using T = ExtractTraits<L>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
@@ -136,8 +136,8 @@ __global__ __launch_bounds__(256) void extract_kernel(
     }
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nvalid, s_scan, &tile_total);
+    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
     if (tid == 0) {
-        s_base = lookback(desc, tile, 1, tile_total, error);
         const uint64_t ntiles = (npos + TILE - 1) / TILE;
         if (tile + 1 == ntiles) *total_out = s_base + tile_total;
     }
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void unique_kernel(const Key<L> *__restrict__ 
                                                      const uint32_t *__restrict__ in_counts,
                                                      uint64_t n, Key<L> *__restrict__ out,
                                                      unsigned long long *__restrict__ sums,
-                                                     uint64_t *desc, uint32_t *tile_counter,
+                                                     uint64_t *desc, uint32_t epoch, uint32_t *tile_counter,
                                                      unsigned long long *total_out,
                                                      uint32_t *error) {
     constexpr int BLOCK = 256, ITEMS = 8, TILE = BLOCK * ITEMS;
@@ -202,8 +202,8 @@ __global__ __launch_bounds__(256) void unique_kernel(const Key<L> *__restrict__ 
     }
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nheads, s_scan, &tile_total);
+    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
     if (tid == 0) {
-        s_base = lookback(desc, tile, 1, tile_total, error);
         const uint64_t ntiles = (n + TILE - 1) / TILE;
         if (tile + 1 == ntiles) *total_out = s_base + tile_total;
     }
@@ -248,7 +248,7 @@ __global__ void count_clamp_kernel(const unsigned long long *__restrict__ sums, 
 template <int L, bool COUNTED>
 __global__ __launch_bounds__(256) void rc_augment_kernel(Key<L> *keys, uint32_t *counts,
                                                          uint64_t n, unsigned K, unsigned cbits,
-                                                         uint32_t cmax, uint64_t *desc,
+                                                         uint32_t cmax, uint64_t *desc, uint32_t epoch,
                                                          uint32_t *tile_counter,
                                                          unsigned long long *total_out,
                                                          uint32_t *error) {
@@ -282,8 +282,8 @@ __global__ __launch_bounds__(256) void rc_augment_kernel(Key<L> *keys, uint32_t 
     }
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(cnt, s_scan, &tile_total);
+    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
     if (tid == 0) {
-        s_base = lookback(desc, tile, 1, tile_total, error);
         const uint64_t ntiles = (n + TILE - 1) / TILE;
         if (tile + 1 == ntiles) *total_out = s_base + tile_total;
     }
@@ -412,7 +412,7 @@ __device__ __forceinline__ Key<LO> lift_fast(const Key<LI> &x, unsigned K) {
 template <int L2, int L3>
 __global__ __launch_bounds__(256) void dummy_write_kernel(
     const Key<L2> *__restrict__ keys, const uint8_t *__restrict__ flags, uint64_t n, unsigned K,
-    Key<L3> *__restrict__ out, uint64_t *desc, uint32_t *tile_counter, uint32_t *error) {
+    Key<L3> *__restrict__ out, uint64_t *desc, uint32_t epoch, uint32_t *tile_counter, uint32_t *error) {
     constexpr int BLOCK = 256, ITEMS = 4, TILE = BLOCK * ITEMS;
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
     __shared__ uint32_t s_tile;
@@ -432,8 +432,7 @@ __global__ __launch_bounds__(256) void dummy_write_kernel(
     }
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(cnt, s_scan, &tile_total);
-    if (tid == 0) s_base = lookback(desc, tile, 1, tile_total, error);
-    __syncthreads();
+    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
     uint64_t o = s_base + off;
     const Key<L2> full = Key<L2>::lowmask(2 * K);
     const Key<L3> full3 = Key<L3>::lowmask(3 * K);
@@ -522,6 +521,7 @@ __global__ __launch_bounds__(256) void emit_kernel(
     const Key<L3> *__restrict__ s, const uint32_t *__restrict__ sc, uint64_t m, unsigned k,
     uint32_t wmax, uint8_t *__restrict__ W, uint8_t *__restrict__ last,
     uint32_t *__restrict__ weights, unsigned long long *__restrict__ fhist, uint64_t *desc,
+    uint32_t epoch,
     uint32_t *tile_counter, unsigned long long *total_out, uint32_t *error) {
     constexpr int BLOCK = 256, ITEMS = 4, TILE = BLOCK * ITEMS;
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
@@ -575,8 +575,8 @@ __global__ __launch_bounds__(256) void emit_kernel(
         if (fcount[c]) atomicAdd(&s_f[c], fcount[c]);
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nkeep, s_scan, &tile_total);
+    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
     if (tid == 0) {
-        s_base = lookback(desc, tile, 1, tile_total, error);
         const uint64_t ntiles = (m + TILE - 1) / TILE;
         if (tile + 1 == ntiles) *total_out = s_base + tile_total;
     }

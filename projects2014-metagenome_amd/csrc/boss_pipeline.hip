@@ -110,6 +110,11 @@ struct Ctx {
     hipStream_t stream = nullptr;
     Small *small = nullptr;
     mtg_boss_timings timings{};
+    uint32_t epoch = 0;           // look-back granule epoch of the last launch
+    size_t desc_words = 0;        // zeroed capacity of the descriptor buffer
+    // accumulated over the onesweep launches of the real-k-mer sorts of one build
+    double radix_ms = 0, radix_bytes = 0;
+    uint64_t radix_launches = 0;
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -130,22 +135,26 @@ static void check_error_word(Ctx &c) {
     if (e) throw std::runtime_error("device look-back timed out (error word set)");
 }
 
-static uint64_t *zeroed_desc(Ctx &c, uint64_t words) {
+// Descriptor array for one look-back launch plus its epoch.  Granules of older epochs read as
+// "not ready", so the array is zeroed only when it grows or the 16-bit epoch wraps.
+static uint64_t *acquire_desc(Ctx &c, uint64_t words, uint32_t *epoch) {
     uint64_t *d = (uint64_t *)c.ws.get(Workspace::DESC, words * 8);
-    HIP_CHECK(hipMemsetAsync(d, 0, words * 8, c.stream));
+    if (words > c.desc_words || c.epoch >= 0xFFFF) {
+        size_t cap = std::max<size_t>(words, c.desc_words);
+        d = (uint64_t *)c.ws.get(Workspace::DESC, cap * 8);
+        HIP_CHECK(hipMemsetAsync(d, 0, cap * 8, c.stream));
+        c.desc_words = cap;
+        c.epoch = 0;
+    }
+    *epoch = ++c.epoch;
     return d;
 }
-
-struct SortStats {
-    double pass_ms = 0;
-    uint64_t passes = 0;
-};
 
 // LSD radix sort of keys[0..n) (and vals) over the low nbits; result left in *keys / *vals
 // (pointers swapped with *alt / *valt as passes ping-pong).
 template <int L, bool HAS_VAL>
 static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uint32_t **valt,
-                       uint64_t n, unsigned nbits, SortStats *stats) {
+                       uint64_t n, unsigned nbits, bool stats) {
     if (n < 2) return;
     const int passes = (int)ceil_div(nbits, 8);
     auto *hist = (unsigned long long *)c.ws.get(Workspace::HIST, passes * 256 * 8);
@@ -176,25 +185,23 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
     if (tiles > 0xFFFFFFFFull) throw std::runtime_error("sort too large");
     EventTimer tm(c.stream);
     for (int p : active) {
-        uint64_t *desc = zeroed_desc(c, tiles * 256);
+        uint32_t epoch;
+        uint64_t *desc = acquire_desc(c, tiles * 256, &epoch);
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-        int e0 = tm.mark();
-        onesweep_kernel<L, HAS_VAL><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+        tm.mark();
+        onesweep_kernel<L, HAS_VAL><<<dim3((unsigned)tiles), dim3(SortTraits<L>::BLOCK), 0, c.stream>>>(
             *keys, *alt, HAS_VAL ? *vals : nullptr, HAS_VAL ? *valt : nullptr, n, 8u * p,
-            dstart + p * 256, desc, &c.small->counter, &c.small->error);
+            dstart + p * 256, desc, epoch, &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
-        int e1 = tm.mark();
-        (void)e0;
-        (void)e1;
+        tm.mark();
         std::swap(*keys, *alt);
         if (HAS_VAL) std::swap(*vals, *valt);
     }
     if (stats) {
         HIP_CHECK(hipStreamSynchronize(c.stream));
-        double sum = 0;
-        for (size_t i = 0; i < active.size(); ++i) sum += tm.ms(2 * i, 2 * i + 1);
-        stats->pass_ms = sum / active.size();
-        stats->passes = active.size();
+        for (size_t i = 0; i < active.size(); ++i) c.radix_ms += tm.ms(2 * i, 2 * i + 1);
+        c.radix_launches += active.size();
+        c.radix_bytes += (double)active.size() * 2.0 * n * (sizeof(Key<L>) + (HAS_VAL ? 4 : 0));
     }
 }
 
@@ -249,10 +256,11 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     if (npos) {
         constexpr int TILE = ExtractTraits<L2>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
-        uint64_t *desc = zeroed_desc(c, tiles);
+        uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
         extract_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
             in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts,
-            in.n_reads, cmax, ka, ca, desc, &c.small->counter, &c.small->total, &c.small->error);
+            in.n_reads, cmax, ka, ca, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
         HIP_CHECK(hipGetLastError());
         N = read_u64(c, &c.small->total);
     }
@@ -260,12 +268,10 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     const int ev_extract = tm.mark();
 
     // ---- K2 sort
-    SortStats ss;
-    radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, &ss);
-    T.radix_pass_ms = ss.pass_ms;
-    T.radix_passes = ss.passes;
-    T.radix_keys = N;
-    T.radix_key_bytes = sizeof(K2) + (COUNTED ? 4 : 0);
+    c.radix_ms = 0;
+    c.radix_bytes = 0;
+    c.radix_launches = 0;
+    radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, true);
     const int ev_sort = tm.mark();
 
     // ---- K3 unique / saturating count merge: ka -> kb
@@ -273,14 +279,15 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     reset_small(c);
     if (N) {
         const uint64_t tiles = ceil_div(N, 2048);
-        uint64_t *desc = zeroed_desc(c, tiles);
+        uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
         unsigned long long *sums = nullptr;
         if (COUNTED) {
             sums = (unsigned long long *)c.ws.get(Workspace::SUMS, N * 8);
             HIP_CHECK(hipMemsetAsync(sums, 0, N * 8, c.stream));
         }
         unique_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            ka, ca, N, kb, sums, desc, &c.small->counter, &c.small->total, &c.small->error);
+            ka, ca, N, kb, sums, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
         HIP_CHECK(hipGetLastError());
         U = read_u64(c, &c.small->total);
         if (COUNTED) {
@@ -315,12 +322,13 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         }
         reset_small(c);
         const uint64_t tiles = ceil_div(U, 1024);
-        uint64_t *desc = zeroed_desc(c, tiles);
+        uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
         rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            ka, ca, U, K, cbits, cmax, desc, &c.small->counter, &c.small->total, &c.small->error);
+            ka, ca, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
         HIP_CHECK(hipGetLastError());
         R = U + read_u64(c, &c.small->total);
-        radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, nullptr);
+        radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, true);
     }
     T.n_real = R;
     const int ev_rc = tm.mark();
@@ -353,17 +361,19 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         if (Draw) {
             reset_small(c);
             const uint64_t tiles = ceil_div(R, 1024);
-            uint64_t *desc = zeroed_desc(c, tiles);
+            uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
             dummy_write_kernel<L2, L3><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-                ka, flags, R, K, da, desc, &c.small->counter, &c.small->error);
+                ka, flags, R, K, da, desc, desc_ep, &c.small->counter, &c.small->error);
             HIP_CHECK(hipGetLastError());
             uint32_t *nv = nullptr;
-            radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, nullptr);
+            radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
             reset_small(c);
             const uint64_t ut = ceil_div(Draw, 2048);
-            uint64_t *udesc = zeroed_desc(c, ut);
+            uint32_t udesc_ep;
+        uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
             unique_kernel<L3, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
-                da, nullptr, Draw, db, nullptr, udesc, &c.small->counter, &c.small->total,
+                da, nullptr, Draw, db, nullptr, udesc, desc_ep, &c.small->counter, &c.small->total,
                 &c.small->error);
             HIP_CHECK(hipGetLastError());
             D = read_u64(c, &c.small->total);
@@ -397,9 +407,10 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     uint64_t rows;
     {
         const uint64_t tiles = ceil_div(M, 1024);
-        uint64_t *desc = zeroed_desc(c, tiles);
+        uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
         emit_kernel<L3, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            sk, sc, M, k, wmax, W, last, weights, c.small->fhist, desc, &c.small->counter,
+            sk, sc, M, k, wmax, W, last, weights, c.small->fhist, desc, desc_ep, &c.small->counter,
             &c.small->total, &c.small->error);
         HIP_CHECK(hipGetLastError());
         unsigned long long fh[8];
@@ -430,6 +441,9 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     T.merge_ms = tm.ms(ev_dummy, ev_merge);
     T.emit_ms = tm.ms(ev_merge, ev_emit);
     T.total_ms = tm.ms(ev_start, ev_emit);
+    T.radix_launches = c.radix_launches;
+    T.radix_pass_ms = c.radix_launches ? c.radix_ms / c.radix_launches : 0;
+    T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
 }
 
 template <int L2, int L3>

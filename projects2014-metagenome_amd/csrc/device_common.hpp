@@ -1,11 +1,18 @@
 // device_common.hpp -- wave64 / workgroup primitives and the decoupled look-back protocol
 // shared by the sort, scan and compaction kernels.
 //
-// Inter-workgroup hand-off: every tile publishes 64-bit granules {status:2 | value:62} with a
-// single agent-scope relaxed atomic store; readers poll them with agent-scope relaxed atomic
-// loads.  The data IS the flag (8-byte granule, R2 of the CDNA4 guide), so no fences are
-// needed; the descriptor arrays are zeroed by hipMemsetAsync before every launch and spins are
-// bounded (a timeout sets an error word the host checks).
+// Inter-workgroup hand-off: every tile publishes 64-bit granules
+//     {epoch:16 | status:2 | value:46}
+// with one agent-scope relaxed atomic store; readers poll them with agent-scope relaxed atomic
+// loads.  The data IS the flag (8-byte granule, R2 of the CDNA4 guide), so no fences are needed.
+// The epoch is the launch's id: a granule from an older launch reads as "not ready", so the
+// descriptor array needs zeroing only when it is (re)allocated or the 16-bit epoch wraps.
+//
+// Why windows: on MI355X a tile's predecessors run on other XCDs, so every poll is a fabric
+// round trip (~0.5-2 us).  Walking back one tile per round trip serialises the chain; both
+// look-backs below inspect many predecessors per round trip (64 lanes of a wave for a single
+// column, LB_WINDOW loads in flight per lane for the per-digit columns of the radix sort).
+// Spins are bounded: a timeout sets an error word the host checks.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -15,11 +22,23 @@ namespace mtg {
 
 constexpr int kWave = 64;
 
-constexpr uint64_t kStatusShift = 62;
-constexpr uint64_t kStatusAgg = 1ull << kStatusShift;
-constexpr uint64_t kStatusIncl = 2ull << kStatusShift;
+constexpr int kEpochShift = 48;
+constexpr int kStatusShift = 46;
 constexpr uint64_t kValueMask = (1ull << kStatusShift) - 1;
-constexpr uint32_t kSpinLimit = 1u << 26;
+constexpr uint64_t kAgg = 1;
+constexpr uint64_t kIncl = 2;
+constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr int LB_WINDOW = 4;
+
+__device__ __forceinline__ uint64_t granule(uint32_t epoch, uint64_t status, uint64_t value) {
+    return ((uint64_t)epoch << kEpochShift) | (status << kStatusShift) | value;
+}
+
+// status of a granule for this launch: 0 = not ready (or stale epoch), 1 = aggregate,
+// 2 = inclusive prefix
+__device__ __forceinline__ uint32_t granule_status(uint64_t v, uint32_t epoch) {
+    return (uint32_t)(v >> kEpochShift) == epoch ? (uint32_t)((v >> kStatusShift) & 3) : 0u;
+}
 
 __device__ __forceinline__ void publish(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -30,38 +49,97 @@ __device__ __forceinline__ uint64_t poll(const uint64_t *p) {
                              __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Exclusive prefix of `agg` over all tiles < tile, via decoupled look-back on desc[tile*stride].
-// Called by ONE lane per (tile, column).  Publishes the inclusive prefix for its successors.
-__device__ __forceinline__ uint64_t lookback(uint64_t *desc, uint32_t tile, uint32_t stride,
-                                             uint64_t agg, uint32_t *error) {
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+/*
+ * Single-column look-back by ONE whole wave: returns the exclusive prefix of `agg` over all
+ * tiles < tile (same value in every lane) and publishes this tile's inclusive prefix.
+ * Lane i inspects tile (base - i), so each round trip covers 64 predecessors.
+ */
+__device__ __forceinline__ uint64_t wave_lookback(uint64_t *desc, uint32_t tile, uint64_t agg,
+                                                  uint32_t epoch, uint32_t *error) {
+    const uint32_t lane = __lane_id();
     if (tile == 0) {
-        publish(desc, kStatusIncl | agg);
+        if (lane == 0) publish(desc, granule(epoch, kIncl, agg));
         return 0;
     }
-    publish(desc + (size_t)tile * stride, kStatusAgg | agg);
+    if (lane == 0) publish(desc + tile, granule(epoch, kAgg, agg));
     uint64_t excl = 0;
-    int64_t t = (int64_t)tile - 1;
+    int64_t base = (int64_t)tile - 1;
     uint32_t spins = 0;
-    while (t >= 0) {
-        uint64_t v = poll(desc + (size_t)t * stride);
-        uint64_t st = v >> kStatusShift;
-        if (st == 0) {
+    while (true) {
+        const int64_t t = base - (int64_t)lane;
+        const uint64_t v = t >= 0 ? poll(desc + t) : granule(epoch, kIncl, 0);
+        const uint32_t st = granule_status(v, epoch);
+        const uint64_t incl = __ballot(st == 2);
+        const uint64_t notready = __ballot(st == 0);
+        const uint32_t first = incl ? (uint32_t)(__ffsll((unsigned long long)incl) - 1) : 64u;
+        const uint64_t upto = first < 63 ? ((2ull << first) - 1) : ~0ull;
+        if (notready & upto) {
             if (++spins > kSpinLimit) {
-                atomicOr(error, 1u);
+                if (lane == 0) atomicOr(error, 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        excl += v & kValueMask;
-        if (st == 2) break;
-        --t;
+        excl += wave_sum_u64(lane <= first ? (v & kValueMask) : 0);
+        if (first < 64) break;
+        base -= 64;
     }
-    publish(desc + (size_t)tile * stride, kStatusIncl | (excl + agg));
+    if (lane == 0) publish(desc + tile, granule(epoch, kIncl, excl + agg));
     return excl;
 }
 
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+/*
+ * Per-column look-back (one lane per column, e.g. per radix digit): desc[tile * stride].
+ * Each lane keeps LB_WINDOW predecessor loads in flight per round trip.
+ */
+__device__ __forceinline__ uint64_t column_lookback(uint64_t *desc, uint32_t tile, uint32_t stride,
+                                                    uint64_t agg, uint32_t epoch,
+                                                    uint32_t *error) {
+    if (tile == 0) {
+        publish(desc, granule(epoch, kIncl, agg));
+        return 0;
+    }
+    publish(desc + (size_t)tile * stride, granule(epoch, kAgg, agg));
+    uint64_t excl = 0;
+    int64_t t = (int64_t)tile - 1;
+    uint32_t spins = 0;
+    bool done = false;
+    while (!done) {
+        uint64_t v[LB_WINDOW];
+#pragma unroll
+        for (int i = 0; i < LB_WINDOW; ++i)
+            v[i] = t - i >= 0 ? poll(desc + (size_t)(t - i) * stride) : granule(epoch, kIncl, 0);
+        bool stalled = false;
+#pragma unroll
+        for (int i = 0; i < LB_WINDOW; ++i) {
+            if (done || stalled) continue;
+            const uint32_t st = granule_status(v[i], epoch);
+            if (st == 0) {
+                stalled = true;
+                continue;
+            }
+            excl += v[i] & kValueMask;
+            --t;
+            if (st == 2) done = true;
+        }
+        if (stalled && !done) {
+            if (++spins > kSpinLimit) {
+                atomicOr(error, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    publish(desc + (size_t)tile * stride, granule(epoch, kIncl, excl + agg));
+    return excl;
+}
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
     uint32_t lane = __lane_id();
@@ -80,7 +158,7 @@ __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
 }
 
 // Exclusive block scan of one 32-bit value per thread; returns exclusive prefix and total.
-// `scratch` must hold blockDim.x / 64 + 1 words.  Contains __syncthreads().
+// `scratch` must hold BLOCK / 64 + 1 words.  Contains __syncthreads().
 template <int BLOCK>
 __device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t *scratch,
                                                         uint32_t *total) {
@@ -104,6 +182,25 @@ __device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t *sc
     *total = scratch[NW];
     __syncthreads();
     return res;
+}
+
+// Tile prologue shared by the single-column compaction kernels: dynamic tile id (so every
+// predecessor is already resident) and, after the block's count is known, the wave-0
+// look-back.  `s_tile` / `s_base` are LDS words.
+__device__ __forceinline__ uint32_t take_tile(uint32_t *tile_counter, uint32_t *s_tile) {
+    if (threadIdx.x == 0) *s_tile = atomicAdd(tile_counter, 1u);
+    __syncthreads();
+    return *s_tile;
+}
+
+__device__ __forceinline__ void tile_base_lookback(uint64_t *desc, uint32_t tile, uint32_t count,
+                                                   uint32_t epoch, uint32_t *error,
+                                                   uint64_t *s_base) {
+    if (threadIdx.x < 64) {
+        const uint64_t b = wave_lookback(desc, tile, count, epoch, error);
+        if (threadIdx.x == 0) *s_base = b;
+    }
+    __syncthreads();
 }
 
 }  // namespace mtg

@@ -22,7 +22,7 @@ namespace mtg {
 template <int L>
 struct SortTraits {
     static constexpr int ITEMS = L == 1 ? 16 : L == 2 ? 8 : 4;
-    static constexpr int BLOCK = 256;
+    static constexpr int BLOCK = 512;
     static constexpr int TILE = ITEMS * BLOCK;
 };
 
@@ -43,14 +43,17 @@ __global__ __launch_bounds__(256) void radix_histogram_kernel(const Key<L> *__re
         if (s_hist[i]) atomicAdd(&hist[i], (unsigned long long)s_hist[i]);
 }
 
-template <int L, bool HAS_VAL>
-__global__ __launch_bounds__(256) void onesweep_kernel(
+// ABL (timing ablations for tools/sort_bench only; 0 in the product): bit 0 = replace the
+// look-back by an atomic per-digit cursor, bit 1 = write the tile back in place (no
+// scatter), bit 2 = skip the wave ranking
+template <int L, bool HAS_VAL, int ABL = 0>
+__global__ __launch_bounds__(512) void onesweep_kernel(
     const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ vout, uint64_t n, unsigned shift,
-    const uint64_t *__restrict__ digit_start, uint64_t *desc, uint32_t *tile_counter,
-    uint32_t *error) {
+    const uint64_t *__restrict__ digit_start, uint64_t *desc, uint32_t epoch,
+    uint32_t *tile_counter, uint32_t *error) {
     constexpr int ITEMS = SortTraits<L>::ITEMS;
-    constexpr int BLOCK = 256;
+    constexpr int BLOCK = SortTraits<L>::BLOCK;
     constexpr int NW = BLOCK / 64;
     constexpr int TILE = ITEMS * BLOCK;
     constexpr int WT = ITEMS * 64;
@@ -94,6 +97,10 @@ __global__ __launch_bounds__(256) void onesweep_kernel(
     for (int j = 0; j < ITEMS; ++j) {
         const bool valid = wbase + (uint64_t)j * 64 + lane < n;
         const uint32_t d = bits_at(k[j], shift, 8);
+        if (ABL & 4) {
+            rank[j] = j * 64 + lane;
+            continue;
+        }
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -112,24 +119,26 @@ __global__ __launch_bounds__(256) void onesweep_kernel(
     }
     __syncthreads();
 
-    // per digit: exclusive prefix over waves, tile total, tile-local digit offsets
-    uint32_t total;
-    {
-        const uint32_t d = tid;
+    // per digit (threads 0..255): exclusive prefix over waves, tile total, tile-local digit
+    // offsets, and the per-digit look-back for the global offset
+    uint32_t total = 0;
+    if (tid < 256) {
         uint32_t s = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
-            uint32_t c = s_whist[w * 256 + d];
-            s_whist[w * 256 + d] = s;
+            uint32_t c = s_whist[w * 256 + tid];
+            s_whist[w * 256 + tid] = s;
             s += c;
         }
         total = s;
     }
     uint32_t tile_total;
     const uint32_t loff = block_exclusive_sum<BLOCK>(total, s_scan, &tile_total);
-    s_loff[tid] = loff;
-    {
-        const uint64_t excl = lookback(desc + tid, tile, 256, total, error);
+    if (tid < 256) {
+        s_loff[tid] = loff;
+        const uint64_t excl = (ABL & 1) ? atomicAdd((unsigned long long *)desc + tid,
+                                                    (unsigned long long)total)
+                                        : column_lookback(desc + tid, tile, 256, total, epoch, error);
         s_gbase[tid] = digit_start[tid] + excl;
     }
     __syncthreads();
@@ -138,7 +147,8 @@ __global__ __launch_bounds__(256) void onesweep_kernel(
     for (int j = 0; j < ITEMS; ++j) {
         if (wbase + (uint64_t)j * 64 + lane < n) {
             const uint32_t d = bits_at(k[j], shift, 8);
-            const uint32_t pos = s_loff[d] + s_whist[wid * 256 + d] + rank[j];
+            uint32_t pos = s_loff[d] + s_whist[wid * 256 + d] + rank[j];
+            if (ABL & 4) pos = wid * WT + j * 64 + lane;
             s_keys[pos] = k[j];
             if (HAS_VAL) s_vals[pos] = v[j];
         }
@@ -149,7 +159,9 @@ __global__ __launch_bounds__(256) void onesweep_kernel(
     for (uint32_t p = tid; p < tile_n; p += BLOCK) {
         const Key<L> key = s_keys[p];
         const uint32_t d = bits_at(key, shift, 8);
-        const uint64_t o = s_gbase[d] + (p - s_loff[d]);
+        uint64_t o = s_gbase[d] + (p - s_loff[d]);
+        if (ABL & 2) o = base + p;
+        if (ABL & 5) o = o % n;
         kout[o] = key;
         if (HAS_VAL) vout[o] = s_vals[p];
     }
