@@ -19,6 +19,7 @@
 
 #include "../../include/mtg_boss.h"
 #include "boss_kernels.hpp"
+#include "msd_sort.hpp"
 #include "radix_sort.hpp"
 
 namespace mtg {
@@ -40,7 +41,8 @@ class Workspace {
   public:
     enum Slot {
         SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
-        FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, NSLOTS
+        FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, MSD_COUNTS, MSD_BSTART,
+        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -115,6 +117,9 @@ struct Ctx {
     // accumulated over the onesweep launches of the real-k-mer sorts of one build
     double radix_ms = 0, radix_bytes = 0;
     uint64_t radix_launches = 0;
+    bool track_partition = false;  // time the msd_partition launches of the real-k-mer sorts
+    bool use_lsd = false;          // MTG_SORT=lsd: LSD onesweep + unique instead of MSD
+    bool debug = false;            // MTG_DEBUG=1: host-side checks between stages
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -180,6 +185,7 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
     if (active.empty()) return;
     auto *dstart = (uint64_t *)c.ws.get(Workspace::STARTS_DIGIT, passes * 256 * 8);
     HIP_CHECK(hipMemcpyAsync(dstart, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // `starts` is a local: the copy must land first
     constexpr int TILE = SortTraits<L>::TILE;
     const uint64_t tiles = ceil_div(n, TILE);
     if (tiles > 0xFFFFFFFFull) throw std::runtime_error("sort too large");
@@ -202,6 +208,179 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
         for (size_t i = 0; i < active.size(); ++i) c.radix_ms += tm.ms(2 * i, 2 * i + 1);
         c.radix_launches += active.size();
         c.radix_bytes += (double)active.size() * 2.0 * n * (sizeof(Key<L>) + (HAS_VAL ? 4 : 0));
+    }
+}
+
+__global__ void set_pair_kernel(uint64_t *p, uint64_t a, uint64_t b) {
+    p[0] = a;
+    p[1] = b;
+}
+
+// Sort + unique (+ saturating count merge) of keys[0..n) over their low nbits by MSD
+// partitioning and per-group LDS hashing (msd_sort.hpp).  `dup` is the expected number of
+// copies per distinct key, used only to plan the partition depth; a wrong guess costs time,
+// never correctness (overflowing groups take another level or the LSD fallback).
+// Result: sorted distinct keys in *keys (counts in *vals); returns their number.
+template <int L, bool COUNTED>
+static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
+                                uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
+                                double dup) {
+    if (n == 0) return 0;
+    constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
+    constexpr int TILE = MsdTraits<L>::TILE;
+    const uint64_t tiles = ceil_div(n, TILE);
+    // levels: until an average bucket holds ~LIMIT/2 distinct keys
+    unsigned levels = 0;
+    while (levels < 3 && 8 * levels < nbits &&
+           (double)n / dup / (double)(1ull << (8 * levels)) > (double)LIMIT)
+        ++levels;
+    unsigned b = 0;
+    uint64_t *bstart = nullptr;
+    uint64_t nbuckets = 1;
+    auto run_level = [&](unsigned lev) {
+        const unsigned bb = std::min(nbits, 8 * lev), bp = std::min(nbits, 8 * (lev - 1));
+        nbuckets = 1ull << bb;
+        uint32_t *cnt = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nbuckets * 4);
+        HIP_CHECK(hipMemsetAsync(cnt, 0, nbuckets * 4, c.stream));
+        msd_hist_kernel<L><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, cnt);
+        HIP_CHECK(hipGetLastError());
+        bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nbuckets + 1) * 8);
+        uint32_t ep;
+        const uint64_t st = ceil_div(nbuckets, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(cnt, nbuckets, bstart, desc, ep,
+                                                                      &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        auto *cur = (unsigned long long *)c.ws.get(Workspace::MSD_CURSOR, nbuckets * 8);
+        HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
+        EventTimer tm(c.stream);
+        tm.mark();
+        msd_partition_kernel<L, COUNTED><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
+        HIP_CHECK(hipGetLastError());
+        tm.mark();
+        if (c.track_partition) {
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            c.radix_ms += tm.ms(0, 1);
+            c.radix_launches += 1;
+            c.radix_bytes += 2.0 * n * (sizeof(Key<L>) + (COUNTED ? 4 : 0));
+        }
+        std::swap(*keys, *alt);
+        if (COUNTED) std::swap(*vals, *valt);
+        b = bb;
+    };
+    for (unsigned lev = 1; lev <= levels; ++lev) run_level(lev);
+
+    while (true) {
+        // groups of consecutive buckets holding <= LIMIT keys (bigger buckets stand alone)
+        const uint64_t G = LIMIT / 2;
+        const uint64_t ng = ceil_div(n, G);
+        uint64_t *gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, (ng + 1) * 8);
+        if (b == 0) {
+            set_pair_kernel<<<1, 1, 0, c.stream>>>(gstart, 0, n);
+            HIP_CHECK(hipGetLastError());
+        }
+        const uint64_t ngroups = b == 0 ? 1 : ng;
+        if (b) {
+            group_bounds_kernel<<<dim3((unsigned)ceil_div(ngroups + 1, 256)), dim3(256), 0, c.stream>>>(
+                bstart, nbuckets, G, ngroups, n, gstart);
+            HIP_CHECK(hipGetLastError());
+        }
+        uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (ngroups + 1) * 4);
+        uint32_t *ovf = (uint32_t *)c.ws.get(Workspace::MSD_OVF, ngroups * 4);
+        HIP_CHECK(hipMemsetAsync(ovf, 0, ngroups * 4, c.stream));
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        auto launch_local = [&](const uint32_t *glist, uint64_t count, unsigned sbits) {
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            if (L == 1 && nbits < 64)
+                local_unique_kernel<L, COUNTED, true><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
+                    *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt,
+                    COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax);
+            else
+                local_unique_kernel<L, COUNTED, false><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
+                    *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt,
+                    COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax);
+            HIP_CHECK(hipGetLastError());
+            uint32_t nov = 0;
+            HIP_CHECK(hipMemcpyAsync(&nov, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            return nov;
+        };
+        uint32_t novf = launch_local(nullptr, ngroups, 0);
+        // overflowing one-bucket groups: rerun them alone in 2, 4, 8, 16 key-range slices
+        std::vector<uint32_t> flags;
+        std::vector<uint64_t> gs;
+        for (unsigned sbits = 1; novf && b && sbits <= 4 && b + sbits <= nbits; ++sbits) {
+            flags.resize(ngroups);
+            HIP_CHECK(hipMemcpyAsync(flags.data(), ovf, ngroups * 4, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            std::vector<uint32_t> list;
+            for (uint64_t g = 0; g < ngroups; ++g)
+                if (flags[g]) list.push_back((uint32_t)g);
+            uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
+            HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
+            novf = launch_local(dlist, list.size(), sbits);  // syncs: `list` outlives the copy
+        }
+        if (novf) {
+            flags.resize(ngroups);
+            gs.resize(ngroups + 1);
+            HIP_CHECK(hipMemcpyAsync(flags.data(), ovf, ngroups * 4, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipMemcpyAsync(gs.data(), gstart, (ngroups + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            uint64_t ovf_keys = 0;
+            for (uint64_t g = 0; g < ngroups; ++g)
+                if (flags[g]) ovf_keys += gs[g + 1] - gs[g];
+            if (ovf_keys * 20 > n && levels < 3 && 8 * levels < nbits) {
+                run_level(++levels);  // many overflows: one more level for everything
+                continue;
+            }
+            // the rest: LSD radix sort + unique of each group in place
+            for (uint64_t g = 0; g < ngroups; ++g) {
+                if (!flags[g]) continue;
+                const uint64_t g0 = gs[g], m = gs[g + 1] - gs[g];
+                Key<L> *fk = (Key<L> *)c.ws.get(Workspace::FB_K, m * sizeof(Key<L>));
+                uint32_t *fv = COUNTED ? (uint32_t *)c.ws.get(Workspace::FB_V, m * 4) : nullptr;
+                Key<L> *ka = *keys + g0, *kb = fk;
+                uint32_t *va = COUNTED ? *vals + g0 : nullptr, *vb = fv;
+                radix_sort<L, COUNTED>(c, &ka, &kb, &va, &vb, m, nbits, false);
+                reset_small(c);
+                const uint64_t ut = ceil_div(m, 2048);
+                uint32_t ep;
+                uint64_t *desc = acquire_desc(c, ut, &ep);
+                unsigned long long *sums = nullptr;
+                if (COUNTED) {
+                    sums = (unsigned long long *)c.ws.get(Workspace::SUMS, m * 8);
+                    HIP_CHECK(hipMemsetAsync(sums, 0, m * 8, c.stream));
+                }
+                unique_kernel<L, COUNTED><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+                    ka, va, m, *alt + g0, sums, desc, ep, &c.small->counter, &c.small->total, &c.small->error);
+                HIP_CHECK(hipGetLastError());
+                const uint64_t u = read_u64(c, &c.small->total);
+                if (COUNTED)
+                    count_clamp_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(u, 256), 4096))),
+                                         dim3(256), 0, c.stream>>>(sums, u, cmax, *valt + g0);
+                const uint32_t u32 = (uint32_t)u;
+                HIP_CHECK(hipMemcpyAsync(ucount + g, &u32, 4, hipMemcpyHostToDevice, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));
+            }
+        }
+        // pack: ustart = exclusive scan of ucount, gather tmp (= *alt) -> *keys
+        uint64_t *ustart = (uint64_t *)c.ws.get(Workspace::MSD_USTART, (ngroups + 1) * 8);
+        uint32_t ep;
+        const uint64_t st = ceil_div(ngroups, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(ucount, ngroups, ustart, desc, ep,
+                                                                      &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        group_gather_kernel<L, COUNTED><<<dim3((unsigned)ngroups), dim3(256), 0, c.stream>>>(
+            *alt, COUNTED ? *valt : nullptr, gstart, ustart, *keys, COUNTED ? *vals : nullptr);
+        HIP_CHECK(hipGetLastError());
+        uint64_t u = 0;
+        HIP_CHECK(hipMemcpyAsync(&u, ustart + ngroups, 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        return u;
     }
 }
 
@@ -229,6 +408,21 @@ struct BuildOutput {
     uint64_t n_real;
     uint64_t n_dummy;
 };
+
+// MTG_DEBUG=1: host-side check that a device key array is strictly increasing
+template <int L>
+static void debug_check_sorted(Ctx &c, const char *what, const Key<L> *d, uint64_t n) {
+    if (!c.debug || n == 0) return;
+    std::vector<Key<L>> h(n);
+    HIP_CHECK(hipMemcpyAsync(h.data(), d, n * sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    uint64_t bad = 0;
+    for (uint64_t i = 1; i < n; ++i) bad += !(h[i - 1] < h[i]);
+    fprintf(stderr, "[mtg debug] %s: n=%lu, %lu order violations; first keys:", what,
+            (unsigned long)n, (unsigned long)bad);
+    for (uint64_t i = 0; i < std::min<uint64_t>(n, 8); ++i) fprintf(stderr, " %lx", (unsigned long)h[i].w[0]);
+    fprintf(stderr, "\n");
+}
 
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
@@ -267,38 +461,45 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     T.n_extracted = N;
     const int ev_extract = tm.mark();
 
-    // ---- K2 sort
+    // ---- K2 sort + K3 unique / saturating count merge (ka)
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
-    radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, true);
-    const int ev_sort = tm.mark();
-
-    // ---- K3 unique / saturating count merge: ka -> kb
     uint64_t U = 0;
-    reset_small(c);
-    if (N) {
-        const uint64_t tiles = ceil_div(N, 2048);
-        uint32_t desc_ep;
-        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
-        unsigned long long *sums = nullptr;
-        if (COUNTED) {
-            sums = (unsigned long long *)c.ws.get(Workspace::SUMS, N * 8);
-            HIP_CHECK(hipMemsetAsync(sums, 0, N * 8, c.stream));
-        }
-        unique_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            ka, ca, N, kb, sums, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
-        HIP_CHECK(hipGetLastError());
-        U = read_u64(c, &c.small->total);
-        if (COUNTED) {
-            count_clamp_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256), 4096)),
-                                 dim3(256), 0, c.stream>>>(sums, U, cmax, cb);
+    int ev_sort;
+    if (c.use_lsd) {
+        radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, true);
+        ev_sort = tm.mark();
+        reset_small(c);
+        if (N) {
+            const uint64_t tiles = ceil_div(N, 2048);
+            uint32_t desc_ep;
+            uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
+            unsigned long long *sums = nullptr;
+            if (COUNTED) {
+                sums = (unsigned long long *)c.ws.get(Workspace::SUMS, N * 8);
+                HIP_CHECK(hipMemsetAsync(sums, 0, N * 8, c.stream));
+            }
+            unique_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+                ka, ca, N, kb, sums, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
             HIP_CHECK(hipGetLastError());
+            U = read_u64(c, &c.small->total);
+            if (COUNTED) {
+                count_clamp_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(U, 256), 4096))),
+                                     dim3(256), 0, c.stream>>>(sums, U, cmax, cb);
+                HIP_CHECK(hipGetLastError());
+            }
         }
+        std::swap(ka, kb);
+        std::swap(ca, cb);
+    } else {
+        c.track_partition = true;
+        U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, 8.0);
+        c.track_partition = false;
+        ev_sort = tm.mark();
     }
-    std::swap(ka, kb);
-    std::swap(ca, cb);
     T.n_unique = U;
+    debug_check_sorted(c, "collected k-mers", ka, U);
     const int ev_unique = tm.mark();
 
     // ---- K4 reverse complements (CANONICAL_ONLY) + re-sort
@@ -328,9 +529,16 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
             ka, ca, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
         HIP_CHECK(hipGetLastError());
         R = U + read_u64(c, &c.small->total);
-        radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, true);
+        if (c.use_lsd) {
+            radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, true);
+        } else {
+            c.track_partition = true;
+            R = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, cmax, 1.0);
+            c.track_partition = false;
+        }
     }
     T.n_real = R;
+    debug_check_sorted(c, "real k-mers", ka, R);
     const int ev_rc = tm.mark();
 
     // ---- K5/K6 dummy sinks and sources (all levels), sort + unique
@@ -367,20 +575,26 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
                 ka, flags, R, K, da, desc, desc_ep, &c.small->counter, &c.small->error);
             HIP_CHECK(hipGetLastError());
             uint32_t *nv = nullptr;
-            radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
-            reset_small(c);
-            const uint64_t ut = ceil_div(Draw, 2048);
-            uint32_t udesc_ep;
-        uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
-            unique_kernel<L3, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
-                da, nullptr, Draw, db, nullptr, udesc, desc_ep, &c.small->counter, &c.small->total,
-                &c.small->error);
-            HIP_CHECK(hipGetLastError());
-            D = read_u64(c, &c.small->total);
+            if (c.use_lsd) {
+                radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
+                reset_small(c);
+                const uint64_t ut = ceil_div(Draw, 2048);
+                uint32_t udesc_ep;
+                uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
+                unique_kernel<L3, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+                    da, nullptr, Draw, db, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total,
+                    &c.small->error);
+                HIP_CHECK(hipGetLastError());
+                D = read_u64(c, &c.small->total);
+            } else {
+                D = msd_sort_unique<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, 0, 2.0);
+                std::swap(da, db);
+            }
             dk = db;
         }
     }
     T.n_dummy = D + 1;
+    debug_check_sorted(c, "dummy k-mers", dk, D);
     const int ev_dummy = tm.mark();
 
     // ---- K7 lift + merge -> stream of M = 1 + R + D lifted k-mers
@@ -394,6 +608,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
             ka, ca, R, dk, D, K, sk, sc);
         HIP_CHECK(hipGetLastError());
     }
+    debug_check_sorted(c, "merged stream", sk, M);
     const int ev_merge = tm.mark();
 
     // ---- K8 W / last / F / weights
@@ -518,6 +733,9 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
+        const char *sortenv = getenv("MTG_SORT");
+        c->ctx.use_lsd = sortenv && std::string(sortenv) == "lsd";
+        c->ctx.debug = getenv("MTG_DEBUG") != nullptr;
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;

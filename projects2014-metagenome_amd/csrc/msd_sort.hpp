@@ -1,0 +1,453 @@
+// msd_sort.hpp -- sort + unique (+ saturating count merge) of k-mer words by MSD partitioning
+// and per-group LDS hashing.  Replaces ips4o::parallel::sort + std::unique
+// (sorted_set.cpp:41-48) and the sort + saturating merge of sorted_multiset.cpp:54-84.
+//
+// Why not LSD: every LSD pass re-reads and re-writes all N keys (8 passes for 62-bit keys)
+// before duplicates can be removed.  Here:
+//   level l = 1..L : partition by the top 8l significant bits, given that keys are already
+//                    grouped by the top 8(l-1) bits (msd_hist_kernel + scan + msd_partition).
+//                    Order inside a bucket does not matter, so a tile reserves its bucket runs
+//                    with one atomic per (tile, bucket): no look-back chain.
+//   local          : consecutive buckets form groups of <= G keys; one workgroup per group
+//                    hashes its keys into LDS (duplicates collapse, counts add), sorts the
+//                    distinct keys with a bitonic network and writes them; a scan + gather
+//                    packs the groups.  A group with more distinct keys than the table holds
+//                    is flagged and finished by the LSD fallback (radix_sort.hpp).
+// The final array is globally sorted because groups are contiguous key ranges in order.
+#pragma once
+
+#include "device_common.hpp"
+#include "keys.hpp"
+
+namespace mtg {
+
+constexpr int MSD_BLOCK = 512;
+constexpr int MSD_WIN = 2;  // previous-level segments a tile keeps in its LDS window
+
+template <int L>
+struct MsdTraits {
+    static constexpr int ITEMS = L == 1 ? 16 : L == 2 ? 8 : 4;
+    static constexpr int TILE = ITEMS * MSD_BLOCK;
+};
+
+// top `bits` of the nbits-bit significant range of a key, as an integer (bits <= 32)
+template <int L>
+__device__ __forceinline__ uint32_t key_prefix(const Key<L> &k, unsigned nbits, unsigned bits) {
+    return bits ? bits_at(k, nbits - bits, bits) : 0u;
+}
+
+/*
+ * Histogram of bucket = top `b` bits over all keys (keys grouped by their top `bp` bits).
+ * Counts go to an LDS window of MSD_WIN previous-level segments starting at the tile's first
+ * key; keys beyond the window add to global memory directly.
+ */
+template <int L>
+__global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__restrict__ keys,
+                                                             uint64_t n, unsigned nbits,
+                                                             unsigned b, unsigned bp,
+                                                             uint32_t *__restrict__ counts) {
+    constexpr int TILE = MsdTraits<L>::TILE;
+    constexpr int WMAX = MSD_WIN * 256;
+    __shared__ uint32_t s_cnt[WMAX];
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const unsigned sub = b - bp;
+    const uint32_t wsize = MSD_WIN << sub;
+    for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
+    const uint32_t wbase = key_prefix(keys[base], nbits, bp) << sub;
+    __syncthreads();
+    const uint64_t end = min(n, base + TILE);
+    for (uint64_t i = base + threadIdx.x; i < end; i += MSD_BLOCK) {
+        const uint32_t bucket = key_prefix(keys[i], nbits, b);
+        const uint32_t lb = bucket - wbase;
+        if (lb < wsize) atomicAdd(&s_cnt[lb], 1u);
+        else atomicAdd(&counts[bucket], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK)
+        if (s_cnt[i]) atomicAdd(&counts[wbase + i], s_cnt[i]);
+}
+
+/*
+ * Exclusive scan of u32 counts into u64 starts (starts[n] = total), chained by a wave
+ * look-back over tiles of 4096 entries.
+ */
+__global__ __launch_bounds__(512) void scan_counts_kernel(const uint32_t *__restrict__ counts,
+                                                          uint64_t n, uint64_t *__restrict__ starts,
+                                                          uint64_t *desc, uint32_t epoch,
+                                                          uint32_t *tile_counter, uint32_t *error) {
+    constexpr int ITEMS = 8, TILE = 512 * ITEMS;
+    __shared__ uint32_t s_scan[512 / 64 + 1];
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_base;
+    const uint32_t tile = take_tile(tile_counter, &s_tile);
+    const uint64_t i0 = (uint64_t)tile * TILE + (uint64_t)threadIdx.x * ITEMS;
+    uint32_t v[ITEMS];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        v[j] = i0 + j < n ? counts[i0 + j] : 0;
+        sum += v[j];
+    }
+    uint32_t tile_total;
+    const uint32_t off = block_exclusive_sum<512>(sum, s_scan, &tile_total);
+    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
+    uint64_t s = s_base + off;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        if (i0 + j < n) starts[i0 + j] = s;
+        s += v[j];
+    }
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    if (tile + 1 == ntiles && threadIdx.x == 511) starts[n] = s_base + tile_total;
+}
+
+/*
+ * Partition by bucket = top `b` bits.  cursor[bucket] starts at the bucket's first slot and
+ * is advanced by one atomic per (tile, bucket) run; the tile is reordered by bucket in LDS
+ * and each run is written contiguously.  Keys outside the tile's LDS window (tiles spanning
+ * more than MSD_WIN tiny segments) take one atomic each.
+ */
+template <int L, bool HAS_VAL>
+__global__ __launch_bounds__(MSD_BLOCK) void msd_partition_kernel(
+    const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
+    uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
+    unsigned long long *__restrict__ cursor) {
+    constexpr int ITEMS = MsdTraits<L>::ITEMS;
+    constexpr int TILE = MsdTraits<L>::TILE;
+    constexpr int WMAX = MSD_WIN * 256;
+    __shared__ Key<L> s_keys[TILE];
+    __shared__ uint32_t s_vals[HAS_VAL ? TILE : 1];
+    __shared__ uint32_t s_cnt[WMAX];
+    __shared__ uint32_t s_loff[WMAX];
+    __shared__ unsigned long long s_gbase[WMAX];
+    __shared__ uint32_t s_scan[MSD_BLOCK / 64 + 1];
+
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const unsigned sub = b - bp;
+    const uint32_t wsize = MSD_WIN << sub;
+    for (int i = tid; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
+    const uint32_t wbase = key_prefix(kin[base], nbits, bp) << sub;
+    __syncthreads();
+
+    Key<L> k[ITEMS];
+    uint32_t v[ITEMS];
+    uint32_t r[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * MSD_BLOCK + tid;
+        r[j] = 0xFFFFFFFFu;
+        if (i < n) {
+            k[j] = kin[i];
+            if (HAS_VAL) v[j] = vin[i];
+            const uint32_t lb = key_prefix(k[j], nbits, b) - wbase;
+            if (lb < wsize) {
+                r[j] = atomicAdd(&s_cnt[lb], 1u);
+            } else {  // outside the window: reserve and write directly
+                const unsigned long long o = atomicAdd(&cursor[lb + wbase], 1ull);
+                kout[o] = k[j];
+                if (HAS_VAL) vout[o] = v[j];
+            }
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the window counts (wsize <= 1024: two per thread)
+    constexpr int PER = WMAX / MSD_BLOCK;
+    uint32_t c[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        c[q] = i < wsize ? s_cnt[i] : 0;
+        sum += c[q];
+    }
+    uint32_t total;
+    uint32_t off = block_exclusive_sum<MSD_BLOCK>(sum, s_scan, &total);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < wsize) {
+            s_loff[i] = off;
+            s_gbase[i] = c[q] ? atomicAdd(&cursor[wbase + i], (unsigned long long)c[q]) : 0;
+        }
+        off += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        if (r[j] != 0xFFFFFFFFu) {
+            const uint32_t lb = key_prefix(k[j], nbits, b) - wbase;
+            const uint32_t pos = s_loff[lb] + r[j];
+            s_keys[pos] = k[j];
+            if (HAS_VAL) s_vals[pos] = v[j];
+        }
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < total; p += MSD_BLOCK) {
+        const Key<L> key = s_keys[p];
+        const uint32_t lb = key_prefix(key, nbits, b) - wbase;
+        const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
+        kout[o] = key;
+        if (HAS_VAL) vout[o] = s_vals[p];
+    }
+}
+
+// group g starts at the first bucket whose start is >= g * G (buckets never split)
+__global__ void group_bounds_kernel(const uint64_t *__restrict__ bstart, uint64_t nbuckets,
+                                    uint64_t G, uint64_t ngroups, uint64_t n,
+                                    uint64_t *__restrict__ gstart) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g > ngroups) return;
+    if (g == ngroups) {
+        gstart[g] = n;
+        return;
+    }
+    const uint64_t target = g * G;
+    uint64_t lo = 0, hi = nbuckets + 1;  // bstart has nbuckets + 1 entries
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (bstart[mid] < target) lo = mid + 1; else hi = mid;
+    }
+    gstart[g] = lo <= nbuckets ? bstart[lo] : n;
+}
+
+template <int L>
+struct LocalTraits {
+    // hash slots per group: keys (+ state) (+ u32 counts) within the LDS budget
+    static constexpr int SLOTS = L == 1 ? 8192 : L == 2 ? 4096 : 2048;
+    static constexpr uint32_t LIMIT = SLOTS / 2;  // distinct keys per group (load <= 1/2)
+};
+
+template <int L>
+__device__ __forceinline__ uint32_t key_hash(const Key<L> &k) {
+    uint64_t h = k.w[0] * 0x9E3779B97F4A7C15ull;
+#pragma unroll
+    for (int i = 1; i < L; ++i) h ^= (k.w[i] + (h << 6) + (h >> 2)) * 0xC2B2AE3D27D4EB4Full;
+    return (uint32_t)(h >> 32);
+}
+
+// index of the highest set bit of a key (-1 for zero)
+template <int L>
+__device__ __forceinline__ int key_msb(const Key<L> &k) {
+    int r = -1;
+#pragma unroll
+    for (int i = 0; i < L; ++i)
+        if (k.w[i]) r = 64 * i + 63 - __clzll((long long)k.w[i]);
+    return r;
+}
+
+/*
+ * One workgroup per group [gstart[g], gstart[g+1]):
+ *   1. LDS open-addressing hash of the group's keys.  KEYCAS: the key word itself is CASed
+ *      against an EMPTY sentinel no key can take (top bit of a 64-bit word whose significant
+ *      range is narrower); otherwise a per-slot state word is claimed (0 -> 1), the key stored
+ *      and the state published (-> 2).  Counts add with saturation (sorted_multiset.cpp:66-83).
+ *   2. The D distinct keys are compacted; min/max give the highest bit in which they differ;
+ *      a counting sort on the 8 bits below it splits them into 256 ordered sub-buckets; each
+ *      key's final slot is its sub-bucket start + the number of smaller keys in its sub-bucket.
+ *   3. Keys (and counts) go to tmp[gstart[g] + slot]; ucount[g] = D.
+ * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
+ */
+template <int L, bool COUNTED, bool KEYCAS>
+__global__ __launch_bounds__(512) void local_unique_kernel(
+    const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
+    const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
+    unsigned b, unsigned sbits, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
+    uint32_t *__restrict__ ucount, uint32_t *__restrict__ overflow, uint32_t *__restrict__ novf,
+    uint32_t cmax) {
+    constexpr int SLOTS = LocalTraits<L>::SLOTS;
+    constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
+    constexpr uint64_t EMPTY = ~0ull;
+    __shared__ Key<L> s_key[SLOTS];
+    __shared__ uint32_t s_state[KEYCAS ? 1 : SLOTS];
+    __shared__ uint32_t s_sum[COUNTED ? SLOTS : 1];
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_fill[256];
+    __shared__ uint32_t s_distinct;
+    __shared__ uint32_t s_scan[512 / 64 + 1];
+    __shared__ int s_hb;
+
+    const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
+    const uint64_t g0 = gstart[g], g1 = gstart[g + 1];
+    const uint32_t tid = threadIdx.x;
+    if (g0 >= g1) {
+        if (tid == 0) ucount[g] = 0;
+        return;
+    }
+    // slices: keys split by the sbits bits right below the b-bit bucket prefix; only valid for
+    // a group made of one bucket (several buckets would interleave)
+    const unsigned sshift = nbits - b - sbits;
+    if (sbits && key_prefix(keys[g0], nbits, b) != key_prefix(keys[g1 - 1], nbits, b)) {
+        if (tid == 0) {
+            overflow[g] = 1;
+            atomicAdd(novf, 1u);
+        }
+        return;
+    }
+    uint64_t out_off = 0;
+    for (uint32_t slice = 0; slice < (1u << sbits); ++slice) {
+        for (int i = tid; i < SLOTS; i += 512) {
+            if (KEYCAS) s_key[i].w[0] = EMPTY;
+            else s_state[i] = 0;
+            if (COUNTED) s_sum[i] = 0;
+        }
+        if (tid < 256) {
+            s_hist[tid] = 0;
+            s_fill[tid] = 0;
+        }
+        if (tid == 0) {
+            s_distinct = 0;
+            s_hb = -1;
+        }
+        __syncthreads();
+
+        bool ovf = false;
+        for (uint64_t i = g0 + tid; i < g1 && !ovf; i += 512) {
+            const Key<L> key = keys[i];
+            if (sbits && bits_at(key, sshift, sbits) != slice) continue;
+            uint32_t h = key_hash(key) & (SLOTS - 1);
+            for (uint32_t probes = 0;;) {
+                if (KEYCAS) {
+                    const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
+                                                   (unsigned long long)EMPTY,
+                                                   (unsigned long long)key.w[0]);
+                    if (old == EMPTY) {
+                        if (atomicAdd(&s_distinct, 1u) >= LIMIT) ovf = true;
+                        break;
+                    }
+                    if (old == key.w[0]) break;
+                } else {
+                    const uint32_t st = atomicCAS(&s_state[h], 0u, 1u);
+                    if (st == 0) {
+                        s_key[h] = key;
+                        __atomic_store_n(&s_state[h], 2u, __ATOMIC_RELEASE);
+                        if (atomicAdd(&s_distinct, 1u) >= LIMIT) ovf = true;
+                        break;
+                    }
+                    if (st != 2 && __atomic_load_n(&s_state[h], __ATOMIC_ACQUIRE) != 2) continue;
+                    if (s_key[h] == key) break;
+                }
+                h = (h + 1) & (SLOTS - 1);
+                if (++probes >= SLOTS) {
+                    ovf = true;
+                    break;
+                }
+            }
+            if (COUNTED && !ovf) {
+                const uint32_t add = vals[i];
+                uint32_t old = s_sum[h], assumed;
+                do {
+                    assumed = old;
+                    const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
+                    old = atomicCAS(&s_sum[h], assumed, nv);
+                } while (old != assumed);
+            }
+        }
+        if (__syncthreads_or(ovf) || s_distinct > LIMIT) {
+            if (tid == 0) {
+                overflow[g] = 1;
+                ucount[g] = 0;
+                atomicAdd(novf, 1u);
+            }
+            return;
+        }
+        const uint32_t D = s_distinct;
+
+        // compact occupied slots to s_key[0..D) / s_sum[0..D)
+        constexpr int PER = SLOTS / 512;
+        Key<L> kk[PER];
+        uint32_t ss[PER];
+        uint32_t mine = 0, occ = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int slot = tid * PER + q;
+            kk[q] = s_key[slot];
+            if (COUNTED) ss[q] = s_sum[slot];
+            const bool o = KEYCAS ? kk[q].w[0] != EMPTY : s_state[slot] == 2;
+            occ |= (uint32_t)o << q;
+            mine += o;
+        }
+        uint32_t tot;
+        uint32_t o = block_exclusive_sum<512>(mine, s_scan, &tot);
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            if (occ & (1u << q)) {
+                s_key[o] = kk[q];
+                if (COUNTED) s_sum[o] = ss[q];
+                ++o;
+            }
+        }
+        __syncthreads();
+        // highest bit in which the slice's keys differ = max over keys of msb(key ^ s_key[0])
+        if (D) {
+            const Key<L> ref = s_key[0];
+            int hb_local = -1;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                if (occ & (1u << q)) {
+                    Key<L> dx;
+#pragma unroll
+                    for (int i = 0; i < L; ++i) dx.w[i] = kk[q].w[i] ^ ref.w[i];
+                    hb_local = max(hb_local, key_msb(dx));
+                }
+            }
+            if (hb_local >= 0) atomicMax(&s_hb, hb_local);
+        }
+        __syncthreads();
+        const int hb = s_hb;
+        const unsigned dshift = hb >= 7 ? (unsigned)(hb - 7) : 0u;
+        Key<L> *scratch = s_key + LIMIT;  // free half of the table
+        uint32_t *sscr = COUNTED ? s_sum + LIMIT : nullptr;
+        for (uint32_t i = tid; i < D; i += 512) atomicAdd(&s_hist[bits_at(s_key[i], dshift, 8)], 1u);
+        __syncthreads();
+        if (tid < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
+            const uint32_t c0 = s_hist[4 * tid], c1 = s_hist[4 * tid + 1], c2 = s_hist[4 * tid + 2],
+                           c3 = s_hist[4 * tid + 3];
+            const uint32_t sum4 = c0 + c1 + c2 + c3;
+            const uint32_t bb = wave_inclusive_sum(sum4) - sum4;
+            s_hist[4 * tid] = bb;
+            s_hist[4 * tid + 1] = bb + c0;
+            s_hist[4 * tid + 2] = bb + c0 + c1;
+            s_hist[4 * tid + 3] = bb + c0 + c1 + c2;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < D; i += 512) {
+            const uint32_t d = bits_at(s_key[i], dshift, 8);
+            const uint32_t p = s_hist[d] + atomicAdd(&s_fill[d], 1u);
+            scratch[p] = s_key[i];
+            if (COUNTED) sscr[p] = s_sum[i];
+        }
+        __syncthreads();
+        for (uint32_t p = tid; p < D; p += 512) {
+            const Key<L> key = scratch[p];
+            const uint32_t d = bits_at(key, dshift, 8);
+            const uint32_t b0 = s_hist[d], b1 = b0 + s_fill[d];
+            uint32_t rank = 0;
+            for (uint32_t j = b0; j < b1; ++j) rank += scratch[j] < key;
+            tmp[g0 + out_off + b0 + rank] = key;
+            if (COUNTED) tcnt[g0 + out_off + b0 + rank] = sscr[p];
+        }
+        out_off += D;
+        __syncthreads();  // the next slice reuses the table
+    }
+    if (tid == 0) {
+        ucount[g] = (uint32_t)out_off;
+        overflow[g] = 0;
+    }
+}
+
+// copy every group's distinct keys from tmp[gstart[g]..] to out[ustart[g]..]
+template <int L, bool COUNTED>
+__global__ __launch_bounds__(256) void group_gather_kernel(
+    const Key<L> *__restrict__ tmp, const uint32_t *__restrict__ tcnt,
+    const uint64_t *__restrict__ gstart, const uint64_t *__restrict__ ustart,
+    Key<L> *__restrict__ out, uint32_t *__restrict__ ocnt) {
+    const uint64_t g = blockIdx.x;
+    const uint64_t src = gstart[g], dst = ustart[g], m = ustart[g + 1] - dst;
+    for (uint64_t i = threadIdx.x; i < m; i += 256) {
+        out[dst + i] = tmp[src + i];
+        if (COUNTED) ocnt[dst + i] = tcnt[src + i];
+    }
+}
+
+}  // namespace mtg

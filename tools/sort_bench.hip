@@ -24,6 +24,21 @@ __global__ void fill_kernel(Key<1> *k, uint64_t n, uint64_t seed) {
     }
 }
 
+// keys[i] = keys[hash(i) % (n / dupf)]: every distinct key about dupf times, shuffled
+__global__ void dup_kernel(Key<1> *k, uint64_t n, int dupf) {
+    const uint64_t m = n / dupf;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = i * 0xD6E8FEB86659FD93ull;
+        z ^= z >> 32;
+        uint64_t j = z % m;
+        uint64_t y = (j + 7) * 0x9E3779B97F4A7C15ull;
+        y = (y ^ (y >> 30)) * 0xBF58476D1CE4E5B9ull;
+        y = (y ^ (y >> 27)) * 0x94D049BB133111EBull;
+        k[i].w[0] = (y ^ (y >> 31)) >> 2;
+    }
+}
+
 template <int ITEMS>
 __global__ __launch_bounds__(512) void copy_kernel(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, uint64_t n) {
@@ -91,6 +106,36 @@ int main(int argc, char **argv) {
         for (size_t i = 1; i < h.size(); ++i) ok &= h[i - 1] <= h[i];
         printf("         sorted prefix ok=%d\n", ok);
         if (ka != a) std::swap(a, b);
+    }
+
+    // MSD sort + unique on keys with `dupf` copies of each distinct key (shuffled)
+    for (int dupf : {1, 8}) {
+        for (int rep = 0; rep < 2; ++rep) {
+            fill_kernel<<<4096, 256, 0, c.stream>>>(a, n, 100 + rep);
+            if (dupf > 1) dup_kernel<<<4096, 256, 0, c.stream>>>(a, n, dupf);
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            Key<1> *ka = a, *kb = b;
+            uint32_t *nv = nullptr;
+            c.radix_ms = 0;
+            c.radix_launches = 0;
+            c.radix_bytes = 0;
+            c.track_partition = true;
+            double t0 = now_ms();
+            uint64_t u = msd_sort_unique<1, false>(c, &ka, &kb, &nv, &nv, n, 62, 0, dupf);
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            double t1 = now_ms();
+            c.track_partition = false;
+            printf("msd dup=%d: total %.3f ms, unique %lu, %lu partition passes avg %.3f ms = %.0f GB/s\n",
+                   dupf, t1 - t0, (unsigned long)u, (unsigned long)c.radix_launches,
+                   c.radix_ms / std::max<uint64_t>(1, c.radix_launches),
+                   c.radix_launches ? c.radix_bytes / c.radix_ms / 1e6 : 0.0);
+            std::vector<uint64_t> h(1 << 20);
+            HIP_CHECK(hipMemcpy(h.data(), ka, h.size() * 8, hipMemcpyDeviceToHost));
+            bool ok = true;
+            for (size_t i = 1; i < h.size(); ++i) ok &= h[i - 1] < h[i];
+            printf("         strictly increasing prefix ok=%d\n", ok);
+            if (ka != a) std::swap(a, b);
+        }
     }
 
     // ablations of one pass (shift 0): timing only, outputs are not a sort
