@@ -242,11 +242,14 @@ __global__ void count_clamp_kernel(const unsigned long long *__restrict__ sums, 
 
 /*
  * K4: rc_augment.  Replaces add_reverse_complements (boss_chunk_construct.cpp:179-222):
- * appends rc(x) for every non-palindromic x behind the array (compacted in order) and doubles
- * a palindrome's count with saturation (c >> (bits-1) ? max : 2c).  The caller re-sorts.
+ * writes rc(x) for every non-palindromic x to rc_out (compacted in order) and doubles a
+ * palindrome's count with saturation (c >> (bits-1) ? max : 2c).  The caller sorts rc_out
+ * and merges it with the (sorted) canonical array instead of re-sorting both.
  */
 template <int L, bool COUNTED>
 __global__ __launch_bounds__(256) void rc_augment_kernel(Key<L> *keys, uint32_t *counts,
+                                                         Key<L> *__restrict__ rc_out,
+                                                         uint32_t *__restrict__ rc_counts,
                                                          uint64_t n, unsigned K, unsigned cbits,
                                                          uint32_t cmax, uint64_t *desc, uint32_t epoch,
                                                          uint32_t *tile_counter,
@@ -288,12 +291,12 @@ __global__ __launch_bounds__(256) void rc_augment_kernel(Key<L> *keys, uint32_t 
         if (tile + 1 == ntiles) *total_out = s_base + tile_total;
     }
     __syncthreads();
-    uint64_t o = n + s_base + off;
+    uint64_t o = s_base + off;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         if (mask & (1u << j)) {
-            keys[o] = r[j];
-            if (COUNTED) counts[o] = c[j];
+            rc_out[o] = r[j];
+            if (COUNTED) rc_counts[o] = c[j];
             ++o;
         }
     }
@@ -389,6 +392,174 @@ __global__ __launch_bounds__(256) void dummy_flag_kernel(const Key<L> *__restric
     }
 }
 
+// first index with keys[i] > hi (hi within the 2K-bit key range, or all-ones)
+template <int L>
+__device__ __forceinline__ uint64_t upper_bucketed(const Key<L> *__restrict__ keys, uint64_t n,
+                                                   const uint64_t *__restrict__ start,
+                                                   unsigned shift, uint64_t nbuckets,
+                                                   const Key<L> &hi, unsigned K) {
+    if (hi == Key<L>::lowmask(2 * K)) return n;
+    const Key<L> h1 = hi + Key<L>::from(1);
+    if (bits_at(shr(h1, shift), 0, 32) >= nbuckets) return n;
+    return lower_bound_bucketed(keys, start, shift, h1);
+}
+
+template <int L>
+struct DummyTraits {
+    static constexpr int TILE = L == 1 ? 2048 : L == 2 ? 1024 : 512;
+    static constexpr int CAP = 2 * TILE;
+    static constexpr int PER = TILE / 256;
+};
+
+/*
+ * K5 + K6 flag pass, tiled (same predicates as dummy_flag_kernel below).  A workgroup takes
+ * TILE consecutive real edges.  Per probe class -- sink probes of label c = 0..3 and the source
+ * probes -- the probes of the tile are monotone, so every real edge they can hit lies in one
+ * contiguous key range: two bucketed searches find it, it is staged in LDS and the probes are
+ * resolved there.  A range larger than CAP (or source probes of a tile that straddles a change
+ * of the last node char) falls back to per-probe bucketed searches.
+ */
+template <int L>
+__global__ __launch_bounds__(256) void dummy_flag_tiled_kernel(
+    const Key<L> *__restrict__ keys, uint64_t n, unsigned K, const uint64_t *__restrict__ start,
+    unsigned bshift, uint64_t nbuckets, uint8_t *__restrict__ flags,
+    unsigned long long *totals) {
+    using T = DummyTraits<L>;
+    __shared__ Key<L> s_x[T::TILE];
+    __shared__ Key<L> s_r[T::CAP];
+    __shared__ uint64_t s_a, s_cnt;
+    __shared__ unsigned long long s_tot[2];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * T::TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)T::TILE, n - base);
+    if (tid < 2) s_tot[tid] = 0;
+    for (uint32_t j = tid; j < tn; j += 256) s_x[j] = keys[base + j];
+    __syncthreads();
+    const Key<L> full = Key<L>::lowmask(2 * K);
+    const Key<L> x_first = s_x[0], x_last = s_x[tn - 1];
+    const unsigned k = K - 1;
+    uint8_t f[T::PER];
+    Key<L> probe[T::PER];
+#pragma unroll
+    for (int q = 0; q < T::PER; ++q) f[q] = 0;
+
+    // classes 0..3: sink probes of label c over the whole tile; classes 4..7: source probes of
+    // one quarter of the tile each (their key range is ~4x wider than the edges' range)
+    constexpr uint32_t QT = T::TILE / 4;
+    for (int cls = 0; cls < 8; ++cls) {
+        const uint32_t sub = cls < 4 ? 0 : cls - 4;
+        const uint32_t q0 = sub * QT, q1 = min(tn, q0 + QT);
+        if (cls >= 4 && q0 >= tn) break;
+        // this class's probes and the key range they can hit
+        bool mine[T::PER];
+#pragma unroll
+        for (int q = 0; q < T::PER; ++q) {
+            const uint32_t j = tid + 256 * q;
+            mine[q] = false;
+            if (j >= tn) continue;
+            if (cls >= 4 && (j < q0 || j >= q1)) continue;
+            const Key<L> x = s_x[j];
+            if (cls < 4) {
+                if ((uint32_t)(x.w[0] & 3) != (uint32_t)cls) continue;
+                // to_next(x, K, 0): node a_2..a_K, label 0 (kmer_boss.hpp:147-169)
+                probe[q] = (shr(x, 2) | shl(Key<L>::from(x.w[0] & 3), 2 * (K - 1))) & ~Key<L>::from(3);
+                mine[q] = true;
+            } else {
+                const bool first = base + j == 0 ||
+                                   shr(j ? s_x[j - 1] : keys[base - 1], 2) != shr(x, 2);
+                if (!first) continue;
+                // to_prev(x, K, 0): node 0 a_1..a_{k-1}, label a_k (kmer_boss.hpp:171-186)
+                probe[q] = (shl(x & ~Key<L>::from(3), 2) & full) | shr(x, 2 * (K - 1));
+                mine[q] = true;
+            }
+        }
+        if (tid == 0) {
+            Key<L> lo, hi;
+            bool ok = true;
+            if (cls < 4) {
+                const Key<L> c = shl(Key<L>::from(cls), 2 * (K - 1));
+                lo = (shr(x_first, 2) | c) & ~Key<L>::from(3);
+                hi = shr(x_last, 2) | c | Key<L>::from(3);
+            } else {
+                const Key<L> xf = s_x[q0], xl = s_x[q1 - 1];
+                ok = char_at(xf, k, 2) == char_at(xl, k, 2);
+                const Key<L> pf = (shl(xf & ~Key<L>::from(3), 2) & full) | shr(xf, 2 * (K - 1));
+                const Key<L> pl = (shl(xl & ~Key<L>::from(3), 2) & full) | shr(xl, 2 * (K - 1));
+                lo = pf & ~Key<L>::from(15);
+                hi = pl | Key<L>::from(15);
+            }
+            uint64_t a = 0, b = 0;
+            if (ok) {
+                a = lower_bound_bucketed(keys, start, bshift, lo);
+                b = upper_bucketed(keys, n, start, bshift, nbuckets, hi, K);
+            }
+            s_a = a;
+            s_cnt = ok && b - a <= (uint64_t)T::CAP ? b - a : ~0ull;
+        }
+        __syncthreads();
+        const uint64_t a = s_a, cnt = s_cnt;
+        if (cnt != ~0ull)
+            for (uint32_t j = tid; j < cnt; j += 256) s_r[j] = keys[a + j];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < T::PER; ++q) {
+            if (!mine[q]) continue;
+            const Key<L> p = probe[q];
+            if (cls < 4) {
+                bool found;
+                if (cnt != ~0ull) {
+                    uint32_t lo = 0, hi = (uint32_t)cnt;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_r[mid] < p) lo = mid + 1; else hi = mid;
+                    }
+                    found = lo < cnt && shr(s_r[lo], 2) == shr(p, 2);
+                } else {
+                    const uint64_t j = lower_bound_bucketed(keys, start, bshift, p);
+                    found = j < n && shr(keys[j], 2) == shr(p, 2);
+                }
+                if (!found) f[q] |= 1;
+            } else {
+                const Key<L> lo4 = p & ~Key<L>::from(15);
+                const uint32_t label = (uint32_t)(p.w[0] & 3);
+                bool redundant = false;
+                if (cnt != ~0ull) {
+                    uint32_t lo = 0, hi = (uint32_t)cnt;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_r[mid] < lo4) lo = mid + 1; else hi = mid;
+                    }
+                    for (uint32_t j = lo; j < cnt && shr(s_r[j], 4) == shr(p, 4); ++j)
+                        if ((uint32_t)(s_r[j].w[0] & 3) == label) { redundant = true; break; }
+                } else {
+                    for (uint64_t j = lower_bound_bucketed(keys, start, bshift, lo4);
+                         j < n && shr(keys[j], 4) == shr(p, 4); ++j)
+                        if ((uint32_t)(keys[j].w[0] & 3) == label) { redundant = true; break; }
+                }
+                if (!redundant) f[q] |= 2;
+            }
+        }
+        __syncthreads();
+    }
+    unsigned long long ns = 0, nsrc = 0;
+#pragma unroll
+    for (int q = 0; q < T::PER; ++q) {
+        const uint32_t j = tid + 256 * q;
+        if (j < tn) {
+            flags[base + j] = f[q];
+            ns += f[q] & 1;
+            nsrc += f[q] >> 1;
+        }
+    }
+    atomicAdd(&s_tot[0], ns);
+    atomicAdd(&s_tot[1], nsrc);
+    __syncthreads();
+    if (tid == 0) {
+        atomicAdd(&totals[0], s_tot[0]);
+        atomicAdd(&totals[1], s_tot[1]);
+    }
+}
+
 // byte of four 2-bit chars -> four 3-bit chars, each + 1 ($ACGT lift, kmer_transform.hpp:102-165)
 __device__ __forceinline__ uint64_t lift_byte(uint32_t b) {
     return ((b & 3u) | ((b & 0xCu) << 1) | ((b & 0x30u) << 2) | ((b & 0xC0u) << 3)) + 0x249u;
@@ -460,49 +631,109 @@ __global__ __launch_bounds__(256) void dummy_write_kernel(
 }
 
 /*
- * K7: lift + merge (boss_chunk_construct.cpp:308-348).  Output row 0 is the main dummy
- * KMER(0); rows 1.. merge lift(real) (+ its count) with the sorted dummies (count 0).
- * Merge path: every thread finds its diagonal split by binary search and merges ITEMS outputs.
+ * Merge path over two sorted arrays, tiled: A (LA-limb keys, lifted to LO limbs on the fly when
+ * LIFT -- kmer_transform.hpp:75-100 + get_sentinel_delta) and B (LO-limb keys); equal keys do
+ * not occur (real vs dummy k-mers, canonical vs non-canonical).  Output index off + i.
+ * Used for K7 (boss_chunk_construct.cpp:308-348: lift(real) merged with the sorted dummies
+ * behind the main dummy row, dummies carrying count 0) and for the reverse-complement merge.
+ * A workgroup owns TILE consecutive outputs: one diagonal search per tile boundary, the two
+ * input runs staged in LDS (A lifted once), per-thread merge of ITEMS outputs out of LDS, and a
+ * coalesced store from an LDS output image.
  */
-template <int L2, int L3, bool COUNTED>
-__global__ __launch_bounds__(256) void merge_kernel(const Key<L2> *__restrict__ a,
-                                                    const uint32_t *__restrict__ ac, uint64_t na,
-                                                    const Key<L3> *__restrict__ b, uint64_t nb,
-                                                    unsigned K, Key<L3> *__restrict__ out,
-                                                    uint32_t *__restrict__ oc) {
-    constexpr int ITEMS = 8;
-    const uint64_t total = na + nb;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t d0 = t * ITEMS;
-    if (d0 == 0 && t == 0) {
-        out[0] = Key<L3>::zero();
-        if (COUNTED) oc[0] = 0;
+template <int LO, int LA, bool LIFT>
+__device__ __forceinline__ Key<LO> merge_key(const Key<LA> &a, unsigned K) {
+    if constexpr (LIFT) {
+        return lift_fast<LO>(a, K);
+    } else {
+        Key<LO> r;
+#pragma unroll
+        for (int i = 0; i < LO; ++i) r.w[i] = i < LA ? a.w[i] : 0;
+        return r;
     }
-    if (d0 >= total) return;
-    // split: smallest i in [max(0,d0-nb), min(d0,na)] with a[i] > b[d0-i-1] (a first on ties,
-    // ties cannot occur: real and dummy k-mers differ)
-    uint64_t lo = d0 > nb ? d0 - nb : 0, hi = d0 < na ? d0 : na;
+}
+
+template <int LO, int LA, bool LIFT>
+__device__ __forceinline__ uint64_t merge_split(const Key<LA> *__restrict__ a, uint64_t na,
+                                                const Key<LO> *__restrict__ b, uint64_t nb,
+                                                uint64_t diag, unsigned K) {
+    uint64_t lo = diag > nb ? diag - nb : 0, hi = diag < na ? diag : na;
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
-        // take a[mid] before b[d0-mid-1]?
-        if (lift_fast<L3>(a[mid], K) < b[d0 - mid - 1]) lo = mid + 1; else hi = mid;
+        if (merge_key<LO, LA, LIFT>(a[mid], K) < b[diag - mid - 1]) lo = mid + 1; else hi = mid;
     }
-    uint64_t i = lo, j = d0 - lo;
-    const uint64_t end = min(total, d0 + ITEMS);
-    Key<L3> la = i < na ? lift_fast<L3>(a[i], K) : Key<L3>::zero();
-    for (uint64_t o = d0; o < end; ++o) {
-        const bool take_a = i < na && (j >= nb || la < b[j]);
-        if (take_a) {
-            out[1 + o] = la;
-            if (COUNTED) oc[1 + o] = ac[i];
-            ++i;
-            if (i < na) la = lift_fast<L3>(a[i], K);
-        } else {
-            out[1 + o] = b[j];
-            if (COUNTED) oc[1 + o] = 0;
-            ++j;
-        }
+    return lo;
+}
+
+constexpr int MERGE_TILE = 2048;
+
+// diagonal split of every tile boundary (one thread each, all in flight together)
+template <int LO, int LA, bool LIFT>
+__global__ void merge_partition_kernel(const Key<LA> *__restrict__ a, uint64_t na,
+                                       const Key<LO> *__restrict__ b, uint64_t nb, unsigned K,
+                                       uint64_t ntiles, uint64_t *__restrict__ splits) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t diag = min(na + nb, t * MERGE_TILE);
+    splits[t] = merge_split<LO, LA, LIFT>(a, na, b, nb, diag, K);
+}
+
+template <int LO, int LA, bool LIFT, bool COUNTED, bool BCOUNTS>
+__global__ __launch_bounds__(256) void merge_kernel(const Key<LA> *__restrict__ a,
+                                                    const uint32_t *__restrict__ ac, uint64_t na,
+                                                    const Key<LO> *__restrict__ b,
+                                                    const uint32_t *__restrict__ bc, uint64_t nb,
+                                                    unsigned K, const uint64_t *__restrict__ splits,
+                                                    Key<LO> *__restrict__ out,
+                                                    uint32_t *__restrict__ oc, uint64_t off) {
+    constexpr int ITEMS = MERGE_TILE / 256, TILE = MERGE_TILE;
+    __shared__ Key<LO> s_in[TILE];
+    __shared__ Key<LO> s_out[TILE];
+    __shared__ uint32_t s_cin[COUNTED ? TILE : 1];
+    __shared__ uint32_t s_cout[COUNTED ? TILE : 1];
+    __shared__ uint64_t s_split[2];
+    const uint64_t total = na + nb;
+    const uint64_t d0 = (uint64_t)blockIdx.x * TILE;
+    const uint64_t d1 = min(total, d0 + TILE);
+    if (threadIdx.x < 2) s_split[threadIdx.x] = splits[blockIdx.x + threadIdx.x];
+    __syncthreads();
+    const uint64_t a0 = s_split[0], a1 = s_split[1];
+    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
+    const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0);
+    for (uint32_t i = threadIdx.x; i < la; i += 256) {
+        s_in[i] = merge_key<LO, LA, LIFT>(a[a0 + i], K);
+        if (COUNTED) s_cin[i] = ac[a0 + i];
     }
+    for (uint32_t i = threadIdx.x; i < lb; i += 256) {
+        s_in[la + i] = b[b0 + i];
+        if (COUNTED) s_cin[la + i] = BCOUNTS ? bc[b0 + i] : 0;
+    }
+    __syncthreads();
+    // thread's sub-diagonal inside the tile: A run = s_in[0..la), B run = s_in[la..la+lb)
+    const uint32_t t0 = min((uint32_t)threadIdx.x * ITEMS, la + lb);
+    const uint32_t t1 = min(t0 + ITEMS, la + lb);
+    uint32_t lo = t0 > lb ? t0 - lb : 0, hi = min(t0, la);
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_in[mid] < s_in[la + t0 - mid - 1]) lo = mid + 1; else hi = mid;
+    }
+    uint32_t i = lo, j = t0 - lo;
+    for (uint32_t o = t0; o < t1; ++o) {
+        const bool take_a = i < la && (j >= lb || s_in[i] < s_in[la + j]);
+        const uint32_t src = take_a ? i : la + j;
+        s_out[o] = s_in[src];
+        if (COUNTED) s_cout[o] = s_cin[src];
+        if (take_a) ++i; else ++j;
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < la + lb; o += 256) {
+        out[off + d0 + o] = s_out[o];
+        if (COUNTED) oc[off + d0 + o] = s_cout[o];
+    }
+}
+
+__global__ void set_root_row_kernel(uint64_t *key_words, int limbs, uint32_t *count) {
+    for (int i = 0; i < limbs; ++i) key_words[i] = 0;  // the main dummy KMER(0)
+    if (count) *count = 0;
 }
 
 /*

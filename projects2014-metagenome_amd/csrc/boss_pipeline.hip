@@ -42,7 +42,7 @@ class Workspace {
     enum Slot {
         SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
         FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, MSD_COUNTS, MSD_BSTART,
-        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, NSLOTS
+        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -124,7 +124,10 @@ struct Ctx {
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
-static void reset_small(Ctx &c) { HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream)); }
+// zero the per-stage words; the error word is sticky for the whole build (checked at the end)
+static void reset_small(Ctx &c) {
+    HIP_CHECK(hipMemsetAsync(c.small, 0, offsetof(Small, error), c.stream));
+}
 
 static uint64_t read_u64(Ctx &c, const unsigned long long *p) {
     unsigned long long v = 0;
@@ -137,7 +140,7 @@ static void check_error_word(Ctx &c) {
     uint32_t e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, &c.small->error, sizeof(e), hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
-    if (e) throw std::runtime_error("device look-back timed out (error word set)");
+    if (e) throw std::runtime_error("device look-back timed out (error word " + std::to_string(e) + ")");
 }
 
 // Descriptor array for one look-back launch plus its epoch.  Granules of older epochs read as
@@ -273,18 +276,32 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     for (unsigned lev = 1; lev <= levels; ++lev) run_level(lev);
 
     while (true) {
-        // groups of consecutive buckets holding <= LIMIT keys (bigger buckets stand alone)
+        // groups of consecutive buckets holding <= G keys; bigger buckets stand alone
         const uint64_t G = LIMIT / 2;
-        const uint64_t ng = ceil_div(n, G);
-        uint64_t *gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, (ng + 1) * 8);
+        uint64_t ngroups = 1;
+        uint64_t *gstart;
         if (b == 0) {
+            gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, 16);
             set_pair_kernel<<<1, 1, 0, c.stream>>>(gstart, 0, n);
             HIP_CHECK(hipGetLastError());
-        }
-        const uint64_t ngroups = b == 0 ? 1 : ng;
-        if (b) {
-            group_bounds_kernel<<<dim3((unsigned)ceil_div(ngroups + 1, 256)), dim3(256), 0, c.stream>>>(
-                bstart, nbuckets, G, ngroups, n, gstart);
+        } else {
+            uint32_t *gf = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nbuckets + 1) * 4);
+            group_flags_kernel<<<dim3((unsigned)ceil_div(nbuckets, 256)), dim3(256), 0, c.stream>>>(
+                bstart, nbuckets, G, gf);
+            HIP_CHECK(hipGetLastError());
+            uint64_t *gpos = (uint64_t *)c.ws.get(Workspace::MSD_USTART, (nbuckets + 1) * 8);
+            uint32_t ep;
+            const uint64_t st = ceil_div(nbuckets, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(gf, nbuckets, gpos, desc, ep,
+                                                                          &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(&ngroups, gpos + nbuckets, 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, (ngroups + 1) * 8);
+            group_scatter_kernel<<<dim3((unsigned)ceil_div(nbuckets + 1, 256)), dim3(256), 0, c.stream>>>(
+                bstart, gf, gpos, nbuckets, n, gstart);
             HIP_CHECK(hipGetLastError());
         }
         uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (ngroups + 1) * 4);
@@ -308,6 +325,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             return nov;
         };
         uint32_t novf = launch_local(nullptr, ngroups, 0);
+        if (c.debug)
+            fprintf(stderr, "[mtg debug] msd n=%lu nbits=%u levels=%u b=%u buckets=%lu groups=%lu overflow=%u\n",
+                    (unsigned long)n, nbits, levels, b, (unsigned long)nbuckets, (unsigned long)ngroups, novf);
         // overflowing one-bucket groups: rerun them alone in 2, 4, 8, 16 key-range slices
         std::vector<uint32_t> flags;
         std::vector<uint64_t> gs;
@@ -321,6 +341,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
             HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
             novf = launch_local(dlist, list.size(), sbits);  // syncs: `list` outlives the copy
+            if (c.debug) fprintf(stderr, "[mtg debug]   sliced rerun sbits=%u groups=%zu -> overflow=%u\n", sbits, list.size(), novf);
         }
         if (novf) {
             flags.resize(ngroups);
@@ -331,6 +352,16 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             uint64_t ovf_keys = 0;
             for (uint64_t g = 0; g < ngroups; ++g)
                 if (flags[g]) ovf_keys += gs[g + 1] - gs[g];
+            if (c.debug) {
+                fprintf(stderr, "[mtg debug]   fallback: %u groups, %lu keys\n", novf, (unsigned long)ovf_keys);
+                int shown = 0;
+                for (uint64_t g = 0; g < ngroups && shown < 5; ++g)
+                    if (flags[g]) {
+                        fprintf(stderr, "[mtg debug]     group %lu [%lu, %lu)\n", (unsigned long)g,
+                                (unsigned long)gs[g], (unsigned long)gs[g + 1]);
+                        ++shown;
+                    }
+            }
             if (ovf_keys * 20 > n && levels < 3 && 8 * levels < nbits) {
                 run_level(++levels);  // many overflows: one more level for everything
                 continue;
@@ -424,6 +455,22 @@ static void debug_check_sorted(Ctx &c, const char *what, const Key<L> *d, uint64
     fprintf(stderr, "\n");
 }
 
+// merge of two sorted arrays through the tiled merge-path kernels (boss_kernels.hpp)
+template <int LO, int LA, bool LIFT, bool COUNTED, bool BCOUNTS>
+static void merge_sorted(Ctx &c, const Key<LA> *a, const uint32_t *ac, uint64_t na,
+                         const Key<LO> *b, const uint32_t *bc, uint64_t nb, unsigned K,
+                         Key<LO> *out, uint32_t *oc, uint64_t off) {
+    const uint64_t ntiles = ceil_div(na + nb, MERGE_TILE);
+    if (!ntiles) return;
+    uint64_t *splits = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
+    merge_partition_kernel<LO, LA, LIFT><<<dim3((unsigned)ceil_div(ntiles + 1, 256)), dim3(256), 0, c.stream>>>(
+        a, na, b, nb, K, ntiles, splits);
+    HIP_CHECK(hipGetLastError());
+    merge_kernel<LO, LA, LIFT, COUNTED, BCOUNTS><<<dim3((unsigned)ntiles), dim3(256), 0, c.stream>>>(
+        a, ac, na, b, bc, nb, K, splits, out, oc, off);
+    HIP_CHECK(hipGetLastError());
+}
+
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
                          const BuildInput &in, BuildOutput *out) {
@@ -435,6 +482,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
     mtg_boss_timings &T = c.timings;
     T = mtg_boss_timings{};
+    HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
     EventTimer tm(c.stream);
     const int ev_start = tm.mark();
 
@@ -502,40 +550,31 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     debug_check_sorted(c, "collected k-mers", ka, U);
     const int ev_unique = tm.mark();
 
-    // ---- K4 reverse complements (CANONICAL_ONLY) + re-sort
+    // ---- K4 reverse complements (CANONICAL_ONLY): rc(x) of the sorted canonical set is sorted
+    // on its own (no duplicates) and merged with it
     uint64_t R = U;
     if (canonical && U) {
-        // ka holds U keys; needs room for 2U.  Buffers are the workspace's KA/KB slots in
-        // some order: find which slot ka currently is.
-        const size_t need = 2 * U;
-        // re-acquire with keep (may reallocate); keep the slot mapping in sync
-        void *pa = c.ws.get(Workspace::KA, 0);
-        Workspace::Slot sa = (pa == (void *)ka) ? Workspace::KA : Workspace::KB;
-        Workspace::Slot sb = sa == Workspace::KA ? Workspace::KB : Workspace::KA;
-        ka = (K2 *)c.ws.get(sa, need * sizeof(K2), U * sizeof(K2), c.stream);
-        kb = (K2 *)c.ws.get(sb, need * sizeof(K2));
-        if (COUNTED) {
-            void *pc = c.ws.get(Workspace::CA, 0);
-            Workspace::Slot qa = (pc == (void *)ca) ? Workspace::CA : Workspace::CB;
-            Workspace::Slot qb = qa == Workspace::CA ? Workspace::CB : Workspace::CA;
-            ca = (uint32_t *)c.ws.get(qa, need * 4, U * 4, c.stream);
-            cb = (uint32_t *)c.ws.get(qb, need * 4);
-        }
         reset_small(c);
         const uint64_t tiles = ceil_div(U, 1024);
         uint32_t desc_ep;
         uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
         rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            ka, ca, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
+            ka, ca, kb, cb, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total,
+            &c.small->error);
         HIP_CHECK(hipGetLastError());
-        R = U + read_u64(c, &c.small->total);
-        if (c.use_lsd) {
-            radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, true);
-        } else {
-            c.track_partition = true;
-            R = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, R, 2 * K, cmax, 1.0);
-            c.track_partition = false;
-        }
+        uint64_t Urc = read_u64(c, &c.small->total);
+        K2 *ra = kb, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
+        uint32_t *rca = cb, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
+        c.track_partition = true;
+        if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, true);
+        else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0);
+        c.track_partition = false;
+        R = U + Urc;
+        K2 *real = (K2 *)c.ws.get(Workspace::REAL, R * sizeof(K2));
+        uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, R * 4) : nullptr;
+        merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, ra, rca, Urc, K, real, realc, 0);
+        ka = real;
+        ca = realc;
     }
     T.n_real = R;
     debug_check_sorted(c, "real k-mers", ka, R);
@@ -555,9 +594,8 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         reset_small(c);
         uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
         if (R) {
-            dummy_flag_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(R, 256), 8192)),
-                                    dim3(256), 0, c.stream>>>(ka, R, K, bstart, bshift, flags,
-                                                              c.small->totals);
+            dummy_flag_tiled_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0,
+                                          c.stream>>>(ka, R, K, bstart, bshift, nb, flags, c.small->totals);
             HIP_CHECK(hipGetLastError());
         }
         unsigned long long tot[2] = {0, 0};
@@ -601,13 +639,9 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     const uint64_t M = 1 + R + D;
     K3 *sk = (K3 *)c.ws.get(Workspace::STREAM, M * sizeof(K3));
     uint32_t *sc = COUNTED ? (uint32_t *)c.ws.get(Workspace::SCOUNT, M * 4) : nullptr;
-    {
-        const uint64_t threads = ceil_div(R + D, 8);
-        const uint64_t g = std::max<uint64_t>(1, ceil_div(threads, 256));
-        merge_kernel<L2, L3, COUNTED><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(
-            ka, ca, R, dk, D, K, sk, sc);
-        HIP_CHECK(hipGetLastError());
-    }
+    set_root_row_kernel<<<1, 1, 0, c.stream>>>((uint64_t *)sk, L3, COUNTED ? sc : nullptr);
+    HIP_CHECK(hipGetLastError());
+    merge_sorted<L3, L2, true, COUNTED, false>(c, ka, ca, R, dk, nullptr, D, K, sk, sc, 1);
     debug_check_sorted(c, "merged stream", sk, M);
     const int ev_merge = tm.mark();
 

@@ -27,7 +27,7 @@ constexpr int kStatusShift = 46;
 constexpr uint64_t kValueMask = (1ull << kStatusShift) - 1;
 constexpr uint64_t kAgg = 1;
 constexpr uint64_t kIncl = 2;
-constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr uint32_t kSpinLimit = 1u << 22;
 constexpr int LB_WINDOW = 4;
 
 __device__ __forceinline__ uint64_t granule(uint32_t epoch, uint64_t status, uint64_t value) {

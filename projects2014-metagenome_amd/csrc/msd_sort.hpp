@@ -192,23 +192,37 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_partition_kernel(
     }
 }
 
-// group g starts at the first bucket whose start is >= g * G (buckets never split)
-__global__ void group_bounds_kernel(const uint64_t *__restrict__ bstart, uint64_t nbuckets,
-                                    uint64_t G, uint64_t ngroups, uint64_t n,
-                                    uint64_t *__restrict__ gstart) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g > ngroups) return;
-    if (g == ngroups) {
-        gstart[g] = n;
-        return;
+// Group boundaries over buckets (buckets never split): bucket b opens a group when it crosses
+// a multiple of G or when it or its predecessor holds more than G keys, so every big bucket is
+// a group of its own (and can be processed in key-range slices).  flags[b] = 1 for openers.
+__global__ void group_flags_kernel(const uint64_t *__restrict__ bstart, uint64_t nbuckets,
+                                   uint64_t G, uint32_t *__restrict__ flags) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbuckets) return;
+    const uint64_t s0 = bstart[b], s1 = bstart[b + 1];
+    uint32_t f = 0;
+    if (s1 > s0) {  // empty buckets never open a group
+        if (b == 0 || s0 == 0) {
+            f = 1;
+        } else {
+            // previous non-empty bucket ends at s0; its start is the previous distinct start
+            uint64_t p = b;
+            uint64_t ps = s0;
+            while (p > 0 && bstart[p - 1] == s0) --p;  // skip empty predecessors
+            if (p > 0) ps = bstart[p - 1];
+            f = (s0 / G != ps / G) || (s1 - s0 > G) || (s0 - ps > G);
+        }
     }
-    const uint64_t target = g * G;
-    uint64_t lo = 0, hi = nbuckets + 1;  // bstart has nbuckets + 1 entries
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (bstart[mid] < target) lo = mid + 1; else hi = mid;
-    }
-    gstart[g] = lo <= nbuckets ? bstart[lo] : n;
+    flags[b] = f;
+}
+
+__global__ void group_scatter_kernel(const uint64_t *__restrict__ bstart,
+                                     const uint32_t *__restrict__ flags,
+                                     const uint64_t *__restrict__ pos, uint64_t nbuckets,
+                                     uint64_t n, uint64_t *__restrict__ gstart) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nbuckets && flags[b]) gstart[pos[b]] = bstart[b];
+    if (b == nbuckets) gstart[pos[nbuckets]] = n;
 }
 
 template <int L>
@@ -302,47 +316,66 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
         __syncthreads();
 
         bool ovf = false;
-        for (uint64_t i = g0 + tid; i < g1 && !ovf; i += 512) {
-            const Key<L> key = keys[i];
-            if (sbits && bits_at(key, sshift, sbits) != slice) continue;
-            uint32_t h = key_hash(key) & (SLOTS - 1);
-            for (uint32_t probes = 0;;) {
-                if (KEYCAS) {
-                    const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
-                                                   (unsigned long long)EMPTY,
-                                                   (unsigned long long)key.w[0]);
-                    if (old == EMPTY) {
-                        if (atomicAdd(&s_distinct, 1u) >= LIMIT) ovf = true;
-                        break;
-                    }
-                    if (old == key.w[0]) break;
-                } else {
-                    const uint32_t st = atomicCAS(&s_state[h], 0u, 1u);
-                    if (st == 0) {
-                        s_key[h] = key;
-                        __atomic_store_n(&s_state[h], 2u, __ATOMIC_RELEASE);
-                        if (atomicAdd(&s_distinct, 1u) >= LIMIT) ovf = true;
-                        break;
-                    }
-                    if (st != 2 && __atomic_load_n(&s_state[h], __ATOMIC_ACQUIRE) != 2) continue;
-                    if (s_key[h] == key) break;
-                }
-                h = (h + 1) & (SLOTS - 1);
-                if (++probes >= SLOTS) {
-                    ovf = true;
-                    break;
+        uint32_t mynew = 0;  // distinct keys this thread inserted (summed once per thread)
+        // keys are loaded BATCH at a time per thread so the global loads overlap
+        constexpr int BATCH = 8;
+        for (uint64_t ib = g0 + tid; ib < g1 && !ovf; ib += 512 * BATCH) {
+            Key<L> kb[BATCH];
+            uint32_t vb[BATCH];
+#pragma unroll
+            for (int q = 0; q < BATCH; ++q) {
+                const uint64_t i = ib + (uint64_t)q * 512;
+                if (i < g1) {
+                    kb[q] = keys[i];
+                    if (COUNTED) vb[q] = vals[i];
                 }
             }
-            if (COUNTED && !ovf) {
-                const uint32_t add = vals[i];
-                uint32_t old = s_sum[h], assumed;
-                do {
-                    assumed = old;
-                    const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
-                    old = atomicCAS(&s_sum[h], assumed, nv);
-                } while (old != assumed);
+#pragma unroll
+            for (int q = 0; q < BATCH; ++q) {
+                const uint64_t i = ib + (uint64_t)q * 512;
+                if (i >= g1 || ovf) continue;
+                const Key<L> key = kb[q];
+                if (sbits && bits_at(key, sshift, sbits) != slice) continue;
+                uint32_t h = key_hash(key) & (SLOTS - 1);
+                for (uint32_t probes = 0;;) {
+                    if (KEYCAS) {
+                        const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
+                                                       (unsigned long long)EMPTY,
+                                                       (unsigned long long)key.w[0]);
+                        if (old == EMPTY) {
+                            ++mynew;
+                            break;
+                        }
+                        if (old == key.w[0]) break;
+                    } else {
+                        const uint32_t st = atomicCAS(&s_state[h], 0u, 1u);
+                        if (st == 0) {
+                            s_key[h] = key;
+                            __atomic_store_n(&s_state[h], 2u, __ATOMIC_RELEASE);
+                            ++mynew;
+                            break;
+                        }
+                        if (st != 2 && __atomic_load_n(&s_state[h], __ATOMIC_ACQUIRE) != 2) continue;
+                        if (s_key[h] == key) break;
+                    }
+                    h = (h + 1) & (SLOTS - 1);
+                    if (++probes >= SLOTS) {
+                        ovf = true;
+                        break;
+                    }
+                }
+                if (COUNTED && !ovf) {
+                    const uint32_t add = vb[q];
+                    uint32_t old = s_sum[h], assumed;
+                    do {
+                        assumed = old;
+                        const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
+                        old = atomicCAS(&s_sum[h], assumed, nv);
+                    } while (old != assumed);
+                }
             }
         }
+        if (mynew) atomicAdd(&s_distinct, mynew);
         if (__syncthreads_or(ovf) || s_distinct > LIMIT) {
             if (tid == 0) {
                 overflow[g] = 1;
