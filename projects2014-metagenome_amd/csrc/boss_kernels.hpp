@@ -48,29 +48,27 @@ __device__ __forceinline__ Key<L> plain_to_boss(const Key<L> &P, unsigned K, con
  * (so no window spans two reads).  Workgroup = TILE consecutive window starts; its bytes are
  * staged in LDS as 2-bit codes (4 = invalid); each thread slides PPT windows keeping the
  * forward and reverse-complement plain words and the position of the last invalid char.
- * Valid k-mers are compacted in position order: block scan + decoupled look-back for the tile
- * base, staged in LDS, written coalesced.
+ * Valid k-mers are compacted in position order in two launches over the same tiling: the
+ * COUNT_ONLY launch writes each tile's number of valid windows, the caller scans them, and the
+ * full launch writes its tile's k-mers at that offset (block scan, staged in LDS, written
+ * coalesced).  No inter-workgroup hand-off, so tiles need no dequeue counter.
  */
-template <int L, bool COUNTED>
+template <int L, bool COUNTED, bool COUNT_ONLY>
 __global__ __launch_bounds__(256) void extract_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts,
     uint64_t n_reads, uint32_t cmax, Key<L> *__restrict__ out_keys,
-    uint32_t *__restrict__ out_counts, uint64_t *desc, uint32_t epoch, uint32_t *tile_counter,
-    unsigned long long *total_out, uint32_t *error) {
+    uint32_t *__restrict__ out_counts, uint32_t *__restrict__ tcnt,
+    const uint64_t *__restrict__ toff) {
     using T = ExtractTraits<L>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
     __shared__ uint8_t s_code[TILE + T::MAXK];
-    __shared__ Key<L> s_out[TILE];
-    __shared__ uint32_t s_cnt[COUNTED ? TILE : 1];
+    __shared__ Key<L> s_out[COUNT_ONLY ? 1 : TILE];
+    __shared__ uint32_t s_cnt[COUNTED && !COUNT_ONLY ? TILE : 1];
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
-    __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_base;
 
     const uint32_t tid = threadIdx.x;
-    if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = blockIdx.x;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
     const uint64_t base = (uint64_t)tile * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
@@ -107,7 +105,9 @@ __global__ __launch_bounds__(256) void extract_kernel(
         for (int j = 0; j < PPT; ++j) {
             const uint64_t p = p0 + j;
             if (p < npos) {
-                if (last_bad < (int64_t)j) {
+                if (last_bad < (int64_t)j && COUNT_ONLY) {
+                    ++nvalid;
+                } else if (last_bad < (int64_t)j) {
                     Key<L> f = plain_to_boss(P, K, low);
                     if (canonical) {
                         Key<L> r = plain_to_boss(R, K, low);
@@ -136,10 +136,9 @@ __global__ __launch_bounds__(256) void extract_kernel(
     }
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nvalid, s_scan, &tile_total);
-    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
-    if (tid == 0) {
-        const uint64_t ntiles = (npos + TILE - 1) / TILE;
-        if (tile + 1 == ntiles) *total_out = s_base + tile_total;
+    if constexpr (COUNT_ONLY) {
+        if (tid == 0) tcnt[tile] = tile_total;
+        return;
     }
     {
         uint32_t o = off;
@@ -153,7 +152,7 @@ __global__ __launch_bounds__(256) void extract_kernel(
         }
     }
     __syncthreads();
-    const uint64_t gb = s_base;
+    const uint64_t gb = toff[tile];
     for (uint32_t i = tid; i < tile_total; i += BLOCK) {
         out_keys[gb + i] = s_out[i];
         if (COUNTED) out_counts[gb + i] = s_cnt[i];
@@ -331,233 +330,145 @@ __device__ __forceinline__ uint64_t lower_bound_bucketed(const Key<L> *__restric
     return lo;
 }
 
-/*
- * K5 + K6 (flag pass): for each real edge x (sorted, 2-bit):
- *   sink   -- add_dummy_sink_kmers (boss_chunk_construct.cpp:54-98): the target node
- *             a_2..a_K has no real out-edge  <=>  no key y with y >> 2 == to_next(x, 0) >> 2;
- *   source -- add_dummy_source_kmers (:123-168): x is the first edge of its node and no real
- *             y has chars 2..k equal to x's chars 1..k-1 with label a_k (y >> 4 == prev >> 4
- *             and y & 3 == prev & 3, prev = to_prev(x, 0)).
- * flags[i] = sink | source << 1.  Duplicated sinks (several x with one target) are removed by
- * the final unique over all dummies, as are repeated higher-level sources.
- */
-template <int L>
-__global__ __launch_bounds__(256) void dummy_flag_kernel(const Key<L> *__restrict__ keys,
-                                                         uint64_t n, unsigned K,
-                                                         const uint64_t *__restrict__ start,
-                                                         unsigned bshift, uint8_t *__restrict__ flags,
-                                                         unsigned long long *totals) {
-    __shared__ unsigned long long s_tot[2];
-    if (threadIdx.x < 2) s_tot[threadIdx.x] = 0;
-    __syncthreads();
-    unsigned long long ns = 0, nsrc = 0;
-    const Key<L> full = Key<L>::lowmask(2 * K);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const Key<L> x = keys[i];
-        uint8_t f = 0;
-        // to_next(x, K, 0): node a_2..a_K, label 0
-        const Key<L> t = (shr(x, 2) | shl(Key<L>::from(x.w[0] & 3), 2 * (K - 1))) &
-                         ~Key<L>::from(3);
-        {
-            const uint64_t j = lower_bound_bucketed(keys, start, bshift, t);
-            if (j >= n || shr(keys[j], 2) != shr(t, 2)) f |= 1;
-        }
-        if (i == 0 || shr(keys[i - 1], 2) != shr(x, 2)) {
-            // to_prev(x, K, 0): node 0 a_1..a_{k-1}, label a_k
-            const Key<L> prev = (shl(x & ~Key<L>::from(3), 2) & full) | shr(x, 2 * (K - 1));
-            const Key<L> lo = prev & ~Key<L>::from(15);
-            uint64_t j = lower_bound_bucketed(keys, start, bshift, lo);
-            bool redundant = false;
-            const uint32_t label = (uint32_t)(prev.w[0] & 3);
-            while (j < n && shr(keys[j], 4) == shr(prev, 4)) {
-                if ((uint32_t)(keys[j].w[0] & 3) == label) {
-                    redundant = true;
-                    break;
-                }
-                ++j;
-            }
-            if (!redundant) f |= 2;
-        }
-        flags[i] = f;
-        ns += f & 1;
-        nsrc += f >> 1;
-    }
-    atomicAdd(&s_tot[0], ns);
-    atomicAdd(&s_tot[1], nsrc);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        atomicAdd(&totals[0], s_tot[0]);
-        atomicAdd(&totals[1], s_tot[1]);
-    }
-}
-
-// first index with keys[i] > hi (hi within the 2K-bit key range, or all-ones)
-template <int L>
-__device__ __forceinline__ uint64_t upper_bucketed(const Key<L> *__restrict__ keys, uint64_t n,
-                                                   const uint64_t *__restrict__ start,
-                                                   unsigned shift, uint64_t nbuckets,
-                                                   const Key<L> &hi, unsigned K) {
-    if (hi == Key<L>::lowmask(2 * K)) return n;
-    const Key<L> h1 = hi + Key<L>::from(1);
-    if (bits_at(shr(h1, shift), 0, 32) >= nbuckets) return n;
-    return lower_bound_bucketed(keys, start, shift, h1);
-}
-
 template <int L>
 struct DummyTraits {
-    static constexpr int TILE = L == 1 ? 2048 : L == 2 ? 1024 : 512;
-    static constexpr int CAP = 2 * TILE;
-    static constexpr int PER = TILE / 256;
+    static constexpr int BLOCK = 256;
+    static constexpr int PER = L == 1 ? 4 : 2;   // consecutive edges per thread
+    static constexpr int TILE = BLOCK * PER;
+    static constexpr int CAP = 2 * TILE;         // staged real edges (the 4 sink ranges)
+    static constexpr int BCAP = TILE;            // staged bucket starts
+    static constexpr int WTILE = 4096;           // edges per tile of the count / write passes
 };
 
 /*
- * K5 + K6 flag pass, tiled (same predicates as dummy_flag_kernel below).  A workgroup takes
- * TILE consecutive real edges.  Per probe class -- sink probes of label c = 0..3 and the source
- * probes -- the probes of the tile are monotone, so every real edge they can hit lies in one
- * contiguous key range: two bucketed searches find it, it is staged in LDS and the probes are
- * resolved there.  A range larger than CAP (or source probes of a tile that straddles a change
- * of the last node char) falls back to per-probe bucketed searches.
+ * K5 (sink pass) over the sorted real edges x (2-bit keys), one join of the reference's two
+ * dummy scans:
+ *   sink   -- add_dummy_sink_kmers (boss_chunk_construct.cpp:54-98): the target node a_2..a_K
+ *             of x has no real out-edge  <=>  no y with y >> 2 == to_next(x, 0) >> 2;
+ *   in-edge marks -- add_dummy_source_kmers (:123-168) emits a source for the first edge x of
+ *             a node with no real y such that y's chars 2..k equal x's chars 1..k-1 and y's label
+ *             is a_k: exactly "no real edge targets x's node".  So when the sink probe of x finds
+ *             its target node, it marks that node's first edge in in_flag, and the count/write
+ *             passes read source = first edge && !in_flag.
+ * flags[i] = sink | first-edge-of-node << 1.
+ *
+ * This is the GPU form of the reference's per-character merge iterators.  A workgroup takes
+ * TILE consecutive edges, PER consecutive ones per thread.  The sink probes of label c are
+ * sorted (to_next is monotone on the edges of one label), so all edges they can hit lie in one
+ * contiguous key range.  The 4 ranges and their slices of the bucket index are staged in LDS;
+ * a probe reads its bucket's slice bounds from LDS and binary-searches the bucket (a few keys).
+ * A range that does not fit falls back to bucketed searches in global memory.
  */
 template <int L>
-__global__ __launch_bounds__(256) void dummy_flag_tiled_kernel(
+__global__ __launch_bounds__(256) void dummy_sink_kernel(
     const Key<L> *__restrict__ keys, uint64_t n, unsigned K, const uint64_t *__restrict__ start,
-    unsigned bshift, uint64_t nbuckets, uint8_t *__restrict__ flags,
-    unsigned long long *totals) {
+    unsigned bshift, uint8_t *__restrict__ flags, uint8_t *__restrict__ in_flag) {
     using T = DummyTraits<L>;
-    __shared__ Key<L> s_x[T::TILE];
+    constexpr int PER = T::PER;
     __shared__ Key<L> s_r[T::CAP];
-    __shared__ uint64_t s_a, s_cnt;
-    __shared__ unsigned long long s_tot[2];
+    __shared__ uint32_t s_b[T::BCAP];
+    __shared__ uint64_t s_lo[4], s_blo[4];
+    __shared__ uint32_t s_cnt[4], s_nb[4], s_off[4], s_boff[4];
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * T::TILE;
     const uint32_t tn = (uint32_t)min((uint64_t)T::TILE, n - base);
-    if (tid < 2) s_tot[tid] = 0;
-    for (uint32_t j = tid; j < tn; j += 256) s_x[j] = keys[base + j];
-    __syncthreads();
-    const Key<L> full = Key<L>::lowmask(2 * K);
-    const Key<L> x_first = s_x[0], x_last = s_x[tn - 1];
-    const unsigned k = K - 1;
-    uint8_t f[T::PER];
-    Key<L> probe[T::PER];
-#pragma unroll
-    for (int q = 0; q < T::PER; ++q) f[q] = 0;
+    const Key<L> m3 = Key<L>::from(3);
 
-    // classes 0..3: sink probes of label c over the whole tile; classes 4..7: source probes of
-    // one quarter of the tile each (their key range is ~4x wider than the edges' range)
-    constexpr uint32_t QT = T::TILE / 4;
-    for (int cls = 0; cls < 8; ++cls) {
-        const uint32_t sub = cls < 4 ? 0 : cls - 4;
-        const uint32_t q0 = sub * QT, q1 = min(tn, q0 + QT);
-        if (cls >= 4 && q0 >= tn) break;
-        // this class's probes and the key range they can hit
-        bool mine[T::PER];
-#pragma unroll
-        for (int q = 0; q < T::PER; ++q) {
-            const uint32_t j = tid + 256 * q;
-            mine[q] = false;
-            if (j >= tn) continue;
-            if (cls >= 4 && (j < q0 || j >= q1)) continue;
-            const Key<L> x = s_x[j];
-            if (cls < 4) {
-                if ((uint32_t)(x.w[0] & 3) != (uint32_t)cls) continue;
-                // to_next(x, K, 0): node a_2..a_K, label 0 (kmer_boss.hpp:147-169)
-                probe[q] = (shr(x, 2) | shl(Key<L>::from(x.w[0] & 3), 2 * (K - 1))) & ~Key<L>::from(3);
-                mine[q] = true;
-            } else {
-                const bool first = base + j == 0 ||
-                                   shr(j ? s_x[j - 1] : keys[base - 1], 2) != shr(x, 2);
-                if (!first) continue;
-                // to_prev(x, K, 0): node 0 a_1..a_{k-1}, label a_k (kmer_boss.hpp:171-186)
-                probe[q] = (shl(x & ~Key<L>::from(3), 2) & full) | shr(x, 2 * (K - 1));
-                mine[q] = true;
-            }
-        }
-        if (tid == 0) {
-            Key<L> lo, hi;
-            bool ok = true;
-            if (cls < 4) {
-                const Key<L> c = shl(Key<L>::from(cls), 2 * (K - 1));
-                lo = (shr(x_first, 2) | c) & ~Key<L>::from(3);
-                hi = shr(x_last, 2) | c | Key<L>::from(3);
-            } else {
-                const Key<L> xf = s_x[q0], xl = s_x[q1 - 1];
-                ok = char_at(xf, k, 2) == char_at(xl, k, 2);
-                const Key<L> pf = (shl(xf & ~Key<L>::from(3), 2) & full) | shr(xf, 2 * (K - 1));
-                const Key<L> pl = (shl(xl & ~Key<L>::from(3), 2) & full) | shr(xl, 2 * (K - 1));
-                lo = pf & ~Key<L>::from(15);
-                hi = pl | Key<L>::from(15);
-            }
-            uint64_t a = 0, b = 0;
-            if (ok) {
-                a = lower_bound_bucketed(keys, start, bshift, lo);
-                b = upper_bucketed(keys, n, start, bshift, nbuckets, hi, K);
-            }
-            s_a = a;
-            s_cnt = ok && b - a <= (uint64_t)T::CAP ? b - a : ~0ull;
-        }
-        __syncthreads();
-        const uint64_t a = s_a, cnt = s_cnt;
-        if (cnt != ~0ull)
-            for (uint32_t j = tid; j < cnt; j += 256) s_r[j] = keys[a + j];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < T::PER; ++q) {
-            if (!mine[q]) continue;
-            const Key<L> p = probe[q];
-            if (cls < 4) {
-                bool found;
-                if (cnt != ~0ull) {
-                    uint32_t lo = 0, hi = (uint32_t)cnt;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_r[mid] < p) lo = mid + 1; else hi = mid;
-                    }
-                    found = lo < cnt && shr(s_r[lo], 2) == shr(p, 2);
-                } else {
-                    const uint64_t j = lower_bound_bucketed(keys, start, bshift, p);
-                    found = j < n && shr(keys[j], 2) == shr(p, 2);
-                }
-                if (!found) f[q] |= 1;
-            } else {
-                const Key<L> lo4 = p & ~Key<L>::from(15);
-                const uint32_t label = (uint32_t)(p.w[0] & 3);
-                bool redundant = false;
-                if (cnt != ~0ull) {
-                    uint32_t lo = 0, hi = (uint32_t)cnt;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_r[mid] < lo4) lo = mid + 1; else hi = mid;
-                    }
-                    for (uint32_t j = lo; j < cnt && shr(s_r[j], 4) == shr(p, 4); ++j)
-                        if ((uint32_t)(s_r[j].w[0] & 3) == label) { redundant = true; break; }
-                } else {
-                    for (uint64_t j = lower_bound_bucketed(keys, start, bshift, lo4);
-                         j < n && shr(keys[j], 4) == shr(p, 4); ++j)
-                        if ((uint32_t)(keys[j].w[0] & 3) == label) { redundant = true; break; }
-                }
-                if (!redundant) f[q] |= 2;
-            }
-        }
-        __syncthreads();
+    if (tid < 4) {
+        // key range of the sink probes of label c = tid, read off the bucket index
+        const Key<L> c = shl(Key<L>::from(tid), 2 * (K - 1));
+        const Key<L> lo = (shr(keys[base], 2) | c) & ~m3;
+        const Key<L> hi = shr(keys[base + tn - 1], 2) | c | m3;
+        const uint64_t blo = bits_at(shr(lo, bshift), 0, 32), bhi = bits_at(shr(hi, bshift), 0, 32);
+        const uint64_t a = start[blo], b = start[bhi + 1];
+        s_lo[tid] = a;
+        s_blo[tid] = blo;
+        s_cnt[tid] = (uint32_t)min(b - a, (uint64_t)0xFFFFFFFFu);
+        s_nb[tid] = (uint32_t)min(bhi - blo + 2, (uint64_t)0xFFFFFFFFu);
     }
-    unsigned long long ns = 0, nsrc = 0;
+    const uint32_t j0 = tid * PER;
+    Key<L> x[PER];
+    uint32_t first = 0;
+    {
+        Key<L> prev = base + j0 > 0 && j0 < tn ? keys[base + j0 - 1] : Key<L>::zero();
 #pragma unroll
-    for (int q = 0; q < T::PER; ++q) {
-        const uint32_t j = tid + 256 * q;
-        if (j < tn) {
-            flags[base + j] = f[q];
-            ns += f[q] & 1;
-            nsrc += f[q] >> 1;
+        for (int q = 0; q < PER; ++q) {
+            x[q] = Key<L>::zero();
+            if (j0 + q < tn) {
+                x[q] = keys[base + j0 + q];
+                if (base + j0 + q == 0 || shr(prev, 2) != shr(x[q], 2)) first |= 1u << q;
+                prev = x[q];
+            }
         }
     }
-    atomicAdd(&s_tot[0], ns);
-    atomicAdd(&s_tot[1], nsrc);
     __syncthreads();
     if (tid == 0) {
-        atomicAdd(&totals[0], s_tot[0]);
-        atomicAdd(&totals[1], s_tot[1]);
+        uint32_t cum = 0, bcum = 0;
+        for (int c = 0; c < 4; ++c) {
+            s_off[c] = ~0u;  // ~0 = global fallback
+            if ((uint64_t)cum + s_cnt[c] <= (uint64_t)T::CAP &&
+                (uint64_t)bcum + s_nb[c] <= (uint64_t)T::BCAP) {
+                s_off[c] = cum;
+                s_boff[c] = bcum;
+                cum += s_cnt[c];
+                bcum += s_nb[c];
+            }
+        }
     }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (s_off[c] == ~0u) continue;
+        const uint64_t a = s_lo[c];
+        const uint32_t off = s_off[c], boff = s_boff[c];
+        for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = keys[a + j];
+        for (uint32_t j = tid; j < s_nb[c]; j += 256) s_b[boff + j] = (uint32_t)(start[s_blo[c] + j] - a);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (j0 + q >= tn) continue;
+        const uint32_t c = (uint32_t)(x[q].w[0] & 3);
+        // to_next(x, K, 0): node a_2..a_K, label 0 (kmer_boss.hpp:147-169)
+        const Key<L> p = (shr(x[q], 2) | shl(Key<L>::from(c), 2 * (K - 1))) & ~m3;
+        uint64_t hit = ~0ull;
+        const uint32_t off = s_off[c];
+        if (off != ~0u) {
+            const uint32_t bo = s_boff[c] + (uint32_t)(bits_at(shr(p, bshift), 0, 32) - s_blo[c]);
+            uint32_t lo = s_b[bo], hi = s_b[bo + 1];
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_r[off + mid] < p) lo = mid + 1; else hi = mid;
+            }
+            if (lo < s_cnt[c] && shr(s_r[off + lo], 2) == shr(p, 2)) hit = s_lo[c] + lo;
+        } else {
+            const uint64_t i = lower_bound_bucketed(keys, start, bshift, p);
+            if (i < n && shr(keys[i], 2) == shr(p, 2)) hit = i;
+        }
+        if (hit != ~0ull) in_flag[hit] = 1;
+        flags[base + j0 + q] = (uint8_t)((hit == ~0ull ? 1u : 0u) | (((first >> q) & 1u) << 1));
+    }
+}
+
+// dummies emitted by edge i: a sink, and a source with its k - 1 higher levels
+__device__ __forceinline__ uint32_t dummy_emits(uint32_t f, uint32_t in, uint32_t k) {
+    return (f & 1u) + ((f >> 1) & ~in & 1u) * k;
+}
+
+// K6a: per-tile dummy counts (WTILE edges per workgroup, 16 consecutive per thread)
+__global__ __launch_bounds__(256) void dummy_count_kernel(const uint8_t *__restrict__ flags,
+                                                          const uint8_t *__restrict__ in_flag,
+                                                          uint64_t n, unsigned k,
+                                                          uint32_t *__restrict__ tcnt) {
+    __shared__ uint32_t s_scan[256 / 64 + 1];
+    const uint64_t i0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if (i0 + j < n) cnt += dummy_emits(flags[i0 + j], in_flag[i0 + j], k);
+    uint32_t total;
+    block_exclusive_sum<256>(cnt, s_scan, &total);
+    if (threadIdx.x == 0) tcnt[blockIdx.x] = total;
 }
 
 // byte of four 2-bit chars -> four 3-bit chars, each + 1 ($ACGT lift, kmer_transform.hpp:102-165)
@@ -575,48 +486,43 @@ __device__ __forceinline__ Key<LO> lift_fast(const Key<LI> &x, unsigned K) {
 }
 
 /*
- * K5/K6 (write pass): emit the lifted dummy k-mers in edge order (block scan + look-back):
- * a sink as lift(to_next(x,0)) with its label char cleared to $ (:94), a source as
+ * K6b (write pass): emit the lifted dummy k-mers in edge order at the offsets of the scanned
+ * tile counts: a sink as lift(to_next(x,0)) with its label char cleared to $ (:94), a source as
  * lift(to_prev(x,0)) with char 1 cleared to $ (:165) followed by its k-1 higher levels
- * to_prev(., $) (:286-303).
+ * to_prev(., $) (:286-303).  Only edges that emit are re-read.
  */
 template <int L2, int L3>
 __global__ __launch_bounds__(256) void dummy_write_kernel(
-    const Key<L2> *__restrict__ keys, const uint8_t *__restrict__ flags, uint64_t n, unsigned K,
-    Key<L3> *__restrict__ out, uint64_t *desc, uint32_t epoch, uint32_t *tile_counter, uint32_t *error) {
-    constexpr int BLOCK = 256, ITEMS = 4, TILE = BLOCK * ITEMS;
-    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
-    __shared__ uint32_t s_tile;
-    __shared__ uint64_t s_base;
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint64_t i0 = (uint64_t)tile * TILE + (uint64_t)tid * ITEMS;
+    const Key<L2> *__restrict__ keys, const uint8_t *__restrict__ flags,
+    const uint8_t *__restrict__ in_flag, uint64_t n, unsigned K,
+    const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out) {
+    __shared__ uint32_t s_scan[256 / 64 + 1];
+    const uint64_t i0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
     const unsigned k = K - 1;
+    uint32_t e[16];
     uint32_t cnt = 0;
-    uint8_t f[ITEMS];
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-        f[j] = i0 + j < n ? flags[i0 + j] : 0;
-        cnt += (f[j] & 1) + (f[j] >> 1) * k;
+    for (int j = 0; j < 16; ++j) {
+        e[j] = i0 + j < n ? dummy_emits(flags[i0 + j], in_flag[i0 + j], k) : 0;
+        cnt += e[j];
     }
     uint32_t tile_total;
-    const uint32_t off = block_exclusive_sum<BLOCK>(cnt, s_scan, &tile_total);
-    tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
-    uint64_t o = s_base + off;
+    const uint32_t off = block_exclusive_sum<256>(cnt, s_scan, &tile_total);
+    if (!cnt) return;
+    uint64_t o = toff[blockIdx.x] + off;
     const Key<L2> full = Key<L2>::lowmask(2 * K);
     const Key<L3> full3 = Key<L3>::lowmask(3 * K);
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-        if (!f[j]) continue;
+    for (int j = 0; j < 16; ++j) {
+        if (!e[j]) continue;
         const Key<L2> x = keys[i0 + j];
-        if (f[j] & 1) {
+        const uint32_t f = flags[i0 + j];
+        if (f & 1) {
             const Key<L2> t = (shr(x, 2) | shl(Key<L2>::from(x.w[0] & 3), 2 * (K - 1))) &
                               ~Key<L2>::from(3);
             out[o++] = lift_fast<L3>(t, K) & ~Key<L3>::from(7);
         }
-        if (f[j] & 2) {
+        if ((f >> 1) & ~(uint32_t)in_flag[i0 + j] & 1u) {
             const Key<L2> prev = (shl(x & ~Key<L2>::from(3), 2) & full) | shr(x, 2 * (K - 1));
             Key<L3> d = lift_fast<L3>(prev, K) & ~Key<L3>::from(7 << 3);
             out[o++] = d;
@@ -734,6 +640,103 @@ __global__ __launch_bounds__(256) void merge_kernel(const Key<LA> *__restrict__ 
 __global__ void set_root_row_kernel(uint64_t *key_words, int limbs, uint32_t *count) {
     for (int i = 0; i < limbs; ++i) key_words[i] = 0;  // the main dummy KMER(0)
     if (count) *count = 0;
+}
+
+/*
+ * K8 fast path: the same rows as emit_kernel below when no row is a redundant dummy sink, which
+ * is the normal case (the dummy unique leaves at most one sink per node and a sink's node has no
+ * other out-edge); a skip row sets *skip and the caller reruns the compacting emit_kernel.
+ * Row r goes to output r + 1 (row 0 of the output is the leading all-$ row).  A thread owns 8
+ * consecutive OUTPUTS, so W and last leave as one aligned 8-byte store each and the weights as
+ * two 16-byte stores; rows r-1 and r+1 come from the same sliding window of keys, and the
+ * same-group look-back for the W "minus" flag rarely leaves the window.
+ */
+template <int L3, bool COUNTED>
+__global__ __launch_bounds__(256) void emit_fast_kernel(
+    const Key<L3> *__restrict__ s, const uint32_t *__restrict__ sc, uint64_t m, unsigned k,
+    uint32_t wmax, uint8_t *__restrict__ W, uint8_t *__restrict__ last,
+    uint32_t *__restrict__ weights, uint32_t *__restrict__ skip) {
+    constexpr int PER = 8;
+    const uint64_t o0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * PER;
+    if (o0 > m) return;
+    // window: rows o0 - 2 .. o0 + PER - 1 (row r = output o - 1)
+    Key<L3> win[PER + 2];
+#pragma unroll
+    for (int j = 0; j < PER + 2; ++j) {
+        const int64_t r = (int64_t)o0 - 2 + j;
+        win[j] = r >= 0 && r < (int64_t)m ? s[r] : Key<L3>::zero();
+    }
+    uint64_t wpack = 0, lpack = 0;
+    uint32_t wt[PER];
+    bool skipped = false;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        wt[j] = 0;
+        const int64_t r = (int64_t)o0 - 1 + j;
+        if (r < 0 || r >= (int64_t)m) continue;
+        const Key<L3> key = win[j + 1];
+        const uint32_t c = (uint32_t)(key.w[0] & 7);
+        const Key<L3> node = shr(key, 3);
+        const bool same_next = r + 1 < (int64_t)m && shr(win[j + 2], 3) == node;
+        if (same_next && c == 0 && char_at(key, k, 3) > 0) skipped = true;
+        uint32_t ww = c;
+        if (c) {
+            // an earlier row of the same chars-2..k group with the same label -> "minus"
+            const Key<L3> grp = shr(key, 6);
+            int64_t p = r - 1;
+            bool done = false;
+#pragma unroll
+            for (int q = j; q >= 0; --q) {  // window rows r-1 .. o0-2
+                if (done || p < 0) break;
+                const Key<L3> y = win[q];
+                if (shr(y, 6) != grp) done = true;
+                else if ((uint32_t)(y.w[0] & 7) == c) { ww = c + 5; done = true; }
+                --p;
+            }
+            for (; !done && p >= 0; --p) {
+                const Key<L3> y = s[p];
+                if (shr(y, 6) != grp) break;
+                if ((uint32_t)(y.w[0] & 7) == c) { ww = c + 5; break; }
+            }
+        }
+        wpack |= (uint64_t)ww << (8 * j);
+        lpack |= (uint64_t)(same_next ? 0 : 1) << (8 * j);
+        if (COUNTED) {
+            const uint32_t cnt = sc[r];
+            wt[j] = (cnt && ww && char_at(key, 1, 3)) ? (cnt < wmax ? cnt : wmax) : 0;
+        }
+    }
+    if (skipped) atomicOr(skip, 1u);
+    if (o0 + PER <= m + 1) {
+        *(uint64_t *)(W + o0) = wpack;
+        *(uint64_t *)(last + o0) = lpack;
+        if (COUNTED) {
+            *(uint4 *)(weights + o0) = make_uint4(wt[0], wt[1], wt[2], wt[3]);
+            *(uint4 *)(weights + o0 + 4) = make_uint4(wt[4], wt[5], wt[6], wt[7]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (o0 + j > m) break;
+            W[o0 + j] = (uint8_t)(wpack >> (8 * j));
+            last[o0 + j] = (uint8_t)(lpack >> (8 * j));
+            if (COUNTED) weights[o0 + j] = wt[j];
+        }
+    }
+}
+
+// F[c] = number of stream rows whose last node char is < c (the stream is sorted by that char)
+template <int L3>
+__global__ void f_bounds_kernel(const Key<L3> *__restrict__ s, uint64_t m, unsigned k,
+                                unsigned long long *__restrict__ F) {
+    const uint32_t c = threadIdx.x;
+    if (c >= 5) return;
+    uint64_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (char_at(s[mid], k, 3) < c) lo = mid + 1; else hi = mid;
+    }
+    F[c] = lo;
 }
 
 /*

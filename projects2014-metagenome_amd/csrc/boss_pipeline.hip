@@ -42,7 +42,7 @@ class Workspace {
     enum Slot {
         SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
         FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, MSD_COUNTS, MSD_BSTART,
-        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, NSLOTS
+        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -80,6 +80,7 @@ struct Small {  // one device word block, zeroed per use
     unsigned long long totals[2];
     unsigned long long fhist[8];
     uint32_t counter;
+    uint32_t skip;
     uint32_t error;
 };
 
@@ -119,6 +120,9 @@ struct Ctx {
     uint64_t radix_launches = 0;
     bool track_partition = false;  // time the msd_partition launches of the real-k-mer sorts
     bool use_lsd = false;          // MTG_SORT=lsd: LSD onesweep + unique instead of MSD
+    bool emit_slow = false;        // MTG_EMIT=slow: always the compacting emit kernel
+    bool dummy_msd = false;        // MTG_DUMMY_SORT=msd: MSD for the dummy k-mers (default LSD:
+                                   // their $-padded keys crowd a few top-digit buckets)
     bool debug = false;            // MTG_DEBUG=1: host-side checks between stages
 };
 
@@ -418,7 +422,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
 template <int L>
 static unsigned bucket_bits(uint64_t n, unsigned keybits) {
     unsigned b = 1;
-    while (b < 22 && (1ull << (b + 2)) < n) ++b;
+    while (b < 26 && (1ull << (b + 2)) < n) ++b;
     return std::min(b, keybits);
 }
 
@@ -591,29 +595,38 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
         bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
         HIP_CHECK(hipGetLastError());
-        reset_small(c);
         uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
+        uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
+        const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
+        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
+        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (wtiles + 1) * 8);
+        uint64_t Draw = 0;
         if (R) {
-            dummy_flag_tiled_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0,
-                                          c.stream>>>(ka, R, K, bstart, bshift, nb, flags, c.small->totals);
+            HIP_CHECK(hipMemsetAsync(in_flag, 0, R, c.stream));
+            dummy_sink_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0,
+                                    c.stream>>>(ka, R, K, bstart, bshift, flags, in_flag);
             HIP_CHECK(hipGetLastError());
+            dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, k,
+                                                                                  tcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t st = ceil_div(wtiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(
+                tcnt, wtiles, toff, desc, ep, &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(&Draw, toff + wtiles, 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
         }
-        unsigned long long tot[2] = {0, 0};
-        HIP_CHECK(hipMemcpyAsync(tot, c.small->totals, sizeof(tot), hipMemcpyDeviceToHost, c.stream));
-        HIP_CHECK(hipStreamSynchronize(c.stream));
-        const uint64_t Draw = tot[0] + tot[1] * k;
         K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
         K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
         if (Draw) {
-            reset_small(c);
-            const uint64_t tiles = ceil_div(R, 1024);
-            uint32_t desc_ep;
-        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
-            dummy_write_kernel<L2, L3><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-                ka, flags, R, K, da, desc, desc_ep, &c.small->counter, &c.small->error);
+            dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(
+                ka, flags, in_flag, R, K, toff, da);
             HIP_CHECK(hipGetLastError());
             uint32_t *nv = nullptr;
-            if (c.use_lsd) {
+            if (c.use_lsd || !c.dummy_msd) {
                 radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
                 reset_small(c);
                 const uint64_t ut = ceil_div(Draw, 2048);
@@ -653,8 +666,22 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     HIP_CHECK(hipMemsetAsync(last, 0, 1, c.stream));
     if (COUNTED) HIP_CHECK(hipMemsetAsync(weights, 0, 4, c.stream));
     reset_small(c);
-    uint64_t rows;
-    {
+    uint64_t rows = M;
+    bool slow = c.emit_slow;
+    if (!slow) {
+        emit_fast_kernel<L3, COUNTED><<<dim3((unsigned)ceil_div(M + 1, 256 * 8)), dim3(256), 0, c.stream>>>(
+            sk, sc, M, k, wmax, W, last, weights, &c.small->skip);
+        HIP_CHECK(hipGetLastError());
+        f_bounds_kernel<L3><<<1, 64, 0, c.stream>>>(sk, M, k, c.small->fhist);
+        HIP_CHECK(hipGetLastError());
+        Small h;
+        HIP_CHECK(hipMemcpyAsync(&h, c.small, sizeof(Small), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        for (int ch = 0; ch < 5; ++ch) out->F[ch] = h.fhist[ch];
+        slow = h.skip != 0;  // a redundant dummy sink: rows must be compacted
+    }
+    if (slow) {
+        reset_small(c);
         const uint64_t tiles = ceil_div(M, 1024);
         uint32_t desc_ep;
         uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
@@ -769,6 +796,10 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
         const char *sortenv = getenv("MTG_SORT");
         c->ctx.use_lsd = sortenv && std::string(sortenv) == "lsd";
+        const char *dsortenv = getenv("MTG_DUMMY_SORT");
+        c->ctx.dummy_msd = dsortenv && std::string(dsortenv) == "msd";
+        const char *emitenv = getenv("MTG_EMIT");
+        c->ctx.emit_slow = emitenv && std::string(emitenv) == "slow";
         c->ctx.debug = getenv("MTG_DEBUG") != nullptr;
     } catch (const std::exception &e) {
         set_error(e.what());

@@ -155,3 +155,14 @@ def test_device_build_matches_host_build():
         assert t.n_rows == dc.n and t.total_ms > 0
     finally:
         L.mtg_device_free(d)
+
+
+@pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_DUMMY_SORT": "msd"},
+                                 {"MTG_SORT": "lsd"}])
+def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
+    # the compacting emit kernel, the MSD dummy sort and the LSD sorts stay bit-exact too
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    for k, canonical, bits in [(19, True, 8), (30, False, 0), (40, True, 16), (3, False, 8)]:
+        check(k, transcripts_1000[:400], canonical, bits)
+    check(5, CONSTRUCT_SEQS, True, 8)
