@@ -100,9 +100,9 @@ typedef struct mtg_boss_timings {
     double dummy_ms;             /* K5/K6 incl. dummy sort + unique */
     double merge_ms;             /* K7 */
     double emit_ms;              /* K8 */
-    double radix_pass_ms;        /* average onesweep launch over the real-k-mer sorts (K2, K4) */
-    double radix_bytes;          /* average algorithmic bytes per such launch: 2 n (key+payload) */
-    uint64_t radix_launches;     /* onesweep launches of those sorts */
+    double radix_pass_ms;        /* K2's first partition pass (MSD) or average onesweep pass (LSD) */
+    double radix_bytes;          /* algorithmic bytes of that launch: 2 n (key + count) */
+    uint64_t radix_launches;     /* launches averaged into radix_pass_ms */
     uint64_t n_positions;        /* window starts offered to the extractor */
     uint64_t n_extracted;        /* valid k-mers extracted (N) */
     uint64_t n_unique;           /* distinct k-mers collected (U) */

@@ -59,16 +59,21 @@ __global__ __launch_bounds__(256) void extract_kernel(
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts,
     uint64_t n_reads, uint32_t cmax, Key<L> *__restrict__ out_keys,
     uint32_t *__restrict__ out_counts, uint32_t *__restrict__ tcnt,
-    const uint64_t *__restrict__ toff) {
+    const uint64_t *__restrict__ toff, uint32_t *__restrict__ hist, unsigned hist_bits) {
+    // hist: when hist_bits > 0, counts of the top hist_bits (<= 9) bits of the 2K-bit keys
+    // written (the first MSD level's histogram, so the sort skips its own histogram pass)
     using T = ExtractTraits<L>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
     __shared__ uint8_t s_code[TILE + T::MAXK];
     __shared__ Key<L> s_out[COUNT_ONLY ? 1 : TILE];
     __shared__ uint32_t s_cnt[COUNTED && !COUNT_ONLY ? TILE : 1];
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    __shared__ uint32_t s_hist[COUNT_ONLY ? 1 : 512];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t tile = blockIdx.x;
+    if (!COUNT_ONLY && hist_bits)
+        for (uint32_t i = tid; i < (1u << hist_bits); i += BLOCK) s_hist[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
     const uint64_t base = (uint64_t)tile * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
@@ -154,8 +159,15 @@ __global__ __launch_bounds__(256) void extract_kernel(
     __syncthreads();
     const uint64_t gb = toff[tile];
     for (uint32_t i = tid; i < tile_total; i += BLOCK) {
-        out_keys[gb + i] = s_out[i];
+        const Key<L> key = s_out[i];
+        out_keys[gb + i] = key;
         if (COUNTED) out_counts[gb + i] = s_cnt[i];
+        if (hist_bits) atomicAdd(&s_hist[bits_at(key, 2 * K - hist_bits, hist_bits)], 1u);
+    }
+    if (hist_bits) {
+        __syncthreads();
+        for (uint32_t i = tid; i < (1u << hist_bits); i += BLOCK)
+            if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
     }
 }
 
@@ -298,6 +310,33 @@ __global__ __launch_bounds__(256) void rc_augment_kernel(Key<L> *keys, uint32_t 
             if (COUNTED) rc_counts[o] = c[j];
             ++o;
         }
+    }
+}
+
+// K4 for odd K (no palindromes): rc_out[i] = rc(keys[i]), counts carried along; with hist_bits,
+// also the histogram of the top hist_bits bits of the rc keys (the rc sort's first MSD level)
+template <int L, bool COUNTED>
+__global__ __launch_bounds__(256) void rc_map_kernel(const Key<L> *__restrict__ keys,
+                                                     const uint32_t *__restrict__ counts,
+                                                     Key<L> *__restrict__ rc_out,
+                                                     uint32_t *__restrict__ rc_counts, uint64_t n,
+                                                     unsigned K, uint32_t *__restrict__ hist,
+                                                     unsigned hist_bits) {
+    __shared__ uint32_t s_hist[512];
+    if (hist_bits)
+        for (uint32_t i = threadIdx.x; i < (1u << hist_bits); i += 256) s_hist[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const Key<L> r = revcomp2(keys[i], K);
+        rc_out[i] = r;
+        if (COUNTED) rc_counts[i] = counts[i];
+        if (hist_bits) atomicAdd(&s_hist[bits_at(r, 2 * K - hist_bits, hist_bits)], 1u);
+    }
+    if (hist_bits) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < (1u << hist_bits); i += 256)
+            if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
     }
 }
 

@@ -42,7 +42,7 @@ class Workspace {
     enum Slot {
         SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
         FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, MSD_COUNTS, MSD_BSTART,
-        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, NSLOTS
+        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -120,6 +120,8 @@ struct Ctx {
     uint64_t radix_launches = 0;
     bool track_partition = false;  // time the msd_partition launches of the real-k-mer sorts
     bool use_lsd = false;          // MTG_SORT=lsd: LSD onesweep + unique instead of MSD
+    bool part_vec = false;         // MTG_PART_VEC=1: 16-byte partition I/O (measured slower)
+    unsigned max_digit = MSD_DBITS;  // MTG_DIGIT_BITS: widest partition digit
     bool emit_slow = false;        // MTG_EMIT=slow: always the compacting emit kernel
     bool dummy_msd = false;        // MTG_DUMMY_SORT=msd: MSD for the dummy k-mers (default LSD:
                                    // their $-padded keys crowd a few top-digit buckets)
@@ -228,29 +230,54 @@ __global__ void set_pair_kernel(uint64_t *p, uint64_t a, uint64_t b) {
 // copies per distinct key, used only to plan the partition depth; a wrong guess costs time,
 // never correctness (overflowing groups take another level or the LSD fallback).
 // Result: sorted distinct keys in *keys (counts in *vals); returns their number.
+struct MsdPlan {
+    unsigned levels;
+    unsigned digit_end[4];  // cumulative significant bits after each level
+};
+
+// partition depth: enough top bits T that an average final bucket holds <= LIMIT/3 distinct
+// keys (canonical k-mers are up to 2x denser at small prefixes), in levels of <= max_digit
+// bits (one full read + scatter each)
+template <int L>
+static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
+    constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
+    const unsigned dmax = c.max_digit;
+    unsigned T = 0;
+    while (T < nbits && T < 3 * dmax && (double)n / dup / (double)(1ull << T) > (double)LIMIT / 3)
+        ++T;
+    MsdPlan p{};
+    p.levels = (T + dmax - 1) / dmax;
+    for (unsigned l = 1; l <= p.levels; ++l) p.digit_end[l] = T * l / p.levels;
+    return p;
+}
+
 template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
-                                double dup) {
+                                double dup, const uint32_t *hist1 = nullptr) {
+    // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them
     if (n == 0) return 0;
     constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
     constexpr int TILE = MsdTraits<L>::TILE;
     const uint64_t tiles = ceil_div(n, TILE);
-    // levels: until an average bucket holds ~LIMIT/2 distinct keys
-    unsigned levels = 0;
-    while (levels < 3 && 8 * levels < nbits &&
-           (double)n / dup / (double)(1ull << (8 * levels)) > (double)LIMIT)
-        ++levels;
+    const MsdPlan plan = msd_plan<L>(c, n, nbits, dup);
+    unsigned levels = plan.levels;
+    unsigned digit_end[4] = {plan.digit_end[0], plan.digit_end[1], plan.digit_end[2], plan.digit_end[3]};
     unsigned b = 0;
     uint64_t *bstart = nullptr;
     uint64_t nbuckets = 1;
     auto run_level = [&](unsigned lev) {
-        const unsigned bb = std::min(nbits, 8 * lev), bp = std::min(nbits, 8 * (lev - 1));
+        if (digit_end[lev] == 0) digit_end[lev] = std::min(nbits, digit_end[lev - 1] + 8);
+        const unsigned bb = digit_end[lev], bp = digit_end[lev - 1];
         nbuckets = 1ull << bb;
-        uint32_t *cnt = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nbuckets * 4);
-        HIP_CHECK(hipMemsetAsync(cnt, 0, nbuckets * 4, c.stream));
-        msd_hist_kernel<L><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, cnt);
-        HIP_CHECK(hipGetLastError());
+        const uint32_t *cnt = hist1;
+        if (lev != 1 || !hist1) {
+            uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nbuckets * 4);
+            HIP_CHECK(hipMemsetAsync(h, 0, nbuckets * 4, c.stream));
+            msd_hist_kernel<L><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, h);
+            HIP_CHECK(hipGetLastError());
+            cnt = h;
+        }
         bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nbuckets + 1) * 8);
         uint32_t ep;
         const uint64_t st = ceil_div(nbuckets, 4096);
@@ -263,11 +290,23 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
         EventTimer tm(c.stream);
         tm.mark();
-        msd_partition_kernel<L, COUNTED><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
-            *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
+        if (!COUNTED && bb - bp > 8) {  // wide digits: 1024-thread tiles keep the bucket runs long
+            if constexpr (!COUNTED) {
+                constexpr int TILE2 = MsdTraits<L>::ITEMS * 1024;
+                msd_partition_kernel<L, false, false, 1024><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
+                                                              c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits,
+                                                                          bb, bp, cur);
+            }
+        } else if (c.part_vec) {
+            msd_partition_kernel<L, COUNTED, true><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
+                *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
+        } else {
+            msd_partition_kernel<L, COUNTED, false><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
+                *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
+        }
         HIP_CHECK(hipGetLastError());
         tm.mark();
-        if (c.track_partition) {
+        if (c.track_partition && lev == 1) {
             HIP_CHECK(hipStreamSynchronize(c.stream));
             c.radix_ms += tm.ms(0, 1);
             c.radix_launches += 1;
@@ -366,7 +405,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                         ++shown;
                     }
             }
-            if (ovf_keys * 20 > n && levels < 3 && 8 * levels < nbits) {
+            if (ovf_keys * 20 > n && levels < 3 && digit_end[levels] < nbits) {
                 run_level(++levels);  // many overflows: one more level for everything
                 continue;
             }
@@ -498,17 +537,38 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, npos * 4) : nullptr;
     uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, npos * 4) : nullptr;
     uint64_t N = 0;
-    reset_small(c);
+    uint32_t *hist1 = nullptr;
+    unsigned hist_bits = 0;
     if (npos) {
         constexpr int TILE = ExtractTraits<L2>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
-        uint32_t desc_ep;
-        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
-        extract_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts,
-            in.n_reads, cmax, ka, ca, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
+        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
+        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
+        extract_kernel<L2, COUNTED, true><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax,
+            nullptr, nullptr, tcnt, nullptr, nullptr, 0);
         HIP_CHECK(hipGetLastError());
-        N = read_u64(c, &c.small->total);
+        uint32_t ep;
+        const uint64_t st = ceil_div(tiles, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(
+            tcnt, tiles, toff, desc, ep, &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        N = read_u64(c, (const unsigned long long *)(toff + tiles));
+        // the first MSD level's histogram comes out of the write launch
+        if (!c.use_lsd) {
+            const MsdPlan plan = msd_plan<L2>(c, N, 2 * K, 8.0);
+            if (plan.levels) {
+                hist_bits = plan.digit_end[1];
+                hist1 = (uint32_t *)c.ws.get(Workspace::HIST1, (1u << hist_bits) * 4);
+                HIP_CHECK(hipMemsetAsync(hist1, 0, (1u << hist_bits) * 4, c.stream));
+            }
+        }
+        extract_kernel<L2, COUNTED, false><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax,
+            ka, ca, nullptr, toff, hist1, hist_bits);
+        HIP_CHECK(hipGetLastError());
     }
     T.n_extracted = N;
     const int ev_extract = tm.mark();
@@ -546,7 +606,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         std::swap(ca, cb);
     } else {
         c.track_partition = true;
-        U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, 8.0);
+        U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, 8.0, hist1);
         c.track_partition = false;
         ev_sort = tm.mark();
     }
@@ -558,21 +618,37 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     // on its own (no duplicates) and merged with it
     uint64_t R = U;
     if (canonical && U) {
-        reset_small(c);
-        const uint64_t tiles = ceil_div(U, 1024);
-        uint32_t desc_ep;
-        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
-        rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            ka, ca, kb, cb, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total,
-            &c.small->error);
-        HIP_CHECK(hipGetLastError());
-        uint64_t Urc = read_u64(c, &c.small->total);
+        uint64_t Urc = U;
+        uint32_t *rc_hist = nullptr;
+        unsigned rc_hist_bits = 0;
+        if (K & 1) {
+            // odd K: no k-mer is its own reverse complement, every rc(x) is kept in place
+            if (!c.use_lsd) {
+                const MsdPlan plan = msd_plan<L2>(c, U, 2 * K, 1.0);
+                if (plan.levels) {
+                    rc_hist_bits = plan.digit_end[1];
+                    rc_hist = (uint32_t *)c.ws.get(Workspace::HIST1, (1u << rc_hist_bits) * 4);
+                    HIP_CHECK(hipMemsetAsync(rc_hist, 0, (1u << rc_hist_bits) * 4, c.stream));
+                }
+            }
+            rc_map_kernel<L2, COUNTED><<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256 * 4), 16384)),
+                                         dim3(256), 0, c.stream>>>(ka, ca, kb, cb, U, K, rc_hist, rc_hist_bits);
+            HIP_CHECK(hipGetLastError());
+        } else {
+            reset_small(c);
+            const uint64_t tiles = ceil_div(U, 1024);
+            uint32_t desc_ep;
+            uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
+            rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+                ka, ca, kb, cb, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total,
+                &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            Urc = read_u64(c, &c.small->total);
+        }
         K2 *ra = kb, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
         uint32_t *rca = cb, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
-        c.track_partition = true;
-        if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, true);
-        else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0);
-        c.track_partition = false;
+        if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
+        else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist);
         R = U + Urc;
         K2 *real = (K2 *)c.ws.get(Workspace::REAL, R * sizeof(K2));
         uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, R * 4) : nullptr;
@@ -798,6 +874,10 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         c->ctx.use_lsd = sortenv && std::string(sortenv) == "lsd";
         const char *dsortenv = getenv("MTG_DUMMY_SORT");
         c->ctx.dummy_msd = dsortenv && std::string(dsortenv) == "msd";
+        const char *pv = getenv("MTG_PART_VEC");
+        c->ctx.part_vec = pv && std::string(pv) == "1";
+        const char *db = getenv("MTG_DIGIT_BITS");
+        if (db) c->ctx.max_digit = std::max(1, std::min(MSD_DBITS, atoi(db)));
         const char *emitenv = getenv("MTG_EMIT");
         c->ctx.emit_slow = emitenv && std::string(emitenv) == "slow";
         c->ctx.debug = getenv("MTG_DEBUG") != nullptr;

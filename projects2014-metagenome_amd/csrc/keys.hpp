@@ -165,21 +165,28 @@ MTG_HD uint32_t char_at(const Key<L> &a, unsigned i, unsigned bits_per_char) {
     return bits_at(a, i * bits_per_char, bits_per_char);
 }
 
+// reverse the order of the 32 2-bit groups of a word
+MTG_HD inline uint64_t reverse_pairs64(uint64_t v) {
+    v = __builtin_bswap64(v);
+    v = ((v >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((v & 0x0F0F0F0F0F0F0F0Full) << 4);
+    v = ((v >> 2) & 0x3333333333333333ull) | ((v & 0x3333333333333333ull) << 2);
+    return v;
+}
+
 // reverse complement of a tight 2-bit BOSS-layout (K)-mer (kmer_transform.hpp:14-35):
 // label <- comp(a_1), pos 1 <- comp(a_K), pos i <- comp(a_{K+1-i})
 template <int L>
 MTG_HD Key<L> revcomp2(const Key<L> &x, unsigned K) {
     // plain layout P = a_1 at bits 0..1, ..., a_K at the top; the BOSS word is P rotated by
     // one char: boss = ((P & low(2(K-1))) << 2) | (P >> 2(K-1)).  rc in plain layout
-    // reverses char order and complements (3 - c).
-    // BOSS -> plain: P = (boss >> 2) | ((boss & 3) << 2(K-1))
-    Key<L> P = shr(x, 2) | shl(Key<L>::from(x.w[0] & 3), 2 * (K - 1));
-    // reverse 2-bit groups of the low 2K bits, complement
-    Key<L> R = Key<L>::zero();
-    for (unsigned i = 0; i < K; ++i) {
-        uint64_t c = 3 - bits_at(P, 2 * i, 2);
-        R = R | shl(Key<L>::from(c), 2 * (K - 1 - i));
-    }
+    // reverses the char order and complements (3 - c = c ^ 3): complement all bits, reverse the
+    // 2-bit groups of the whole L-limb word, and shift the K chars back down.
+    const Key<L> P = shr(x, 2) | shl(Key<L>::from(x.w[0] & 3), 2 * (K - 1));
+    const Key<L> C = ~P;
+    Key<L> R;
+#pragma unroll
+    for (int i = 0; i < L; ++i) R.w[i] = reverse_pairs64(C.w[L - 1 - i]);
+    R = shr(R, 64 * L - 2 * K);
     return shl(R & Key<L>::lowmask(2 * (K - 1)), 2) | shr(R, 2 * (K - 1));
 }
 

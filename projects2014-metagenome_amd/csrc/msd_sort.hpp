@@ -22,7 +22,8 @@
 namespace mtg {
 
 constexpr int MSD_BLOCK = 512;
-constexpr int MSD_WIN = 2;  // previous-level segments a tile keeps in its LDS window
+constexpr int MSD_WIN = 2;    // previous-level segments a tile keeps in its LDS window
+constexpr int MSD_DBITS = 9;  // widest digit of one partition level
 
 template <int L>
 struct MsdTraits {
@@ -47,20 +48,33 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
                                                              unsigned b, unsigned bp,
                                                              uint32_t *__restrict__ counts) {
     constexpr int TILE = MsdTraits<L>::TILE;
-    constexpr int WMAX = MSD_WIN * 256;
+    constexpr int WMAX = MSD_WIN << 8;
     __shared__ uint32_t s_cnt[WMAX];
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
     const unsigned sub = b - bp;
-    const uint32_t wsize = MSD_WIN << sub;
+    const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
     for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
     const uint32_t wbase = key_prefix(keys[base], nbits, bp) << sub;
     __syncthreads();
     const uint64_t end = min(n, base + TILE);
-    for (uint64_t i = base + threadIdx.x; i < end; i += MSD_BLOCK) {
-        const uint32_t bucket = key_prefix(keys[i], nbits, b);
+    auto add = [&](const Key<L> &key) {
+        const uint32_t bucket = key_prefix(key, nbits, b);
         const uint32_t lb = bucket - wbase;
         if (lb < wsize) atomicAdd(&s_cnt[lb], 1u);
         else atomicAdd(&counts[bucket], 1u);
+    };
+    if constexpr (L == 1) {  // 16-byte loads: two keys per lane
+        for (uint64_t i = base + 2 * threadIdx.x; i < end; i += 2 * MSD_BLOCK) {
+            if (i + 1 < end) {
+                const ulonglong2 v = *(const ulonglong2 *)(keys + i);
+                add(Key<L>::from(v.x));
+                add(Key<L>::from(v.y));
+            } else {
+                add(keys[i]);
+            }
+        }
+    } else {
+        for (uint64_t i = base + threadIdx.x; i < end; i += MSD_BLOCK) add(keys[i]);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK)
@@ -107,44 +121,76 @@ __global__ __launch_bounds__(512) void scan_counts_kernel(const uint32_t *__rest
  * and each run is written contiguously.  Keys outside the tile's LDS window (tiles spanning
  * more than MSD_WIN tiny segments) take one atomic each.
  */
-template <int L, bool HAS_VAL>
-__global__ __launch_bounds__(MSD_BLOCK) void msd_partition_kernel(
+template <int L, bool HAS_VAL, bool VEC = false, int BLOCK = MSD_BLOCK>
+__global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
-    unsigned long long *__restrict__ cursor) {
+    unsigned long long *__restrict__ cursor, unsigned cstride = 1) {
     constexpr int ITEMS = MsdTraits<L>::ITEMS;
-    constexpr int TILE = MsdTraits<L>::TILE;
-    constexpr int WMAX = MSD_WIN * 256;
+    constexpr int TILE = ITEMS * BLOCK;
+    constexpr int WMAX = MSD_WIN << 8;
     __shared__ Key<L> s_keys[TILE];
     __shared__ uint32_t s_vals[HAS_VAL ? TILE : 1];
     __shared__ uint32_t s_cnt[WMAX];
     __shared__ uint32_t s_loff[WMAX];
     __shared__ unsigned long long s_gbase[WMAX];
-    __shared__ uint32_t s_scan[MSD_BLOCK / 64 + 1];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
 
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
     const unsigned sub = b - bp;
-    const uint32_t wsize = MSD_WIN << sub;
-    for (int i = tid; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
+    const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
+    for (int i = tid; i < (int)wsize; i += BLOCK) s_cnt[i] = 0;
     const uint32_t wbase = key_prefix(kin[base], nbits, bp) << sub;
     __syncthreads();
 
     Key<L> k[ITEMS];
     uint32_t v[ITEMS];
     uint32_t r[ITEMS];
+    // L == 1: lane tid loads keys (2 tid, 2 tid + 1) of each 2 * BLOCK span as one 16-byte
+    // load (order inside a tile is irrelevant to the partition)
+    constexpr bool PAIR = L == 1 && VEC;
+    bool have[ITEMS];
+    if constexpr (PAIR) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; j += 2) {
+            const uint64_t i = base + 2 * ((uint64_t)(j / 2) * BLOCK + tid);
+            have[j] = i < n;
+            have[j + 1] = i + 1 < n;
+            if (i + 1 < n) {
+                const ulonglong2 kv = *(const ulonglong2 *)(kin + i);
+                k[j] = Key<L>::from(kv.x);
+                k[j + 1] = Key<L>::from(kv.y);
+                if (HAS_VAL) {
+                    const uint2 vv = *(const uint2 *)(vin + i);
+                    v[j] = vv.x;
+                    v[j + 1] = vv.y;
+                }
+            } else if (i < n) {
+                k[j] = kin[i];
+                if (HAS_VAL) v[j] = vin[i];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t i = base + (uint64_t)j * BLOCK + tid;
+            have[j] = i < n;
+            if (i < n) {
+                k[j] = kin[i];
+                if (HAS_VAL) v[j] = vin[i];
+            }
+        }
+    }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-        const uint64_t i = base + (uint64_t)j * MSD_BLOCK + tid;
         r[j] = 0xFFFFFFFFu;
-        if (i < n) {
-            k[j] = kin[i];
-            if (HAS_VAL) v[j] = vin[i];
+        if (have[j]) {
             const uint32_t lb = key_prefix(k[j], nbits, b) - wbase;
             if (lb < wsize) {
                 r[j] = atomicAdd(&s_cnt[lb], 1u);
             } else {  // outside the window: reserve and write directly
-                const unsigned long long o = atomicAdd(&cursor[lb + wbase], 1ull);
+                const unsigned long long o = atomicAdd(&cursor[(size_t)(lb + wbase) * cstride], 1ull);
                 kout[o] = k[j];
                 if (HAS_VAL) vout[o] = v[j];
             }
@@ -152,7 +198,7 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_partition_kernel(
     }
     __syncthreads();
     // exclusive scan of the window counts (wsize <= 1024: two per thread)
-    constexpr int PER = WMAX / MSD_BLOCK;
+    constexpr int PER = WMAX / BLOCK > 0 ? WMAX / BLOCK : 1;
     uint32_t c[PER];
     uint32_t sum = 0;
 #pragma unroll
@@ -162,13 +208,13 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_partition_kernel(
         sum += c[q];
     }
     uint32_t total;
-    uint32_t off = block_exclusive_sum<MSD_BLOCK>(sum, s_scan, &total);
+    uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
         if (i < wsize) {
             s_loff[i] = off;
-            s_gbase[i] = c[q] ? atomicAdd(&cursor[wbase + i], (unsigned long long)c[q]) : 0;
+            s_gbase[i] = c[q] ? atomicAdd(&cursor[(size_t)(wbase + i) * cstride], (unsigned long long)c[q]) : 0;
         }
         off += c[q];
     }
@@ -183,12 +229,29 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_partition_kernel(
         }
     }
     __syncthreads();
-    for (uint32_t p = tid; p < total; p += MSD_BLOCK) {
+    for (uint32_t p = tid; p < total; p += BLOCK) {
         const Key<L> key = s_keys[p];
         const uint32_t lb = key_prefix(key, nbits, b) - wbase;
         const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
-        kout[o] = key;
-        if (HAS_VAL) vout[o] = s_vals[p];
+        if constexpr (PAIR) {
+            // 16-byte stores at even output slots: the lane at an even slot writes its key and
+            // the next one of the run; an odd slot is written alone only at the run's start
+            if (o & 1) {
+                if (p == s_loff[lb]) {
+                    kout[o] = key;
+                    if (HAS_VAL) vout[o] = s_vals[p];
+                }
+            } else if (p + 1 < s_loff[lb] + s_cnt[lb]) {
+                *(ulonglong2 *)(kout + o) = make_ulonglong2(key.w[0], s_keys[p + 1].w[0]);
+                if (HAS_VAL) *(uint2 *)(vout + o) = make_uint2(s_vals[p], s_vals[p + 1]);
+            } else {
+                kout[o] = key;
+                if (HAS_VAL) vout[o] = s_vals[p];
+            }
+        } else {
+            kout[o] = key;
+            if (HAS_VAL) vout[o] = s_vals[p];
+        }
     }
 }
 
@@ -317,23 +380,45 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
 
         bool ovf = false;
         uint32_t mynew = 0;  // distinct keys this thread inserted (summed once per thread)
-        // keys are loaded BATCH at a time per thread so the global loads overlap
-        constexpr int BATCH = 8;
-        for (uint64_t ib = g0 + tid; ib < g1 && !ovf; ib += 512 * BATCH) {
-            Key<L> kb[BATCH];
-            uint32_t vb[BATCH];
+        // keys are loaded BATCH at a time per thread so the global loads overlap; 8-byte keys
+        // as 16-byte pairs from the even index at or below g0
+        constexpr int PAIR = L == 1 ? 2 : 1;
+        constexpr int BATCH = 8 / PAIR;
+        const uint64_t a0 = PAIR == 2 ? (g0 & ~1ull) : g0;
+        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += 512ull * BATCH * PAIR) {
+            Key<L> kb[BATCH * PAIR];
+            uint32_t vb[BATCH * PAIR];
+            bool hv[BATCH * PAIR];
 #pragma unroll
             for (int q = 0; q < BATCH; ++q) {
-                const uint64_t i = ib + (uint64_t)q * 512;
-                if (i < g1) {
-                    kb[q] = keys[i];
-                    if (COUNTED) vb[q] = vals[i];
+                const uint64_t i = ib + (uint64_t)q * 512 * PAIR;
+                if constexpr (PAIR == 2) {
+                    hv[2 * q] = i >= g0 && i < g1;
+                    hv[2 * q + 1] = i + 1 < g1;
+                    if (i + 1 < g1) {
+                        const ulonglong2 kv = *(const ulonglong2 *)(keys + i);
+                        kb[2 * q] = Key<L>::from(kv.x);
+                        kb[2 * q + 1] = Key<L>::from(kv.y);
+                        if (COUNTED) {
+                            const uint2 vv = *(const uint2 *)(vals + i);
+                            vb[2 * q] = vv.x;
+                            vb[2 * q + 1] = vv.y;
+                        }
+                    } else if (i < g1 && i >= g0) {
+                        kb[2 * q] = keys[i];
+                        if (COUNTED) vb[2 * q] = vals[i];
+                    }
+                } else {
+                    hv[q] = i < g1;
+                    if (i < g1) {
+                        kb[q] = keys[i];
+                        if (COUNTED) vb[q] = vals[i];
+                    }
                 }
             }
 #pragma unroll
-            for (int q = 0; q < BATCH; ++q) {
-                const uint64_t i = ib + (uint64_t)q * 512;
-                if (i >= g1 || ovf) continue;
+            for (int q = 0; q < BATCH * PAIR; ++q) {
+                if (!hv[q] || ovf) continue;
                 const Key<L> key = kb[q];
                 if (sbits && bits_at(key, sshift, sbits) != slice) continue;
                 uint32_t h = key_hash(key) & (SLOTS - 1);

@@ -1,0 +1,53 @@
+"""Summarise a run_pmc.sh output directory into profiles/: per-kernel HBM bytes per launch.
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  The 8-byte-lane copy of a known byte count calibrates the
+counters at the partition pass's access width (MI355X_MICROARCH.md: FETCH_SIZE reports half of
+a wide streaming read; WRITE_SIZE is exact for streaming stores).
+Usage: python tools/pmc_summary.py gpurun_out/<tag> <out_prefix>
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+d, prefix = sys.argv[1], sys.argv[2]
+
+
+def load(kind, ctr):
+    rows = list(csv.DictReader(open("%s/%s_%s/run_counter_collection.csv" % (d, kind, ctr))))
+    out = []
+    for r in rows:
+        name = r["Kernel_Name"]
+        name = name[:name.index("(")] if "(" in name else name
+        out.append((name.replace("void ", ""), int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024))
+    return out
+
+
+KNOWN = 1200000000 * 8
+cf = load("calib", "FETCH_SIZE")[0][2]
+cw = load("calib", "WRITE_SIZE")[0][2]
+fetch_scale, write_scale = KNOWN / cf, KNOWN / cw
+bf, bw = load("bench", "FETCH_SIZE"), load("bench", "WRITE_SIZE")
+rows = []
+for (n1, g1, f), (n2, g2, w) in zip(bf, bw):
+    assert n1 == n2 and g1 == g2
+    rows.append({"kernel": n1, "grid": g1, "read_bytes": f * fetch_scale, "write_bytes": w * write_scale})
+lines = ["# HBM traffic per launch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
+         "",
+         "Calibration: 8-byte-lane copy of %.2f GB: FETCH_SIZE x %.3f, WRITE_SIZE x %.3f." %
+         (KNOWN / 1e9, fetch_scale, write_scale),
+         "Workload: bench.py --steps 1 --warmup 0 (k=31 canonical, 10 M reads); one launch each.",
+         "",
+         "| kernel | grid | read GB | write GB | total GB |", "|---|---|---|---|---|"]
+for r in rows:
+    lines.append("| %s | %d | %.3f | %.3f | %.3f |" % (r["kernel"], r["grid"], r["read_bytes"] / 1e9,
+                                                    r["write_bytes"] / 1e9,
+                                                    (r["read_bytes"] + r["write_bytes"]) / 1e9))
+open(prefix + "_pmc_traffic.md", "w").write("\n".join(lines) + "\n")
+part = [r for r in rows if r["kernel"].startswith("mtg::msd_partition_kernel<1, false, false, 512>")][0]
+json.dump({"kernel": part["kernel"], "hbm_bytes_per_launch": part["read_bytes"] + part["write_bytes"],
+           "read_bytes": part["read_bytes"], "write_bytes": part["write_bytes"],
+           "fetch_scale": fetch_scale, "write_scale": write_scale,
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (run_pmc.sh), calibrated by copy8_kernel"},
+          open(prefix + "_partition_traffic.json", "w"), indent=1)
+print("\n".join(lines))
