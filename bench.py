@@ -115,6 +115,22 @@ def cpu_baseline(args, kb):
                          args.k, args.mode, dt, len(c.W))}
 
 
+def max_over_ranks(elapsed, world, device):
+    """The job's time is the slowest rank's (tests/test_distributed.py runs this over gloo)."""
+    if world <= 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_throughput(kmers_per_rank, world, steps, elapsed):
+    """Whole-job k-mers/s: every rank processes kmers_per_rank per step (weak scaling)."""
+    return kmers_per_rank * world * steps / elapsed
+
+
 def main():
     args = parse()
     import torch
@@ -158,14 +174,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, device)
     kmers_per_rank = args.reads * (args.read_len - args.k + 1)
-    value = kmers_per_rank * world * args.steps / elapsed
+    value = job_throughput(kmers_per_rank, world, args.steps, elapsed)
     last = timings[-1]
     # size-independent sanity of the result
     assert dc.n == last["n_rows"] and dc.n == 1 + dc.n_real + dc.n_dummy
