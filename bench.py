@@ -220,7 +220,7 @@ def main():
                    "parallelism": "replicas" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "msd_partition_kernel<1,false,false,512> (K2 level-1 partition)",
+                     "kernel": "msd_partition_kernel (K2 first MSD partition pass)",
                      "pass_ms": pass_ms, "bytes_per_launch": pass_bytes},
         "stages_ms": {k2: last[k2] for k2 in ("extract_ms", "sort_ms", "unique_ms", "rc_ms",
                                               "dummy_ms", "merge_ms", "emit_ms", "total_ms")},

@@ -609,7 +609,12 @@ __device__ __forceinline__ uint64_t merge_split(const Key<LA> *__restrict__ a, u
     return lo;
 }
 
-constexpr int MERGE_TILE = 2048;
+// outputs per merge workgroup: the two staged runs and the output image fit 32 KB of LDS, so
+// several workgroups share a CU and hide the loads
+template <int LO>
+struct MergeTraits {
+    static constexpr int TILE = LO == 1 ? 2048 : LO == 2 ? 1024 : 512;
+};
 
 // diagonal split of every tile boundary (one thread each, all in flight together)
 template <int LO, int LA, bool LIFT>
@@ -618,7 +623,7 @@ __global__ void merge_partition_kernel(const Key<LA> *__restrict__ a, uint64_t n
                                        uint64_t ntiles, uint64_t *__restrict__ splits) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
-    const uint64_t diag = min(na + nb, t * MERGE_TILE);
+    const uint64_t diag = min(na + nb, t * (uint64_t)MergeTraits<LO>::TILE);
     splits[t] = merge_split<LO, LA, LIFT>(a, na, b, nb, diag, K);
 }
 
@@ -630,7 +635,7 @@ __global__ __launch_bounds__(256) void merge_kernel(const Key<LA> *__restrict__ 
                                                     unsigned K, const uint64_t *__restrict__ splits,
                                                     Key<LO> *__restrict__ out,
                                                     uint32_t *__restrict__ oc, uint64_t off) {
-    constexpr int ITEMS = MERGE_TILE / 256, TILE = MERGE_TILE;
+    constexpr int TILE = MergeTraits<LO>::TILE, ITEMS = TILE / 256;
     __shared__ Key<LO> s_in[TILE];
     __shared__ Key<LO> s_out[TILE];
     __shared__ uint32_t s_cin[COUNTED ? TILE : 1];

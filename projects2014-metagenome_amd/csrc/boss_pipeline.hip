@@ -15,6 +15,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mtg_boss.h"
@@ -42,7 +43,7 @@ class Workspace {
     enum Slot {
         SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
         FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, MSD_COUNTS, MSD_BSTART,
-        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, NSLOTS
+        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -122,6 +123,8 @@ struct Ctx {
     bool use_lsd = false;          // MTG_SORT=lsd: LSD onesweep + unique instead of MSD
     bool part_vec = false;         // MTG_PART_VEC=1: 16-byte partition I/O (measured slower)
     unsigned max_digit = MSD_DBITS;  // MTG_DIGIT_BITS: widest partition digit
+    bool small_table = true;       // MTG_SMALL_TABLE=0: full-size LDS tables in local unique
+    double plan_div = 2.5;         // MTG_PLAN_DIV: planned distinct keys per bucket = LIMIT / div
     bool emit_slow = false;        // MTG_EMIT=slow: always the compacting emit kernel
     bool dummy_msd = false;        // MTG_DUMMY_SORT=msd: MSD for the dummy k-mers (default LSD:
                                    // their $-padded keys crowd a few top-digit buckets)
@@ -240,10 +243,10 @@ struct MsdPlan {
 // bits (one full read + scatter each)
 template <int L>
 static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
-    constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
+    const double LIMIT = (double)LocalTraits<L>::LIMIT / (c.small_table ? 2 : 1);
     const unsigned dmax = c.max_digit;
     unsigned T = 0;
-    while (T < nbits && T < 3 * dmax && (double)n / dup / (double)(1ull << T) > (double)LIMIT / 3)
+    while (T < nbits && T < 3 * dmax && (double)n / dup / (double)(1ull << T) > LIMIT / c.plan_div)
         ++T;
     MsdPlan p{};
     p.levels = (T + dmax - 1) / dmax;
@@ -274,7 +277,16 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         if (lev != 1 || !hist1) {
             uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nbuckets * 4);
             HIP_CHECK(hipMemsetAsync(h, 0, nbuckets * 4, c.stream));
-            msd_hist_kernel<L><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, h);
+            if (bp == 0 && nbuckets <= 512) {
+                const uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, 8192);
+                uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbuckets * 4);
+                msd_hist_rows_kernel<L><<<dim3(nrows), dim3(512), 0, c.stream>>>(*keys, n, nbits, bb, rows);
+                HIP_CHECK(hipGetLastError());
+                hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbuckets, 256)),
+                                          dim3(256), 0, c.stream>>>(rows, nrows, (uint32_t)nbuckets, h);
+            } else {
+                msd_hist_kernel<L><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, h);
+            }
             HIP_CHECK(hipGetLastError());
             cnt = h;
         }
@@ -320,7 +332,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
 
     while (true) {
         // groups of consecutive buckets holding <= G keys; bigger buckets stand alone
-        const uint64_t G = LIMIT / 2;
+        const uint64_t G = (c.small_table ? LIMIT / 2 : LIMIT) / 2;
         uint64_t ngroups = 1;
         uint64_t *gstart;
         if (b == 0) {
@@ -353,14 +365,23 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
         auto launch_local = [&](const uint32_t *glist, uint64_t count, unsigned sbits) {
             HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-            if (L == 1 && nbits < 64)
-                local_unique_kernel<L, COUNTED, true><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
+            auto go = [&](auto keycas, auto sl) {
+                constexpr bool KC = decltype(keycas)::value;
+                constexpr int SL = decltype(sl)::value;
+                local_unique_kernel<L, COUNTED, KC, 512, SL><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
                     *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt,
                     COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax);
-            else
-                local_unique_kernel<L, COUNTED, false><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
-                    *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt,
-                    COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax);
+            };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            using SFull = std::integral_constant<int, LocalTraits<L>::SLOTS>;
+            using SHalf = std::integral_constant<int, LocalTraits<L>::SLOTS / 2>;
+            const bool keycas = L == 1 && nbits < 64;
+            if (c.small_table) {
+                if (keycas) go(T_{}, SHalf{}); else go(F_{}, SHalf{});
+            } else {
+                if (keycas) go(T_{}, SFull{}); else go(F_{}, SFull{});
+            }
             HIP_CHECK(hipGetLastError());
             uint32_t nov = 0;
             HIP_CHECK(hipMemcpyAsync(&nov, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
@@ -503,7 +524,7 @@ template <int LO, int LA, bool LIFT, bool COUNTED, bool BCOUNTS>
 static void merge_sorted(Ctx &c, const Key<LA> *a, const uint32_t *ac, uint64_t na,
                          const Key<LO> *b, const uint32_t *bc, uint64_t nb, unsigned K,
                          Key<LO> *out, uint32_t *oc, uint64_t off) {
-    const uint64_t ntiles = ceil_div(na + nb, MERGE_TILE);
+    const uint64_t ntiles = ceil_div(na + nb, MergeTraits<LO>::TILE);
     if (!ntiles) return;
     uint64_t *splits = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
     merge_partition_kernel<LO, LA, LIFT><<<dim3((unsigned)ceil_div(ntiles + 1, 256)), dim3(256), 0, c.stream>>>(
@@ -556,15 +577,6 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
             tcnt, tiles, toff, desc, ep, &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
         N = read_u64(c, (const unsigned long long *)(toff + tiles));
-        // the first MSD level's histogram comes out of the write launch
-        if (!c.use_lsd) {
-            const MsdPlan plan = msd_plan<L2>(c, N, 2 * K, 8.0);
-            if (plan.levels) {
-                hist_bits = plan.digit_end[1];
-                hist1 = (uint32_t *)c.ws.get(Workspace::HIST1, (1u << hist_bits) * 4);
-                HIP_CHECK(hipMemsetAsync(hist1, 0, (1u << hist_bits) * 4, c.stream));
-            }
-        }
         extract_kernel<L2, COUNTED, false><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
             in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax,
             ka, ca, nullptr, toff, hist1, hist_bits);
@@ -878,6 +890,10 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         c->ctx.part_vec = pv && std::string(pv) == "1";
         const char *db = getenv("MTG_DIGIT_BITS");
         if (db) c->ctx.max_digit = std::max(1, std::min(MSD_DBITS, atoi(db)));
+        const char *stenv = getenv("MTG_SMALL_TABLE");
+        c->ctx.small_table = !(stenv && atoi(stenv) == 0);
+        const char *pdenv = getenv("MTG_PLAN_DIV");
+        if (pdenv) c->ctx.plan_div = std::max(1.0, atof(pdenv));
         const char *emitenv = getenv("MTG_EMIT");
         c->ctx.emit_slow = emitenv && std::string(emitenv) == "slow";
         c->ctx.debug = getenv("MTG_DEBUG") != nullptr;

@@ -82,6 +82,51 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
 }
 
 /*
+ * First-level histogram (bp = 0, at most 512 buckets): every workgroup counts a grid-stride
+ * share of the keys in LDS and stores its row rows[block][bucket]; hist_rows_reduce_kernel adds
+ * the rows.  No global atomics on the few bucket words (thousands of workgroups adding to the
+ * same 256 words serialise at the memory-side atomic unit).
+ */
+template <int L>
+__global__ __launch_bounds__(512) void msd_hist_rows_kernel(const Key<L> *__restrict__ keys,
+                                                            uint64_t n, unsigned nbits, unsigned b,
+                                                            uint32_t *__restrict__ rows) {
+    __shared__ uint32_t s_h[512];
+    const uint32_t nb = 1u << b;
+    for (uint32_t i = threadIdx.x; i < nb; i += 512) s_h[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 512;
+    if constexpr (L == 1) {  // 16-byte loads: two keys per lane
+        for (uint64_t p = (uint64_t)blockIdx.x * 512 + threadIdx.x; 2 * p < n; p += stride) {
+            const uint64_t i = 2 * p;
+            if (i + 1 < n) {
+                const ulonglong2 v = *(const ulonglong2 *)(keys + i);
+                atomicAdd(&s_h[key_prefix(Key<L>::from(v.x), nbits, b)], 1u);
+                atomicAdd(&s_h[key_prefix(Key<L>::from(v.y), nbits, b)], 1u);
+            } else {
+                atomicAdd(&s_h[key_prefix(keys[i], nbits, b)], 1u);
+            }
+        }
+    } else {
+        for (uint64_t i = (uint64_t)blockIdx.x * 512 + threadIdx.x; i < n; i += stride)
+            atomicAdd(&s_h[key_prefix(keys[i], nbits, b)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += 512) rows[(uint64_t)blockIdx.x * nb + i] = s_h[i];
+}
+
+// out[bin] += sum of rows[r][bin] over this block's slice of rows (out zeroed by the caller)
+__global__ __launch_bounds__(256) void hist_rows_reduce_kernel(const uint32_t *__restrict__ rows,
+                                                               uint32_t nrows, uint32_t nb,
+                                                               uint32_t *__restrict__ out) {
+    const uint32_t bin = blockIdx.y * 256 + threadIdx.x;
+    if (bin >= nb) return;
+    uint32_t sum = 0;
+    for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) sum += rows[(uint64_t)r * nb + bin];
+    if (sum) atomicAdd(&out[bin], sum);
+}
+
+/*
  * Exclusive scan of u32 counts into u64 starts (starts[n] = total), chained by a wave
  * look-back over tiles of 4096 entries.
  */
@@ -325,15 +370,15 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  *   3. Keys (and counts) go to tmp[gstart[g] + slot]; ucount[g] = D.
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
-template <int L, bool COUNTED, bool KEYCAS>
-__global__ __launch_bounds__(512) void local_unique_kernel(
+template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS>
+__global__ __launch_bounds__(LB) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
     unsigned b, unsigned sbits, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
     uint32_t *__restrict__ ucount, uint32_t *__restrict__ overflow, uint32_t *__restrict__ novf,
     uint32_t cmax) {
-    constexpr int SLOTS = LocalTraits<L>::SLOTS;
-    constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
+    constexpr int SLOTS = SL;
+    constexpr uint32_t LIMIT = SL / 2;
     constexpr uint64_t EMPTY = ~0ull;
     __shared__ Key<L> s_key[SLOTS];
     __shared__ uint32_t s_state[KEYCAS ? 1 : SLOTS];
@@ -341,7 +386,7 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_fill[256];
     __shared__ uint32_t s_distinct;
-    __shared__ uint32_t s_scan[512 / 64 + 1];
+    __shared__ uint32_t s_scan[LB / 64 + 1];
     __shared__ int s_hb;
 
     const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
@@ -363,7 +408,7 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
     }
     uint64_t out_off = 0;
     for (uint32_t slice = 0; slice < (1u << sbits); ++slice) {
-        for (int i = tid; i < SLOTS; i += 512) {
+        for (int i = tid; i < SLOTS; i += LB) {
             if (KEYCAS) s_key[i].w[0] = EMPTY;
             else s_state[i] = 0;
             if (COUNTED) s_sum[i] = 0;
@@ -383,15 +428,15 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
         // keys are loaded BATCH at a time per thread so the global loads overlap; 8-byte keys
         // as 16-byte pairs from the even index at or below g0
         constexpr int PAIR = L == 1 ? 2 : 1;
-        constexpr int BATCH = 8 / PAIR;
+        constexpr int BATCH = (LB >= 1024 ? 12 : 8) / PAIR;
         const uint64_t a0 = PAIR == 2 ? (g0 & ~1ull) : g0;
-        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += 512ull * BATCH * PAIR) {
+        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += (uint64_t)LB * BATCH * PAIR) {
             Key<L> kb[BATCH * PAIR];
             uint32_t vb[BATCH * PAIR];
             bool hv[BATCH * PAIR];
 #pragma unroll
             for (int q = 0; q < BATCH; ++q) {
-                const uint64_t i = ib + (uint64_t)q * 512 * PAIR;
+                const uint64_t i = ib + (uint64_t)q * LB * PAIR;
                 if constexpr (PAIR == 2) {
                     hv[2 * q] = i >= g0 && i < g1;
                     hv[2 * q + 1] = i + 1 < g1;
@@ -472,7 +517,7 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
         const uint32_t D = s_distinct;
 
         // compact occupied slots to s_key[0..D) / s_sum[0..D)
-        constexpr int PER = SLOTS / 512;
+        constexpr int PER = SLOTS / LB;
         Key<L> kk[PER];
         uint32_t ss[PER];
         uint32_t mine = 0, occ = 0;
@@ -486,7 +531,7 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
             mine += o;
         }
         uint32_t tot;
-        uint32_t o = block_exclusive_sum<512>(mine, s_scan, &tot);
+        uint32_t o = block_exclusive_sum<LB>(mine, s_scan, &tot);
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             if (occ & (1u << q)) {
@@ -516,7 +561,7 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
         const unsigned dshift = hb >= 7 ? (unsigned)(hb - 7) : 0u;
         Key<L> *scratch = s_key + LIMIT;  // free half of the table
         uint32_t *sscr = COUNTED ? s_sum + LIMIT : nullptr;
-        for (uint32_t i = tid; i < D; i += 512) atomicAdd(&s_hist[bits_at(s_key[i], dshift, 8)], 1u);
+        for (uint32_t i = tid; i < D; i += LB) atomicAdd(&s_hist[bits_at(s_key[i], dshift, 8)], 1u);
         __syncthreads();
         if (tid < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
             const uint32_t c0 = s_hist[4 * tid], c1 = s_hist[4 * tid + 1], c2 = s_hist[4 * tid + 2],
@@ -529,14 +574,14 @@ __global__ __launch_bounds__(512) void local_unique_kernel(
             s_hist[4 * tid + 3] = bb + c0 + c1 + c2;
         }
         __syncthreads();
-        for (uint32_t i = tid; i < D; i += 512) {
+        for (uint32_t i = tid; i < D; i += LB) {
             const uint32_t d = bits_at(s_key[i], dshift, 8);
             const uint32_t p = s_hist[d] + atomicAdd(&s_fill[d], 1u);
             scratch[p] = s_key[i];
             if (COUNTED) sscr[p] = s_sum[i];
         }
         __syncthreads();
-        for (uint32_t p = tid; p < D; p += 512) {
+        for (uint32_t p = tid; p < D; p += LB) {
             const Key<L> key = scratch[p];
             const uint32_t d = bits_at(key, dshift, 8);
             const uint32_t b0 = s_hist[d], b1 = b0 + s_fill[d];

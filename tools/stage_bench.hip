@@ -79,6 +79,40 @@ __global__ void gen_random(Key<1> *keys, uint64_t n, unsigned bits, int mode) {
     }
 }
 
+// histogram variants over the top 8 of 62 bits: mode 0 read only, 1 block-shared LDS atomics,
+// 2 per-wave LDS copies, 3 per-wave copies of 16-bit packed pairs
+template <int MODE>
+__global__ __launch_bounds__(512) void hist_variant(const Key<1> *__restrict__ keys, uint64_t n,
+                                                    uint32_t *__restrict__ out) {
+    __shared__ uint32_t s_h[8 * 256];
+    for (int i = threadIdx.x; i < 8 * 256; i += 512) s_h[i] = 0;
+    __syncthreads();
+    const uint32_t w = threadIdx.x / 64;
+    uint32_t acc = 0;
+    const uint64_t base = (uint64_t)blockIdx.x * 8192;
+    const uint64_t end = min(n, base + 8192);
+    for (uint64_t i = base + 2 * threadIdx.x; i < end; i += 1024) {
+        const ulonglong2 v = *(const ulonglong2 *)(keys + i);
+        const uint32_t b0 = (uint32_t)(v.x >> 54), b1 = (uint32_t)(v.y >> 54);
+        if (MODE == 0) acc += b0 + b1;
+        if (MODE == 1) { atomicAdd(&s_h[b0], 1u); atomicAdd(&s_h[b1], 1u); }
+        if (MODE == 2) { atomicAdd(&s_h[w * 256 + b0], 1u); atomicAdd(&s_h[w * 256 + b1], 1u); }
+        if (MODE == 3) {
+            atomicAdd(&s_h[w * 128 + (b0 >> 1)], 1u << (16 * (b0 & 1)));
+            atomicAdd(&s_h[w * 128 + (b1 >> 1)], 1u << (16 * (b1 & 1)));
+        }
+    }
+    __syncthreads();
+    if (MODE == 0) { if (acc == 0xFFFFFFFF) out[0] = acc; return; }
+    if (threadIdx.x < 256) {
+        uint32_t c = 0;
+        if (MODE == 1) c = s_h[threadIdx.x];
+        if (MODE == 2) for (int q = 0; q < 8; ++q) c += s_h[q * 256 + threadIdx.x];
+        if (MODE == 3) for (int q = 0; q < 8; ++q) c += (s_h[q * 128 + threadIdx.x / 2] >> (16 * (threadIdx.x & 1))) & 0xFFFF;
+        out[(uint64_t)blockIdx.x * 256 + threadIdx.x] = c;
+    }
+}
+
 // level-1 MSD partition of n random keys: histogram, host scan, partition with cursor strides
 static void partition_bench(hipStream_t s, uint64_t n) {
     Key<1> *a, *b;
@@ -91,6 +125,18 @@ static void partition_bench(hipStream_t s, uint64_t n) {
     const uint64_t tiles = ceil_div(n, MsdTraits<1>::TILE);
     for (int mode = 1; mode < 2; ++mode) {
         gen_random<<<8192, 256, 0, s>>>(a, n, 62, mode);
+        {
+            uint32_t *rows;
+            HIP_CHECK(hipMalloc(&rows, tiles * 256 * 4));
+            float th[4];
+            th[0] = time_ms(s, 3, [&] { hist_variant<0><<<dim3((unsigned)tiles), dim3(512), 0, s>>>(a, n, rows); });
+            th[1] = time_ms(s, 3, [&] { hist_variant<1><<<dim3((unsigned)tiles), dim3(512), 0, s>>>(a, n, rows); });
+            th[2] = time_ms(s, 3, [&] { hist_variant<2><<<dim3((unsigned)tiles), dim3(512), 0, s>>>(a, n, rows); });
+            th[3] = time_ms(s, 3, [&] { hist_variant<3><<<dim3((unsigned)tiles), dim3(512), 0, s>>>(a, n, rows); });
+            printf("hist variants (read-only, shared, per-wave, per-wave packed): %.3f %.3f %.3f %.3f ms\n",
+                   th[0], th[1], th[2], th[3]);
+            HIP_CHECK(hipFree(rows));
+        }
         float t = time_ms(s, 3, [&] {
             HIP_CHECK(hipMemsetAsync(cnt, 0, 256 * 4, s));
             msd_hist_kernel<1><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, s>>>(a, n, 62, 8, 0, cnt);
@@ -139,6 +185,52 @@ static void partition_bench(hipStream_t s, uint64_t n) {
     HIP_CHECK(hipFree(b));
 }
 
+// reads of 150 random ACGT + '$' (151-byte stride)
+__global__ void gen_reads(uint8_t *seq, uint64_t len) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        seq[i] = i % 151 == 150 ? '$' : "ACGT"[splitmix(i) & 3];
+}
+
+static void extract_bench(hipStream_t s, uint64_t reads) {
+    const uint64_t len = reads * 151;
+    const unsigned K = 31;
+    uint8_t *seq;
+    HIP_CHECK(hipMalloc(&seq, len + 64));
+    gen_reads<<<8192, 256, 0, s>>>(seq, len);
+    const uint64_t npos = len - K + 1;
+    constexpr int TILE = ExtractTraits<1>::TILE;
+    const uint64_t tiles = ceil_div(npos, TILE);
+    uint32_t *tcnt, *hist, *rows;
+    uint64_t *toff;
+    Key<1> *out;
+    HIP_CHECK(hipMalloc(&tcnt, tiles * 4));
+    HIP_CHECK(hipMalloc(&toff, (tiles + 1) * 8));
+    HIP_CHECK(hipMalloc(&hist, 512 * 4));
+    HIP_CHECK(hipMalloc(&rows, tiles * 256 * 4));
+    HIP_CHECK(hipMalloc(&out, npos * 8));
+    float t = time_ms(s, 3, [&] {
+        extract_kernel<1, false, true><<<dim3((unsigned)tiles), dim3(256), 0, s>>>(
+            seq, len, K, 1, nullptr, nullptr, 0, 255, nullptr, nullptr, tcnt, nullptr, nullptr, 0);
+    });
+    printf("extract count: %.3f ms\n", t);
+    std::vector<uint32_t> h(tiles);
+    HIP_CHECK(hipMemcpy(h.data(), tcnt, tiles * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> o(tiles + 1, 0);
+    for (uint64_t i = 0; i < tiles; ++i) o[i + 1] = o[i] + h[i];
+    HIP_CHECK(hipMemcpy(toff, o.data(), (tiles + 1) * 8, hipMemcpyHostToDevice));
+    const double bytes = len + o[tiles] * 8.0;
+    t = time_ms(s, 3, [&] {
+        extract_kernel<1, false, false><<<dim3((unsigned)tiles), dim3(256), 0, s>>>(
+            seq, len, K, 1, nullptr, nullptr, 0, 255, out, nullptr, nullptr, toff, nullptr, 0);
+    });
+    printf("extract write: %.3f ms = %.0f GB/s (%lu k-mers)\n", t, bytes / 1e9 / (t * 1e-3),
+           (unsigned long)o[tiles]);
+    HIP_CHECK(hipFree(seq));
+    HIP_CHECK(hipFree(out));
+    HIP_CHECK(hipFree(rows));
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "calib") {
         // one 8-byte-lane copy of 1.2e9 words (9.6 GB read + 9.6 GB written)
@@ -156,6 +248,7 @@ int main(int argc, char **argv) {
     const unsigned K = 31;
     hipStream_t s;
     HIP_CHECK(hipStreamCreate(&s));
+    extract_bench(s, 10000000ull);
     partition_bench(s, 1200000000ull);
     Key<1> *keys, *tmp;
     HIP_CHECK(hipMalloc(&keys, R * 8 + 64));
