@@ -257,8 +257,9 @@ static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
 template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
-                                double dup, const uint32_t *hist1 = nullptr) {
-    // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them
+                                double dup, const uint32_t *hist1 = nullptr, bool distinct = false) {
+    // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them;
+    // distinct: the input has no duplicates (the local pass skips its hash table)
     if (n == 0) return 0;
     constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
     constexpr int TILE = MsdTraits<L>::TILE;
@@ -365,10 +366,11 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
         auto launch_local = [&](const uint32_t *glist, uint64_t count, unsigned sbits) {
             HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-            auto go = [&](auto keycas, auto sl) {
+            auto go = [&](auto keycas, auto sl, auto nodup) {
                 constexpr bool KC = decltype(keycas)::value;
                 constexpr int SL = decltype(sl)::value;
-                local_unique_kernel<L, COUNTED, KC, 512, SL><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
+                constexpr bool ND = decltype(nodup)::value;
+                local_unique_kernel<L, COUNTED, KC, 512, SL, ND><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
                     *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt,
                     COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax);
             };
@@ -377,10 +379,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             using SFull = std::integral_constant<int, LocalTraits<L>::SLOTS>;
             using SHalf = std::integral_constant<int, LocalTraits<L>::SLOTS / 2>;
             const bool keycas = L == 1 && nbits < 64;
-            if (c.small_table) {
-                if (keycas) go(T_{}, SHalf{}); else go(F_{}, SHalf{});
+            if (distinct) {
+                if (c.small_table) go(F_{}, SHalf{}, T_{}); else go(F_{}, SFull{}, T_{});
+            } else if (c.small_table) {
+                if (keycas) go(T_{}, SHalf{}, F_{}); else go(F_{}, SHalf{}, F_{});
             } else {
-                if (keycas) go(T_{}, SFull{}); else go(F_{}, SFull{});
+                if (keycas) go(T_{}, SFull{}, F_{}); else go(F_{}, SFull{}, F_{});
             }
             HIP_CHECK(hipGetLastError());
             uint32_t nov = 0;
@@ -660,7 +664,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         K2 *ra = kb, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
         uint32_t *rca = cb, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
         if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
-        else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist);
+        else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true);
         R = U + Urc;
         K2 *real = (K2 *)c.ws.get(Workspace::REAL, R * sizeof(K2));
         uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, R * 4) : nullptr;

@@ -370,7 +370,8 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  *   3. Keys (and counts) go to tmp[gstart[g] + slot]; ucount[g] = D.
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
-template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS>
+template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
+          bool NODUP = false>
 __global__ __launch_bounds__(LB) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
@@ -408,10 +409,12 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
     }
     uint64_t out_off = 0;
     for (uint32_t slice = 0; slice < (1u << sbits); ++slice) {
-        for (int i = tid; i < SLOTS; i += LB) {
-            if (KEYCAS) s_key[i].w[0] = EMPTY;
-            else s_state[i] = 0;
-            if (COUNTED) s_sum[i] = 0;
+        if (!NODUP) {
+            for (int i = tid; i < SLOTS; i += LB) {
+                if (KEYCAS) s_key[i].w[0] = EMPTY;
+                else s_state[i] = 0;
+                if (COUNTED) s_sum[i] = 0;
+            }
         }
         if (tid < 256) {
             s_hist[tid] = 0;
@@ -460,6 +463,30 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
                         if (COUNTED) vb[q] = vals[i];
                     }
                 }
+            }
+            if constexpr (NODUP) {
+                // distinct input (the rc set): append the slice's keys, positions by wave ballot
+                const uint32_t lane = __lane_id();
+#pragma unroll
+                for (int q = 0; q < BATCH * PAIR; ++q) {
+                    const bool act = hv[q] && (!sbits || bits_at(kb[q], sshift, sbits) == slice);
+                    const uint64_t m = __ballot(act);
+                    if (!m) continue;
+                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
+                    uint32_t wb = 0;
+                    if (lane == leader) wb = atomicAdd(&s_distinct, (uint32_t)__popcll(m));
+                    wb = __shfl(wb, leader, 64);
+                    const uint32_t pos = wb + (uint32_t)__popcll(m & lanemask_lt());
+                    if (act) {
+                        if (pos < LIMIT) {
+                            s_key[pos] = kb[q];
+                            if (COUNTED) s_sum[pos] = vb[q];
+                        } else {
+                            ovf = true;
+                        }
+                    }
+                }
+                continue;
             }
 #pragma unroll
             for (int q = 0; q < BATCH * PAIR; ++q) {
@@ -516,6 +543,21 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
         }
         const uint32_t D = s_distinct;
 
+        if constexpr (NODUP) {
+            // already compact: highest differing bit over s_key[0..D)
+            if (D) {
+                const Key<L> ref = s_key[0];
+                int hb_local = -1;
+                for (uint32_t i = tid; i < D; i += LB) {
+                    Key<L> dx;
+#pragma unroll
+                    for (int w = 0; w < L; ++w) dx.w[w] = s_key[i].w[w] ^ ref.w[w];
+                    hb_local = max(hb_local, key_msb(dx));
+                }
+                if (hb_local >= 0) atomicMax(&s_hb, hb_local);
+            }
+            __syncthreads();
+        } else {
         // compact occupied slots to s_key[0..D) / s_sum[0..D)
         constexpr int PER = SLOTS / LB;
         Key<L> kk[PER];
@@ -557,6 +599,7 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
             if (hb_local >= 0) atomicMax(&s_hb, hb_local);
         }
         __syncthreads();
+        }
         const int hb = s_hb;
         const unsigned dshift = hb >= 7 ? (unsigned)(hb - 7) : 0u;
         Key<L> *scratch = s_key + LIMIT;  // free half of the table

@@ -13,7 +13,7 @@ using namespace mtg;
 
 template <int L, bool COUNTED>
 static int check(Ctx &c, uint64_t n, unsigned nbits, int dupf, uint32_t seed, bool skew,
-                 double hint_mult = 1.0) {
+                 double hint_mult = 1.0, bool distinct = false) {
     std::mt19937_64 rng(seed);
     const uint64_t m = std::max<uint64_t>(1, n / dupf);
     std::vector<Key<L>> base(m);
@@ -30,9 +30,20 @@ static int check(Ctx &c, uint64_t n, unsigned nbits, int dupf, uint32_t seed, bo
     }
     std::vector<Key<L>> h(n);
     std::vector<uint32_t> hv(n);
-    for (uint64_t i = 0; i < n; ++i) {
-        h[i] = base[rng() % m];
-        hv[i] = (uint32_t)(rng() % 300);
+    if (distinct) {  // a shuffled duplicate-free input (the rc sort's contract)
+        std::sort(base.begin(), base.end(), [](auto &x, auto &y) { return x < y; });
+        base.erase(std::unique(base.begin(), base.end(), [](auto &x, auto &y) { return x == y; }),
+                   base.end());
+        std::shuffle(base.begin(), base.end(), rng);
+        n = base.size();
+        h.assign(base.begin(), base.end());
+        hv.resize(n);
+        for (uint64_t i = 0; i < n; ++i) hv[i] = (uint32_t)(rng() % 300);
+    } else {
+        for (uint64_t i = 0; i < n; ++i) {
+            h[i] = base[rng() % m];
+            hv[i] = (uint32_t)(rng() % 300);
+        }
     }
     // expected
     std::vector<std::pair<Key<L>, uint64_t>> e;
@@ -60,7 +71,8 @@ static int check(Ctx &c, uint64_t n, unsigned nbits, int dupf, uint32_t seed, bo
     HIP_CHECK(hipMemcpy(va, hv.data(), n * 4, hipMemcpyHostToDevice));
     Key<L> *ka = a, *kb = b;
     uint32_t *pa = va, *pb = vb;
-    uint64_t u = msd_sort_unique<L, COUNTED>(c, &ka, &kb, &pa, &pb, n, nbits, cmax, dupf * hint_mult);
+    uint64_t u = msd_sort_unique<L, COUNTED>(c, &ka, &kb, &pa, &pb, n, nbits, cmax, dupf * hint_mult,
+                                             nullptr, distinct);
     std::vector<Key<L>> got(u);
     std::vector<uint32_t> gc(u);
     HIP_CHECK(hipMemcpy(got.data(), ka, u * sizeof(Key<L>), hipMemcpyDeviceToHost));
@@ -109,6 +121,16 @@ int main() {
             fails += check<1, false>(c, n, 62, 1, 1 + runs, true, hint); ++runs;
             fails += check<1, true>(c, n, 62, 2, 1 + runs, true, hint); ++runs;
             fails += check<2, false>(c, n / 4, 93, 1, 1 + runs, true, hint); ++runs;
+        }
+    // duplicate-free inputs through the local pass without hash tables (rc sort), incl. skew
+    for (uint64_t n : {1ull, 50ull, 5000ull, 300000ull, 3000000ull, 20000000ull})
+        for (unsigned nbits : {20u, 40u, 62u}) {
+            fails += check<1, false>(c, n, nbits, 1, 1 + runs, runs & 1, 1.0, true); ++runs;
+            fails += check<1, true>(c, n, nbits, 1, 1 + runs, runs & 1, 1.0, true); ++runs;
+        }
+    for (uint64_t n : {1000ull, 1000000ull})
+        for (unsigned nbits : {66u, 126u}) {
+            fails += check<2, false>(c, n, nbits, 1, 1 + runs, false, 1.0, true); ++runs;
         }
     printf("msd_test: %d / %d failed\n", fails, runs);
     return fails ? 1 : 0;
