@@ -489,9 +489,39 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     }
 }
 
-// dummies emitted by edge i: a sink, and a source with its k - 1 higher levels
-__device__ __forceinline__ uint32_t dummy_emits(uint32_t f, uint32_t in, uint32_t k) {
-    return (f & 1u) + ((f >> 1) & ~in & 1u) * k;
+// the 16 flag bytes of edges i0 .. i0 + 15 (i0 a multiple of 16; zero past n)
+__device__ __forceinline__ void load_flags16(const uint8_t *__restrict__ f, uint64_t i0, uint64_t n,
+                                             uint32_t (&w)[4]) {
+    if (i0 + 16 <= n) {
+        const uint4 v = *(const uint4 *)(f + i0);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[q] = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+                if (i0 + 4 * q + bb < n) w[q] |= (uint32_t)f[i0 + 4 * q + bb] << (8 * bb);
+        }
+    }
+}
+
+// sinks (low 16 bits) and sources (high 16 bits) among edges i0 .. i0 + 15, bit j = edge i0 + j
+__device__ __forceinline__ uint32_t dummy_masks16(const uint8_t *__restrict__ flags,
+                                                  const uint8_t *__restrict__ in_flag, uint64_t i0,
+                                                  uint64_t n) {
+    uint32_t fw[4], iw[4];
+    load_flags16(flags, i0, n, fw);
+    load_flags16(in_flag, i0, n, iw);
+    uint32_t sink = 0, src = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t f = (fw[j / 4] >> (8 * (j % 4))) & 0xFFu;
+        const uint32_t in = (iw[j / 4] >> (8 * (j % 4))) & 0xFFu;
+        sink |= (f & 1u) << j;
+        src |= ((f >> 1) & ~in & 1u) << j;
+    }
+    return sink | src << 16;
 }
 
 // K6a: per-tile dummy counts (WTILE edges per workgroup, 16 consecutive per thread)
@@ -501,10 +531,8 @@ __global__ __launch_bounds__(256) void dummy_count_kernel(const uint8_t *__restr
                                                           uint32_t *__restrict__ tcnt) {
     __shared__ uint32_t s_scan[256 / 64 + 1];
     const uint64_t i0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-        if (i0 + j < n) cnt += dummy_emits(flags[i0 + j], in_flag[i0 + j], k);
+    const uint32_t m = dummy_masks16(flags, in_flag, i0, n);
+    const uint32_t cnt = __popc(m & 0xFFFFu) + __popc(m >> 16) * k;
     uint32_t total;
     block_exclusive_sum<256>(cnt, s_scan, &total);
     if (threadIdx.x == 0) tcnt[blockIdx.x] = total;
@@ -525,10 +553,12 @@ __device__ __forceinline__ Key<LO> lift_fast(const Key<LI> &x, unsigned K) {
 }
 
 /*
- * K6b (write pass): emit the lifted dummy k-mers in edge order at the offsets of the scanned
- * tile counts: a sink as lift(to_next(x,0)) with its label char cleared to $ (:94), a source as
- * lift(to_prev(x,0)) with char 1 cleared to $ (:165) followed by its k-1 higher levels
- * to_prev(., $) (:286-303).  Only edges that emit are re-read.
+ * K6b (write pass): the workgroup's dummies go to its range of the scanned tile counts -- order
+ * inside it is free, the dummies are sorted next.  Sinks first: lift(to_next(x,0)) with the label
+ * char cleared to $ (:94), one per sink edge, by its owner thread.  Then every (source, level)
+ * pair is an independent item spread over the whole workgroup: level 1 is lift(to_prev(x,0))
+ * with char 1 cleared to $ (:165); level 1 + j is its j-fold to_prev(., $) (:286-303), in closed
+ * form (node chars shifted up j places, label = the level-1 word's char K - j).
  */
 template <int L2, int L3>
 __global__ __launch_bounds__(256) void dummy_write_kernel(
@@ -536,42 +566,42 @@ __global__ __launch_bounds__(256) void dummy_write_kernel(
     const uint8_t *__restrict__ in_flag, uint64_t n, unsigned K,
     const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out) {
     __shared__ uint32_t s_scan[256 / 64 + 1];
-    const uint64_t i0 = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    __shared__ uint16_t s_src[4096];  // tile-relative edge index of each source
+    const uint32_t tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 4096;
+    const uint64_t i0 = t0 + tid * 16;
     const unsigned k = K - 1;
-    uint32_t e[16];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        e[j] = i0 + j < n ? dummy_emits(flags[i0 + j], in_flag[i0 + j], k) : 0;
-        cnt += e[j];
-    }
-    uint32_t tile_total;
-    const uint32_t off = block_exclusive_sum<256>(cnt, s_scan, &tile_total);
-    if (!cnt) return;
-    uint64_t o = toff[blockIdx.x] + off;
+    const uint32_t m = dummy_masks16(flags, in_flag, i0, n);
+    // one scan of packed (sinks, sources): both fit 13 bits per tile
+    const uint32_t packed = __popc(m & 0xFFFFu) | (uint32_t)__popc(m >> 16) << 16;
+    uint32_t total;
+    const uint32_t off = block_exclusive_sum<256>(packed, s_scan, &total);
+    const uint32_t nsink = total & 0xFFFFu, nsrc = total >> 16;
+    if (!nsink && !nsrc) return;
+    const uint64_t base = toff[blockIdx.x];
+    uint32_t so = off & 0xFFFFu, qo = off >> 16;
     const Key<L2> full = Key<L2>::lowmask(2 * K);
     const Key<L3> full3 = Key<L3>::lowmask(3 * K);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        if (!e[j]) continue;
-        const Key<L2> x = keys[i0 + j];
-        const uint32_t f = flags[i0 + j];
-        if (f & 1) {
+        if ((m >> j) & 1u) {
+            const Key<L2> x = keys[i0 + j];
             const Key<L2> t = (shr(x, 2) | shl(Key<L2>::from(x.w[0] & 3), 2 * (K - 1))) &
                               ~Key<L2>::from(3);
-            out[o++] = lift_fast<L3>(t, K) & ~Key<L3>::from(7);
+            out[base + so++] = lift_fast<L3>(t, K) & ~Key<L3>::from(7);
         }
-        if ((f >> 1) & ~(uint32_t)in_flag[i0 + j] & 1u) {
-            const Key<L2> prev = (shl(x & ~Key<L2>::from(3), 2) & full) | shr(x, 2 * (K - 1));
-            Key<L3> d = lift_fast<L3>(prev, K) & ~Key<L3>::from(7 << 3);
-            out[o++] = d;
-            for (unsigned lev = 2; lev <= k; ++lev) {
-                // KMerBOSS<., 3>::to_prev(K, $) -- kmer_boss.hpp:171-186
-                const Key<L3> last_char = shr(d, 3 * (K - 1));
-                d = (shl(d & ~Key<L3>::from(7), 3) & full3) | last_char;
-                out[o++] = d;
-            }
-        }
+        if ((m >> (16 + j)) & 1u) s_src[qo++] = (uint16_t)(tid * 16 + j);
+    }
+    __syncthreads();
+    Key<L3> *o = out + base + nsink;
+    for (uint32_t it = tid; it < nsrc * k; it += 256) {
+        const uint32_t q = it / k, lev = it - q * k;
+        const Key<L2> x = keys[t0 + s_src[q]];
+        const Key<L2> prev = (shl(x & ~Key<L2>::from(3), 2) & full) | shr(x, 2 * (K - 1));
+        const Key<L3> d1 = lift_fast<L3>(prev, K) & ~Key<L3>::from(7 << 3);
+        o[it] = lev == 0 ? d1
+                         : (shl(d1 & ~Key<L3>::from(7), 3 * lev) & full3) |
+                               Key<L3>::from(char_at(d1, K - lev, 3));
     }
 }
 
