@@ -6,11 +6,15 @@ extract -> canonicalise -> sort -> unique -> reverse-complement augment -> dummy
 KMerBOSS<uint64_t> keys, canonical mode).  value = k-mer positions offered to the extractor
 (reads * (150 - k + 1)) / seconds, summed over ranks.
 
-Multi-GPU (torchrun, one rank per GPU): every rank builds its own read shard (seed + rank)
-as an independent replica ("scaling": "weak"); no collective is on the data path yet.
+Multi-GPU (torchrun, one rank per GPU): ONE build of all ranks' reads.  Every rank holds its
+own 10 M reads (weak scaling: "scaling": "weak"), all sampled from one shared genome, and
+returns the chunk of one range of BOSS order; the exchange steps (k-mers, sink / in-edge
+queries, dummy sources) run over RCCL on xGMI inside the timed step (libmtg_boss.so's own RCCL
+communicator; torch.distributed only bootstraps it and times the job).
 
-Synthetic data: a seeded random ACGT genome of reads*150/10 bases (10x coverage); reads start
-uniformly, strand 50/50, 0.1 % substitutions; each read is followed by a '$' separator.
+Synthetic data: a seeded random ACGT genome of (all ranks' reads)*150/10 bases (10x coverage);
+reads start uniformly, strand 50/50, 0.1 % substitutions; each read is followed by a '$'
+separator.
 """
 import argparse
 import ctypes
@@ -44,10 +48,12 @@ def parse():
     return ap.parse_args()
 
 
-def make_reads_device(torch, n_reads, read_len, seed, data, coverage, device):
-    """Reads + '$' separators as one uint8 tensor on `device` (ASCII ACGT)."""
+def make_reads_device(torch, n_reads, read_len, seed, data, coverage, device, world=1,
+                      genome_seed=999):
+    """Reads + '$' separators as one uint8 tensor on `device` (ASCII ACGT).  The genome is
+    shared by all `world` ranks (same seed, sized for all their reads); the reads are the
+    rank's own (`seed`)."""
     g = torch.Generator(device=device)
-    g.manual_seed(seed)
     lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=device)
     stride = read_len + 1
     out = torch.empty(n_reads * stride, dtype=torch.uint8, device=device)
@@ -55,8 +61,10 @@ def make_reads_device(torch, n_reads, read_len, seed, data, coverage, device):
     view[:, read_len] = ord("$")
     chunk = 1 << 20
     if data == "genome":
-        glen = max(int(n_reads * read_len / coverage), read_len + 1)
+        glen = max(int(world * n_reads * read_len / coverage), read_len + 1)
+        g.manual_seed(genome_seed)
         genome = torch.randint(0, 4, (glen,), dtype=torch.uint8, device=device, generator=g)
+    g.manual_seed(seed)
     ar = torch.arange(read_len, device=device)
     for r0 in range(0, n_reads, chunk):
         r1 = min(n_reads, r0 + chunk)
@@ -115,6 +123,14 @@ def cpu_baseline(args, kb):
                          args.k, args.mode, dt, len(c.W))}
 
 
+def share_comm_id(rank, make_id):
+    """Rank 0's 128-byte RCCL id, broadcast over the torch.distributed group."""
+    import torch.distributed as dist
+    obj = [make_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
 def max_over_ranks(elapsed, world, device):
     """The job's time is the slowest rank's (tests/test_distributed.py runs this over gloo)."""
     if world <= 1:
@@ -149,15 +165,19 @@ def main():
     boss = importlib.import_module("projects2014-metagenome_amd.boss")
     kb = args.k - 1
     seq = make_reads_device(torch, args.reads, args.read_len, 1000 + rank, args.data,
-                            args.coverage, device)
+                            args.coverage, device, world)
     torch.cuda.synchronize()
     ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=args.mode == "canonical",
                                                  bits_per_count=args.count_width,
                                                  device_id=local)
     stream = torch.cuda.current_stream(device).cuda_stream
+    comm = None
+    if world > 1:
+        uid = share_comm_id(rank, boss.Comm.unique_id)
+        comm = boss.Comm.rccl(uid, world, rank, local)
 
     def step():
-        return ctor.build_device(seq.data_ptr(), seq.numel(), stream=stream)
+        return ctor.build_device(seq.data_ptr(), seq.numel(), stream=stream, comm=comm)
 
     for _ in range(args.warmup):
         step()
@@ -217,7 +237,8 @@ def main():
                    "k": args.k, "reads_per_gpu": args.reads, "read_len": args.read_len,
                    "key": "KMerBOSS<uint64_t,2>" if 2 * args.k <= 64 else
                           "KMerBOSS<uint128_t,2>" if 2 * args.k <= 128 else "KMerBOSS<uint256_t,2>",
-                   "parallelism": "replicas" if world > 1 else "single"},
+                   "parallelism": ("range-partitioned build over %d GPUs (RCCL all-to-all)"
+                                   % world) if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "msd_partition_kernel (K2 first MSD partition pass)",
@@ -225,13 +246,15 @@ def main():
         "stages_ms": {k2: last[k2] for k2 in ("extract_ms", "sort_ms", "unique_ms", "rc_ms",
                                               "dummy_ms", "merge_ms", "emit_ms", "total_ms")},
         "counts": {k2: last[k2] for k2 in ("n_extracted", "n_unique", "n_real", "n_dummy",
-                                           "n_rows", "radix_launches")},
+                                           "n_rows", "radix_launches", "n_sent")},
+        "exchange_ms": last["exchange_ms"],
     }
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, kb)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        del comm
         dist.destroy_process_group()
 
 

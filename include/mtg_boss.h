@@ -22,6 +22,12 @@
  * multi-GPU shards): mtg_boss_build_device runs the whole path on a device buffer and leaves
  * the BOSS arrays in device memory; mtg_boss_last_timings reports per-stage device times.
  *
+ * Multi-GPU (one process per GPU, RCCL over xGMI): every rank calls the *_dist variant with its
+ * own reads and gets the chunk of one range of BOSS order; the rank chunks concatenate in rank
+ * order with BOSS::Chunk::extend (boss_chunk.cpp:230-270) into the chunk a single build of all
+ * reads returns.  This replaces the reference's suffix-sharded `build --suffix` +
+ * `concatenate` route (cli/build.cpp:106-148, 359-456) with one exchange-based build.
+ *
  * No torch types, no C++ types: plain pointers and sizes.  All functions are thread-safe
  * except that one constructor must not be built and added to at the same time.
  */
@@ -35,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 1
+#define MTG_BOSS_ABI_VERSION 2
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -109,6 +115,9 @@ typedef struct mtg_boss_timings {
     uint64_t n_real;             /* real edges after rc augmentation */
     uint64_t n_dummy;            /* dummy edges (sinks + all source levels) */
     uint64_t n_rows;             /* BOSS rows incl. row 0 */
+    double exchange_ms;          /* multi-GPU: time inside the exchanges (RCCL) */
+    uint64_t n_sent;             /* multi-GPU: elements sent to other ranks */
+    uint64_t world;              /* ranks of the build (1 = single GPU) */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);
@@ -142,6 +151,31 @@ int mtg_boss_build_device(mtg_boss_ctor *ctor, const uint8_t *d_seq, uint64_t se
                           uint64_t n_reads, void *stream, mtg_boss_device_chunk *out);
 
 int mtg_boss_last_timings(const mtg_boss_ctor *ctor, mtg_boss_timings *out);
+
+/*
+ * Multi-GPU exchange.  mtg_comm_get_unique_id on one rank, broadcast the 128 bytes (e.g. with
+ * torch.distributed or MPI), then mtg_comm_create_rccl on every rank with its device.
+ * mtg_comm_create_local makes `world` ranks inside one process sharing one device (each rank
+ * builds from its own host thread) -- the same exchange semantics without RCCL, for tests.
+ */
+#define MTG_COMM_ID_BYTES 128
+typedef struct mtg_comm mtg_comm;
+int mtg_comm_get_unique_id(uint8_t *id /* MTG_COMM_ID_BYTES */);
+mtg_comm *mtg_comm_create_rccl(const uint8_t *id, int world, int rank, int device_id);
+int mtg_comm_create_local(int world, mtg_comm **comms /* world entries */);
+void mtg_comm_destroy(mtg_comm *comm);
+int mtg_comm_rank(const mtg_comm *comm);
+int mtg_comm_size(const mtg_comm *comm);
+
+/* this rank's chunk of the global build (host input staged with mtg_boss_ctor_add_*) */
+int mtg_boss_ctor_build_chunk_dist(mtg_boss_ctor *ctor, mtg_comm *comm, mtg_boss_chunk *out);
+/* the same on device-resident reads */
+int mtg_boss_build_device_dist(mtg_boss_ctor *ctor, mtg_comm *comm, const uint8_t *d_seq,
+                               uint64_t seq_len, const uint64_t *d_read_starts,
+                               const uint32_t *d_counts, uint64_t n_reads, void *stream,
+                               mtg_boss_device_chunk *out);
+/* the range split: bounds[0..world] over n_prefixes buckets, balanced on hist (host) */
+int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64_t *bounds);
 
 /* device-memory helpers for callers without their own HIP runtime (ctypes, cgo, JNI) */
 void *mtg_device_alloc(int device_id, uint64_t bytes);

@@ -52,7 +52,9 @@ class Timings(ctypes.Structure):
                  "merge_ms", "emit_ms", "radix_pass_ms", "radix_bytes")] + \
                [(name, ctypes.c_uint64) for name in
                 ("radix_launches", "n_positions", "n_extracted", "n_unique", "n_real",
-                 "n_dummy", "n_rows")]
+                 "n_dummy", "n_rows")] + \
+               [("exchange_ms", ctypes.c_double), ("n_sent", ctypes.c_uint64),
+                ("world", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -64,7 +66,12 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_boss_ctor_add_sequence", "mtg_boss_ctor_add_packed", "mtg_boss_ctor_build_chunk",
            "mtg_boss_chunk_free", "mtg_boss_build_device", "mtg_boss_last_timings",
            "mtg_device_alloc", "mtg_device_free", "mtg_memcpy_h2d", "mtg_memcpy_d2h",
-           "mtg_device_count", "mtg_device_synchronize")
+           "mtg_device_count", "mtg_device_synchronize", "mtg_comm_get_unique_id",
+           "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
+           "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
+           "mtg_dist_bounds")
+
+COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -106,6 +113,21 @@ def lib():
         L.mtg_memcpy_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         L.mtg_device_count.restype = ctypes.c_int
         L.mtg_device_synchronize.argtypes = [ctypes.c_int]
+        L.mtg_comm_get_unique_id.argtypes = [ctypes.c_char_p]
+        L.mtg_comm_create_rccl.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int]
+        L.mtg_comm_create_rccl.restype = ctypes.c_void_p
+        L.mtg_comm_create_local.argtypes = [ctypes.c_int, P(ctypes.c_void_p)]
+        L.mtg_comm_destroy.argtypes = [ctypes.c_void_p]
+        L.mtg_comm_rank.argtypes = [ctypes.c_void_p]
+        L.mtg_comm_size.argtypes = [ctypes.c_void_p]
+        L.mtg_boss_ctor_build_chunk_dist.argtypes = [ctypes.c_void_p, ctypes.c_void_p, P(_Chunk)]
+        L.mtg_boss_build_device_dist.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_void_p, P(_DeviceChunk)]
+        L.mtg_dist_bounds.argtypes = [P(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_int,
+                                      P(ctypes.c_uint64)]
         for name in EXPORTS:
             getattr(L, name)
         _lib = L
@@ -182,9 +204,14 @@ class BOSSChunkConstructor:
             cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None,
             len(bs)))
 
-    def build_chunk(self):
+    def build_chunk(self, comm=None):
+        """BOSS::Chunk of everything added; with `comm`, this rank's range of the global build
+        (concatenate the ranks' chunks in rank order with Chunk.extend)."""
         c = _Chunk()
-        _check(lib().mtg_boss_ctor_build_chunk(self._h, ctypes.byref(c)))
+        if comm is None:
+            _check(lib().mtg_boss_ctor_build_chunk(self._h, ctypes.byref(c)))
+        else:
+            _check(lib().mtg_boss_ctor_build_chunk_dist(self._h, comm.handle, ctypes.byref(c)))
         n = c.n
         W = np.ctypeslib.as_array(c.W, shape=(n,)).copy()
         last = np.ctypeslib.as_array(c.last, shape=(n,)).copy()
@@ -195,11 +222,17 @@ class BOSSChunkConstructor:
         return out
 
     def build_device(self, d_seq, seq_len, d_read_starts=None, d_counts=None, n_reads=0,
-                     stream=None):
-        """Whole path on a device-resident read buffer; returns the device chunk descriptor."""
+                     stream=None, comm=None):
+        """Whole path on a device-resident read buffer; returns the device chunk descriptor
+        (with `comm`: this rank's range of the multi-GPU build)."""
         c = _DeviceChunk()
-        _check(lib().mtg_boss_build_device(self._h, d_seq, seq_len, d_read_starts, d_counts,
-                                           n_reads, stream, ctypes.byref(c)))
+        if comm is None:
+            _check(lib().mtg_boss_build_device(self._h, d_seq, seq_len, d_read_starts, d_counts,
+                                               n_reads, stream, ctypes.byref(c)))
+        else:
+            _check(lib().mtg_boss_build_device_dist(self._h, comm.handle, d_seq, seq_len,
+                                                    d_read_starts, d_counts, n_reads, stream,
+                                                    ctypes.byref(c)))
         return c
 
     def timings(self):
@@ -240,6 +273,70 @@ class BOSSConstructor(BOSSChunkConstructor):
         return IBOSSChunkConstructor.initialize(k, canonical, bits_per_count, filter_suffix,
                                                 num_threads, memory_preallocated,
                                                 container_type)
+
+
+class Comm:
+    """Exchange group of a multi-GPU build (include/mtg_boss.h: mtg_comm_*)."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h and _lib is not None:
+            _lib.mtg_comm_destroy(h)
+
+    @property
+    def rank(self):
+        return lib().mtg_comm_rank(self.handle)
+
+    @property
+    def size(self):
+        return lib().mtg_comm_size(self.handle)
+
+    @staticmethod
+    def unique_id():
+        """128 opaque bytes (ncclGetUniqueId) that rank 0 broadcasts to the others."""
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        _check(lib().mtg_comm_get_unique_id(buf))
+        return buf.raw
+
+    @staticmethod
+    def rccl(unique_id, world, rank, device_id):
+        """One rank of an RCCL group over xGMI (one process per GPU)."""
+        h = lib().mtg_comm_create_rccl(bytes(unique_id), world, rank, device_id)
+        if not h:
+            raise RuntimeError(lib().mtg_last_error().decode())
+        return Comm(h)
+
+    @staticmethod
+    def local_group(world):
+        """`world` ranks inside this process on one device (one host thread per rank)."""
+        arr = (ctypes.c_void_p * world)()
+        _check(lib().mtg_comm_create_local(world, arr))
+        return [Comm(arr[r]) for r in range(world)]
+
+
+def dist_bounds(hist, world):
+    """The range split of the multi-GPU build: bounds[0..world] over len(hist) prefixes."""
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    out = np.zeros(world + 1, dtype=np.uint64)
+    _check(lib().mtg_dist_bounds(h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(h), world,
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+    return out
+
+
+def concatenate(chunks):
+    """Rank chunks -> one chunk, BOSS::Chunk::extend in rank order (boss_chunk.cpp:230-270)."""
+    first = chunks[0]
+    out = Chunk(first.k, first.W.copy(), first.last.copy(), first.F.copy(),
+                None if first.weights is None else first.weights.copy(), first.n_real,
+                first.n_dummy)
+    for ch in chunks[1:]:
+        out.extend(ch)
+        out.n_real += ch.n_real
+        out.n_dummy += ch.n_dummy
+    return out
 
 
 def device_count():

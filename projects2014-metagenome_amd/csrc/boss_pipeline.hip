@@ -20,6 +20,8 @@
 
 #include "../../include/mtg_boss.h"
 #include "boss_kernels.hpp"
+#include "comm.hpp"
+#include "dist_kernels.hpp"
 #include "msd_sort.hpp"
 #include "radix_sort.hpp"
 
@@ -43,7 +45,10 @@ class Workspace {
     enum Slot {
         SEQ, STARTS, RCOUNTS, KA, KB, CA, CB, SUMS, DESC, HIST, STARTS_DIGIT, SMALL, BUCKETS,
         FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, MSD_COUNTS, MSD_BSTART,
-        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS, NSLOTS
+        MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
+        // multi-GPU build: exchange buffers, routing and the query join
+        XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -539,31 +544,21 @@ static void merge_sorted(Ctx &c, const Key<LA> *a, const uint32_t *ac, uint64_t 
     HIP_CHECK(hipGetLastError());
 }
 
-template <int L2, int L3, bool COUNTED>
-static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
-                         const BuildInput &in, BuildOutput *out) {
-    using K2 = Key<L2>;
-    using K3 = Key<L3>;
-    const unsigned K = k + 1;
-    const unsigned cbits = bits <= 8 ? 8 : bits <= 16 ? 16 : 32;
-    const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
-    const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
-    mtg_boss_timings &T = c.timings;
-    T = mtg_boss_timings{};
-    HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
-    EventTimer tm(c.stream);
-    const int ev_start = tm.mark();
+// ---------------------------------------------------------------------------- pipeline stages
 
-    // ---- K1 extract
+// K1: extract (+ canonicalise) every valid k-mer window of the read buffer into *ka (count ->
+// scan -> write over identical tiles).  Returns N.
+template <int L2, bool COUNTED>
+static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                              Key<L2> **ka, Key<L2> **kb, uint32_t **ca, uint32_t **cb) {
+    using K2 = Key<L2>;
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
-    T.n_positions = npos;
-    K2 *ka = (K2 *)c.ws.get(Workspace::KA, npos * sizeof(K2));
-    K2 *kb = (K2 *)c.ws.get(Workspace::KB, npos * sizeof(K2));
-    uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, npos * 4) : nullptr;
-    uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, npos * 4) : nullptr;
+    c.timings.n_positions = npos;
+    *ka = (K2 *)c.ws.get(Workspace::KA, npos * sizeof(K2));
+    *kb = (K2 *)c.ws.get(Workspace::KB, npos * sizeof(K2));
+    *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, npos * 4) : nullptr;
+    *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, npos * 4) : nullptr;
     uint64_t N = 0;
-    uint32_t *hist1 = nullptr;
-    unsigned hist_bits = 0;
     if (npos) {
         constexpr int TILE = ExtractTraits<L2>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
@@ -583,21 +578,21 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         N = read_u64(c, (const unsigned long long *)(toff + tiles));
         extract_kernel<L2, COUNTED, false><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
             in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax,
-            ka, ca, nullptr, toff, hist1, hist_bits);
+            *ka, *ca, nullptr, toff, nullptr, 0);
         HIP_CHECK(hipGetLastError());
     }
-    T.n_extracted = N;
-    const int ev_extract = tm.mark();
+    c.timings.n_extracted = N;
+    return N;
+}
 
-    // ---- K2 sort + K3 unique / saturating count merge (ka)
-    c.radix_ms = 0;
-    c.radix_bytes = 0;
-    c.radix_launches = 0;
+// K2 + K3: sort + unique (saturating count merge) of *ka[0..N) -> *ka[0..U).  `dup` is the
+// expected number of copies per distinct key (plans the MSD depth only).
+template <int L2, bool COUNTED>
+static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, Key<L2> **kb,
+                              uint32_t **ca, uint32_t **cb, uint64_t N, double dup, bool track) {
     uint64_t U = 0;
-    int ev_sort;
     if (c.use_lsd) {
-        radix_sort<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, true);
-        ev_sort = tm.mark();
+        radix_sort<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, track);
         reset_small(c);
         if (N) {
             const uint64_t tiles = ceil_div(N, 2048);
@@ -609,148 +604,160 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
                 HIP_CHECK(hipMemsetAsync(sums, 0, N * 8, c.stream));
             }
             unique_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-                ka, ca, N, kb, sums, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
+                *ka, *ca, N, *kb, sums, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
             HIP_CHECK(hipGetLastError());
             U = read_u64(c, &c.small->total);
             if (COUNTED) {
                 count_clamp_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(U, 256), 4096))),
-                                     dim3(256), 0, c.stream>>>(sums, U, cmax, cb);
+                                     dim3(256), 0, c.stream>>>(sums, U, cmax, *cb);
                 HIP_CHECK(hipGetLastError());
             }
         }
-        std::swap(ka, kb);
-        std::swap(ca, cb);
+        std::swap(*ka, *kb);
+        std::swap(*ca, *cb);
     } else {
-        c.track_partition = true;
-        U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, 8.0, hist1);
+        c.track_partition = track;
+        U = msd_sort_unique<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, cmax, dup, nullptr);
         c.track_partition = false;
-        ev_sort = tm.mark();
     }
-    T.n_unique = U;
-    debug_check_sorted(c, "collected k-mers", ka, U);
-    const int ev_unique = tm.mark();
+    return U;
+}
 
-    // ---- K4 reverse complements (CANONICAL_ONLY): rc(x) of the sorted canonical set is sorted
-    // on its own (no duplicates) and merged with it
-    uint64_t R = U;
-    if (canonical && U) {
-        uint64_t Urc = U;
-        uint32_t *rc_hist = nullptr;
+// K4: the reverse complements of a sorted canonical set ka[0..U) (add_reverse_complements,
+// boss_chunk_construct.cpp:179-222), sorted on their own.  rc(x) of odd K is never x, so it is a
+// 1:1 map; even K drops the palindromes and doubles their counts (rc_augment_kernel).  `buf`
+// (+ `bufc`) takes the rc keys; the sorted result is in *rk / *rkc.  Returns their number.
+template <int L2, bool COUNTED>
+static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<L2> *ka,
+                         uint32_t *ca, uint64_t U, Key<L2> *buf, uint32_t *bufc, Key<L2> **rk,
+                         uint32_t **rkc) {
+    using K2 = Key<L2>;
+    uint64_t Urc = U;
+    uint32_t *rc_hist = nullptr;
+    if (K & 1) {
         unsigned rc_hist_bits = 0;
-        if (K & 1) {
-            // odd K: no k-mer is its own reverse complement, every rc(x) is kept in place
-            if (!c.use_lsd) {
-                const MsdPlan plan = msd_plan<L2>(c, U, 2 * K, 1.0);
-                if (plan.levels) {
-                    rc_hist_bits = plan.digit_end[1];
-                    rc_hist = (uint32_t *)c.ws.get(Workspace::HIST1, (1u << rc_hist_bits) * 4);
-                    HIP_CHECK(hipMemsetAsync(rc_hist, 0, (1u << rc_hist_bits) * 4, c.stream));
-                }
+        if (!c.use_lsd) {
+            const MsdPlan plan = msd_plan<L2>(c, U, 2 * K, 1.0);
+            if (plan.levels) {
+                rc_hist_bits = plan.digit_end[1];
+                rc_hist = (uint32_t *)c.ws.get(Workspace::HIST1, (1u << rc_hist_bits) * 4);
+                HIP_CHECK(hipMemsetAsync(rc_hist, 0, (1u << rc_hist_bits) * 4, c.stream));
             }
-            rc_map_kernel<L2, COUNTED><<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256 * 4), 16384)),
-                                         dim3(256), 0, c.stream>>>(ka, ca, kb, cb, U, K, rc_hist, rc_hist_bits);
-            HIP_CHECK(hipGetLastError());
-        } else {
-            reset_small(c);
-            const uint64_t tiles = ceil_div(U, 1024);
-            uint32_t desc_ep;
-            uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
-            rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-                ka, ca, kb, cb, U, K, cbits, cmax, desc, desc_ep, &c.small->counter, &c.small->total,
-                &c.small->error);
-            HIP_CHECK(hipGetLastError());
-            Urc = read_u64(c, &c.small->total);
         }
-        K2 *ra = kb, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
-        uint32_t *rca = cb, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
-        if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
-        else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true);
-        R = U + Urc;
-        K2 *real = (K2 *)c.ws.get(Workspace::REAL, R * sizeof(K2));
-        uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, R * 4) : nullptr;
-        merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, ra, rca, Urc, K, real, realc, 0);
-        ka = real;
-        ca = realc;
-    }
-    T.n_real = R;
-    debug_check_sorted(c, "real k-mers", ka, R);
-    const int ev_rc = tm.mark();
-
-    // ---- K5/K6 dummy sinks and sources (all levels), sort + unique
-    uint64_t D = 0;
-    K3 *dk = nullptr;
-    {
-        const unsigned B = bucket_bits<L2>(R, 2 * K);
-        const unsigned bshift = 2 * K - B;
-        const uint64_t nb = 1ull << B;
-        uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nb + 2) * 8);
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
-        bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
+        rc_map_kernel<L2, COUNTED><<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256 * 4), 16384)),
+                                     dim3(256), 0, c.stream>>>(ka, ca, buf, bufc, U, K, rc_hist, rc_hist_bits);
         HIP_CHECK(hipGetLastError());
-        uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
-        uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
-        const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
-        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
-        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (wtiles + 1) * 8);
-        uint64_t Draw = 0;
-        if (R) {
-            HIP_CHECK(hipMemsetAsync(in_flag, 0, R, c.stream));
-            dummy_sink_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0,
-                                    c.stream>>>(ka, R, K, bstart, bshift, flags, in_flag);
-            HIP_CHECK(hipGetLastError());
-            dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, k,
-                                                                                  tcnt);
-            HIP_CHECK(hipGetLastError());
-            uint32_t ep;
-            const uint64_t st = ceil_div(wtiles, 4096);
-            uint64_t *desc = acquire_desc(c, st, &ep);
-            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(
-                tcnt, wtiles, toff, desc, ep, &c.small->counter, &c.small->error);
-            HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemcpyAsync(&Draw, toff + wtiles, 8, hipMemcpyDeviceToHost, c.stream));
-            HIP_CHECK(hipStreamSynchronize(c.stream));
-        }
-        K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
-        K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
-        if (Draw) {
-            dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(
-                ka, flags, in_flag, R, K, toff, da);
-            HIP_CHECK(hipGetLastError());
-            uint32_t *nv = nullptr;
-            if (c.use_lsd || !c.dummy_msd) {
-                radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
-                reset_small(c);
-                const uint64_t ut = ceil_div(Draw, 2048);
-                uint32_t udesc_ep;
-                uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
-                unique_kernel<L3, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
-                    da, nullptr, Draw, db, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total,
-                    &c.small->error);
-                HIP_CHECK(hipGetLastError());
-                D = read_u64(c, &c.small->total);
-            } else {
-                D = msd_sort_unique<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, 0, 2.0);
-                std::swap(da, db);
-            }
-            dk = db;
-        }
+    } else {
+        reset_small(c);
+        const uint64_t tiles = ceil_div(U, 1024);
+        uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, tiles, &desc_ep);
+        rc_augment_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            ka, ca, buf, bufc, U, K, cbits, cmax, desc, desc_ep,
+            &c.small->counter, &c.small->total, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        Urc = read_u64(c, &c.small->total);
     }
-    T.n_dummy = D + 1;
-    debug_check_sorted(c, "dummy k-mers", dk, D);
-    const int ev_dummy = tm.mark();
+    K2 *ra = buf, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
+    uint32_t *rca = bufc, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
+    if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
+    else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true);
+    *rk = ra;
+    *rkc = rca;
+    return Urc;
+}
 
-    // ---- K7 lift + merge -> stream of M = 1 + R + D lifted k-mers
-    const uint64_t M = 1 + R + D;
+// LSD sort + unique of the raw dummy k-mers da[0..Draw) (db is the ping-pong buffer); returns
+// D and leaves the distinct dummies in *dk
+template <int L3>
+static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db, uint64_t Draw,
+                                    Key<L3> **dk) {
+    uint64_t D = 0;
+    uint32_t *nv = nullptr;
+    if (c.use_lsd || !c.dummy_msd) {
+        radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
+        reset_small(c);
+        const uint64_t ut = ceil_div(Draw, 2048);
+        uint32_t udesc_ep;
+        uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
+        unique_kernel<L3, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+            da, nullptr, Draw, db, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total,
+            &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        D = read_u64(c, &c.small->total);
+    } else {
+        D = msd_sort_unique<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, 0, 2.0);
+        std::swap(da, db);
+    }
+    *dk = db;
+    return D;
+}
+
+// K5/K6 on one device: dummy sinks and sources (all levels) of the sorted real edges ka[0..R)
+template <int L2, int L3>
+static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint64_t R, Key<L3> **dk) {
+    using K3 = Key<L3>;
+    const unsigned k = K - 1;
+    const unsigned B = bucket_bits<L2>(R, 2 * K);
+    const unsigned bshift = 2 * K - B;
+    const uint64_t nb = 1ull << B;
+    uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nb + 2) * 8);
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
+    bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
+    HIP_CHECK(hipGetLastError());
+    uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
+    uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
+    const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
+    uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
+    uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (wtiles + 1) * 8);
+    uint64_t Draw = 0;
+    if (R) {
+        HIP_CHECK(hipMemsetAsync(in_flag, 0, R, c.stream));
+        dummy_sink_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0,
+                                c.stream>>>(ka, R, K, bstart, bshift, flags, in_flag);
+        HIP_CHECK(hipGetLastError());
+        dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, k, tcnt);
+        HIP_CHECK(hipGetLastError());
+        uint32_t ep;
+        const uint64_t st = ceil_div(wtiles, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(
+            tcnt, wtiles, toff, desc, ep, &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(&Draw, toff + wtiles, 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+    *dk = nullptr;
+    if (!Draw) return 0;
+    K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
+    K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
+    dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(ka, flags, in_flag, R, K,
+                                                                                    toff, da);
+    HIP_CHECK(hipGetLastError());
+    return sort_unique_dummies<L3>(c, K, da, db, Draw, dk);
+}
+
+// K7 + K8: lift + merge the real edges with the sorted dummies (behind the main dummy row when
+// `root`), then W / last / F / weights.  Rows go to out[1..]; out row 0 is the leading row.
+template <int L2, int L3, bool COUNTED>
+static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, unsigned bits,
+                             const Key<L2> *real, const uint32_t *realc, uint64_t R, const Key<L3> *dk,
+                             uint64_t D, bool root, BuildOutput *out) {
+    using K3 = Key<L3>;
+    const unsigned K = k + 1;
+    const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
+    const uint64_t M = (root ? 1 : 0) + R + D;
     K3 *sk = (K3 *)c.ws.get(Workspace::STREAM, M * sizeof(K3));
     uint32_t *sc = COUNTED ? (uint32_t *)c.ws.get(Workspace::SCOUNT, M * 4) : nullptr;
-    set_root_row_kernel<<<1, 1, 0, c.stream>>>((uint64_t *)sk, L3, COUNTED ? sc : nullptr);
-    HIP_CHECK(hipGetLastError());
-    merge_sorted<L3, L2, true, COUNTED, false>(c, ka, ca, R, dk, nullptr, D, K, sk, sc, 1);
+    if (root) {
+        set_root_row_kernel<<<1, 1, 0, c.stream>>>((uint64_t *)sk, L3, COUNTED ? sc : nullptr);
+        HIP_CHECK(hipGetLastError());
+    }
+    merge_sorted<L3, L2, true, COUNTED, false>(c, real, realc, R, dk, nullptr, D, K, sk, sc, root ? 1 : 0);
     debug_check_sorted(c, "merged stream", sk, M);
-    const int ev_merge = tm.mark();
+    *ev_merge = tm.mark();
 
-    // ---- K8 W / last / F / weights
     uint8_t *W = (uint8_t *)c.ws.get(Workspace::OW, M + 1);
     uint8_t *last = (uint8_t *)c.ws.get(Workspace::OLAST, M + 1);
     uint32_t *weights = COUNTED ? (uint32_t *)c.ws.get(Workspace::OWEIGHTS, (M + 1) * 4) : nullptr;
@@ -760,7 +767,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     reset_small(c);
     uint64_t rows = M;
     bool slow = c.emit_slow;
-    if (!slow) {
+    if (!slow && M) {
         emit_fast_kernel<L3, COUNTED><<<dim3((unsigned)ceil_div(M + 1, 256 * 8)), dim3(256), 0, c.stream>>>(
             sk, sc, M, k, wmax, W, last, weights, &c.small->skip);
         HIP_CHECK(hipGetLastError());
@@ -771,6 +778,9 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         HIP_CHECK(hipStreamSynchronize(c.stream));
         for (int ch = 0; ch < 5; ++ch) out->F[ch] = h.fhist[ch];
         slow = h.skip != 0;  // a redundant dummy sink: rows must be compacted
+    } else if (!M) {
+        for (int ch = 0; ch < 5; ++ch) out->F[ch] = 0;
+        slow = false;
     }
     if (slow) {
         reset_small(c);
@@ -790,17 +800,77 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
             s += fh[ch];
         }
     }
-    const int ev_emit = tm.mark();
-    check_error_word(c);
-    HIP_CHECK(hipStreamSynchronize(c.stream));
-
     out->W = W;
     out->last = last;
     out->weights = weights;
     out->n = rows + 1;
     out->n_real = R;
     out->n_dummy = rows - R;
-    T.n_rows = rows + 1;
+}
+
+template <int L2, int L3, bool COUNTED>
+static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
+                         const BuildInput &in, BuildOutput *out) {
+    using K2 = Key<L2>;
+    const unsigned K = k + 1;
+    const unsigned cbits = bits <= 8 ? 8 : bits <= 16 ? 16 : 32;
+    const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+    mtg_boss_timings &T = c.timings;
+    T = mtg_boss_timings{};
+    T.world = 1;
+    HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
+    EventTimer tm(c.stream);
+    const int ev_start = tm.mark();
+
+    // ---- K1 extract
+    K2 *ka, *kb;
+    uint32_t *ca, *cb;
+    const uint64_t N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
+    const int ev_extract = tm.mark();
+
+    // ---- K2 sort + K3 unique / saturating count merge (ka)
+    c.radix_ms = 0;
+    c.radix_bytes = 0;
+    c.radix_launches = 0;
+    const uint64_t U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 8.0, true);
+    const int ev_sort = tm.mark();
+    T.n_unique = U;
+    debug_check_sorted(c, "collected k-mers", ka, U);
+    const int ev_unique = tm.mark();
+
+    // ---- K4 reverse complements (CANONICAL_ONLY): rc(x) of the sorted canonical set is sorted
+    // on its own (no duplicates) and merged with it
+    uint64_t R = U;
+    if (canonical && U) {
+        K2 *rk;
+        uint32_t *rkc;
+        const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc);
+        R = U + Urc;
+        K2 *real = (K2 *)c.ws.get(Workspace::REAL, R * sizeof(K2));
+        uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, R * 4) : nullptr;
+        merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, rk, rkc, Urc, K, real, realc, 0);
+        ka = real;
+        ca = realc;
+    }
+    T.n_real = R;
+    debug_check_sorted(c, "real k-mers", ka, R);
+    const int ev_rc = tm.mark();
+
+    // ---- K5/K6 dummy sinks and sources (all levels), sort + unique
+    Key<L3> *dk = nullptr;
+    const uint64_t D = stage_dummies_local<L2, L3>(c, K, ka, R, &dk);
+    T.n_dummy = D + 1;
+    debug_check_sorted(c, "dummy k-mers", dk, D);
+    const int ev_dummy = tm.mark();
+
+    // ---- K7 lift + merge, K8 W / last / F / weights
+    int ev_merge;
+    stage_merge_emit<L2, L3, COUNTED>(c, tm, &ev_merge, k, bits, ka, ca, R, dk, D, true, out);
+    const int ev_emit = tm.mark();
+    check_error_word(c);
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+
+    T.n_rows = out->n;
     T.extract_ms = tm.ms(ev_start, ev_extract);
     T.sort_ms = tm.ms(ev_extract, ev_sort);
     T.unique_ms = tm.ms(ev_sort, ev_unique);
@@ -814,25 +884,416 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
 }
 
+// ------------------------------------------------------------------------ multi-GPU pipeline
+//
+// One rank per GPU builds the chunk of one range of BOSS order (dist_kernels.hpp):
+//   K1-K3 on the rank's reads -> exchange 1: the sorted distinct k-mers by range (RCCL
+//   all-to-all-v of contiguous slices) -> dedupe / saturating count merge of the P runs ->
+//   [canonical: rc of the owned canonical k-mers, exchange 2 of both strands by the final
+//   ranges, merge] -> exchange of the sink / in-edge queries -> sinks at the owner, sources
+//   routed to theirs -> sort + unique -> lift + merge -> W / last / F / weights.
+// The chunks concatenate in rank order with BOSS::Chunk::extend (boss_chunk.cpp:230-270).
+
+// ranges over 4^m prefixes: bounds[j] = first prefix of rank j, balanced on `hist` (host)
+static std::vector<uint64_t> balanced_bounds(const uint64_t *hist, uint64_t nb, int P) {
+    std::vector<uint64_t> bounds(P + 1, nb);
+    bounds[0] = 0;
+    unsigned __int128 total = 0;
+    for (uint64_t b = 0; b < nb; ++b) total += hist[b];
+    unsigned __int128 cum = 0;
+    int j = 1;
+    for (uint64_t b = 0; b <= nb && j < P; ++b) {
+        while (j < P && cum * (unsigned)P >= total * (unsigned)j) bounds[j++] = b;
+        if (b < nb) cum += hist[b];
+    }
+    return bounds;
+}
+
+// the same ranges in lifted ($ACGT, 3 bits per char) prefixes; a bound past the last prefix
+// becomes 8^m, above every lifted prefix
+static std::vector<uint64_t> lifted_bounds(const std::vector<uint64_t> &b2, unsigned m) {
+    std::vector<uint64_t> b3(b2.size());
+    const uint64_t nb = 1ull << (2 * m);
+    for (size_t j = 0; j < b2.size(); ++j) {
+        if (b2[j] >= nb) {
+            b3[j] = 1ull << (3 * m);
+            continue;
+        }
+        uint64_t v = 0;
+        for (unsigned i = 0; i < m; ++i) v |= (((b2[j] >> (2 * i)) & 3) + 1) << (3 * i);
+        b3[j] = v;
+    }
+    return b3;
+}
+
+__global__ void gather_strided_kernel(const uint64_t *__restrict__ src, uint64_t stride, uint32_t cnt,
+                                      uint64_t *__restrict__ dst) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < cnt) dst[j] = src[(uint64_t)j * stride];
+}
+
+struct Dist {
+    Comm &comm;
+    int P, me;
+    unsigned m;       // prefix chars of the range partition
+    unsigned shift2;  // 2-bit prefix = key >> shift2
+    uint64_t nb;      // 4^m prefixes
+    EventTimer *tm;
+    std::vector<std::pair<int, int>> xev;  // event pairs around exchanges
+};
+
+// prefix index of a sorted 2-bit array: start[p] = first key with prefix >= p, p in [0, nb]
+template <int L2>
+static uint64_t *prefix_index(Ctx &c, const Dist &d, Workspace::Slot slot, const Key<L2> *keys, uint64_t n) {
+    uint64_t *st = (uint64_t *)c.ws.get(slot, (d.nb + 2) * 8);
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n + 1, 256), 8192));
+    bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(keys, n, d.shift2, d.nb, st);
+    HIP_CHECK(hipGetLastError());
+    return st;
+}
+
+// global prefix histogram of the sorted arrays (summed over all ranks) -> balanced ranges;
+// also returns every array's slice offsets for those ranges (host, P + 1 each)
+template <int L2>
+static std::vector<uint64_t> dist_ranges(Ctx &c, Dist &d, int na, const Key<L2> *const *arrs,
+                                         const uint64_t *ns, std::vector<std::vector<uint64_t>> *soff) {
+    uint64_t *hist = (uint64_t *)c.ws.get(Workspace::XHIST, d.nb * 8);
+    std::vector<std::vector<uint64_t>> starts(na);
+    for (int a = 0; a < na; ++a) {
+        uint64_t *st = prefix_index<L2>(c, d, a == 0 ? Workspace::XSTART_A : Workspace::XSTART_B, arrs[a], ns[a]);
+        hist_from_starts_kernel<<<dim3((unsigned)ceil_div(d.nb, 256)), dim3(256), 0, c.stream>>>(st, d.nb, hist, a);
+        HIP_CHECK(hipGetLastError());
+        starts[a].resize(d.nb + 1);
+        HIP_CHECK(hipMemcpyAsync(starts[a].data(), st, (d.nb + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+    }
+    const int e0 = d.tm->mark();
+    d.comm.allreduce_sum_u64(hist, d.nb, c.stream);
+    d.xev.push_back({e0, d.tm->mark()});
+    std::vector<uint64_t> h(d.nb);
+    HIP_CHECK(hipMemcpyAsync(h.data(), hist, d.nb * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<uint64_t> bounds = balanced_bounds(h.data(), d.nb, d.P);
+    soff->assign(na, std::vector<uint64_t>(d.P + 1));
+    for (int a = 0; a < na; ++a)
+        for (int j = 0; j <= d.P; ++j) (*soff)[a][j] = starts[a][bounds[j]];
+    return bounds;
+}
+
+// all-to-all-v of `na` arrays (slice offsets soff[a], P + 1 each) into one receive buffer laid
+// out array-major then by source rank; returns the received element count
+template <typename T>
+static uint64_t exchange_runs(Ctx &c, Dist &d, int na, const T *const *arrs, const uint32_t *const *cnts,
+                         const std::vector<std::vector<uint64_t>> &soff, Workspace::Slot rslot,
+                         Workspace::Slot rcslot, T **recv, uint32_t **recvc) {
+    const int P = d.P;
+    std::vector<uint64_t> scnt(na * P);
+    for (int a = 0; a < na; ++a)
+        for (int j = 0; j < P; ++j) scnt[a * P + j] = soff[a][j + 1] - soff[a][j];
+    // every rank's counts -> the full matrix
+    const size_t V = scnt.size();
+    uint64_t *dm = (uint64_t *)c.ws.get(Workspace::XMAT, (V + V * P) * 8);
+    HIP_CHECK(hipMemcpyAsync(dm, scnt.data(), V * 8, hipMemcpyHostToDevice, c.stream));
+    const int e0 = d.tm->mark();
+    d.comm.allgather_u64(dm, dm + V, V, c.stream);
+    std::vector<uint64_t> mat(V * P);
+    HIP_CHECK(hipMemcpyAsync(mat.data(), dm + V, V * P * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<uint64_t> rcnt(V), roff(V);
+    uint64_t total = 0;
+    for (int a = 0; a < na; ++a)
+        for (int i = 0; i < P; ++i) {
+            rcnt[a * P + i] = mat[(size_t)i * V + a * P + d.me];
+            roff[a * P + i] = total;
+            total += rcnt[a * P + i];
+        }
+    *recv = (T *)c.ws.get(rslot, total * sizeof(T));
+    if (cnts) *recvc = (uint32_t *)c.ws.get(rcslot, total * 4);
+    for (int a = 0; a < na; ++a) {
+        d.comm.alltoallv(arrs[a], &scnt[a * P], soff[a].data(), *recv, &rcnt[a * P], &roff[a * P], sizeof(T),
+                         c.stream);
+        if (cnts)
+            d.comm.alltoallv(cnts[a], &scnt[a * P], soff[a].data(), *recvc, &rcnt[a * P], &roff[a * P], 4,
+                             c.stream);
+        for (int j = 0; j < P; ++j)
+            if (j != d.me) c.timings.n_sent += scnt[a * P + j];
+    }
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    d.xev.push_back({e0, d.tm->mark()});
+    return total;
+}
+
+// route the keys produced by a kernel-side function (MODE, dist_kernels.hpp) to their owners:
+// count -> scan -> write into the send buffer; returns slice offsets (P + 1)
+template <int L, int MODE>
+static std::vector<uint64_t> route(Ctx &c, const Dist &d, const Key<L> *in, uint64_t n, unsigned K,
+                                   unsigned pshift, unsigned pbits, const std::vector<uint64_t> &bounds,
+                                   Key<L> *out) {
+    const int P = d.P;
+    std::vector<uint64_t> soff(P + 1, 0);
+    if (!n) return soff;
+    const uint64_t ntiles = ceil_div(n, RT_TILE);
+    uint64_t *db = (uint64_t *)c.ws.get(Workspace::BOUNDS, (P + 1) * 8);
+    HIP_CHECK(hipMemcpyAsync(db, bounds.data(), (P + 1) * 8, hipMemcpyHostToDevice, c.stream));
+    uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::RTCNT, (P * ntiles + 1) * 4);
+    uint64_t *toff = (uint64_t *)c.ws.get(Workspace::RTOFF, (P * ntiles + 1) * 8);
+    route_count_kernel<L, MODE><<<dim3((unsigned)ntiles), dim3(RT_BLOCK), 0, c.stream>>>(
+        in, n, K, pshift, pbits, db, (uint32_t)P, tcnt, ntiles);
+    HIP_CHECK(hipGetLastError());
+    uint32_t ep;
+    const uint64_t st = ceil_div(P * ntiles, 4096);
+    uint64_t *desc = acquire_desc(c, st, &ep);
+    HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+    scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, P * ntiles, toff, desc, ep,
+                                                                      &c.small->counter, &c.small->error);
+    HIP_CHECK(hipGetLastError());
+    route_write_kernel<L, MODE><<<dim3((unsigned)ntiles), dim3(RT_BLOCK), 0, c.stream>>>(
+        in, n, K, pshift, pbits, db, (uint32_t)P, toff, ntiles, out);
+    HIP_CHECK(hipGetLastError());
+    uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, (P + 1) * 8);
+    gather_strided_kernel<<<1, 256, 0, c.stream>>>(toff, ntiles, (uint32_t)P + 1, g);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(soff.data(), g, (P + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    return soff;
+}
+
+template <int L2, int L3, bool COUNTED>
+static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, unsigned bits,
+                              const BuildInput &in, BuildOutput *out) {
+    using K2 = Key<L2>;
+    using K3 = Key<L3>;
+    const unsigned K = k + 1;
+    const unsigned cbits = bits <= 8 ? 8 : bits <= 16 ? 16 : 32;
+    const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+    mtg_boss_timings &T = c.timings;
+    T = mtg_boss_timings{};
+    HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
+    EventTimer tm(c.stream);
+    const int ev_start = tm.mark();
+    Dist d{comm, comm.size(), comm.rank(), 0, 0, 1, &tm, {}};
+    if (d.P > MAX_RANKS) throw std::runtime_error("more ranks than the routing kernels support");
+    T.world = (uint64_t)d.P;
+    // ranges on the top m node chars, m <= k - 1 keeps every emission group inside one rank
+    d.m = std::min(8u, k >= 2 ? k - 1 : 0u);
+    d.shift2 = 2 * K - 2 * d.m;
+    d.nb = 1ull << (2 * d.m);
+
+    // ---- K1-K3 on this rank's reads
+    K2 *ka, *kb;
+    uint32_t *ca, *cb;
+    const uint64_t N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
+    const int ev_extract = tm.mark();
+    c.radix_ms = 0;
+    c.radix_bytes = 0;
+    c.radix_launches = 0;
+    const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 8.0, true);
+    const int ev_sort = tm.mark();
+
+    // ---- exchange 1: the distinct k-mers by range of their own prefix, merged at the owner
+    std::vector<std::vector<uint64_t>> soff;
+    std::vector<uint64_t> b1;
+    {
+        const K2 *arrs[1] = {ka};
+        const uint64_t ns[1] = {Ul};
+        b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff);
+    }
+    K2 *xa;
+    uint32_t *xac = nullptr;
+    {
+        const K2 *arrs[1] = {ka};
+        const uint32_t *cnts[1] = {ca};
+        const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA,
+                                         Workspace::XAC, &xa, &xac);
+        K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
+        uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
+        // the P runs are sorted and disjoint within a run; duplicates across runs collapse and
+        // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover 1/P of
+        // the prefix space, hence the denser plan.
+        T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, 1.0 / d.P, nullptr);
+    }
+    const uint64_t U = T.n_unique;
+    debug_check_sorted(c, "owned k-mers", xa, U);
+    const int ev_unique = tm.mark();
+
+    // ---- canonical: rc of the owned canonical set, exchange 2 of both strands by final range
+    K2 *E = xa;
+    uint32_t *Ec = xac;
+    uint64_t R = U;
+    std::vector<uint64_t> bounds;
+    if (canonical) {
+        K2 *rbuf = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U, 1) * sizeof(K2));
+        uint32_t *rbufc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U, 1) * 4) : nullptr;
+        K2 *rk = rbuf;
+        uint32_t *rkc = rbufc;
+        uint64_t Urc = 0;
+        if (U) Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, xa, xac, U, rbuf, rbufc, &rk, &rkc);
+        const K2 *arrs[2] = {xa, rk};
+        const uint32_t *cnts[2] = {xac, rkc};
+        const uint64_t ns[2] = {U, Urc};
+        bounds = dist_ranges<L2>(c, d, 2, arrs, ns, &soff);
+        K2 *ra;
+        uint32_t *rac = nullptr;
+        const uint64_t n2 = exchange_runs<K2>(c, d, 2, arrs, COUNTED ? cnts : nullptr, soff, Workspace::REAL,
+                                         Workspace::REALC, &ra, &rac);
+        K2 *rb = (K2 *)c.ws.get(Workspace::KB, n2 * sizeof(K2));
+        uint32_t *rbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, n2 * 4) : nullptr;
+        // all 2P runs are distinct keys (a canonical k-mer and its rc are different edges)
+        R = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rac, &rbc, n2, 2 * K, cmax, 1.0 / d.P, nullptr, true);
+        E = ra;
+        Ec = rac;
+    } else {
+        bounds = b1;  // basic mode: exchange 1 already placed every edge at its final owner
+    }
+    T.n_real = R;
+    debug_check_sorted(c, "real k-mers (owned)", E, R);
+    const int ev_rc = tm.mark();
+
+    // ---- K5/K6: sink / in-edge queries to the target node's owner, sources to theirs
+    const unsigned k_b = K - 1;
+    uint64_t D = 0;
+    K3 *dk = nullptr;
+    {
+        const unsigned B = bucket_bits<L2>(R, 2 * K);
+        const unsigned bshift = 2 * K - B;
+        const uint64_t nbk = 1ull << B;
+        uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nbk + 2) * 8);
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
+        bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(E, R, bshift, nbk, bstart);
+        HIP_CHECK(hipGetLastError());
+        uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
+        uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
+        if (R) {
+            HIP_CHECK(hipMemsetAsync(in_flag, 0, R, c.stream));
+            first_flag_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(R, 256), 16384)), dim3(256), 0,
+                                    c.stream>>>(E, R, flags);
+            HIP_CHECK(hipGetLastError());
+        }
+        // queries t = to_next(x, 0) of every owned edge, routed by the prefix of t
+        K2 *qs = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(R, 1) * sizeof(K2));
+        std::vector<std::vector<uint64_t>> qoff(1);
+        qoff[0] = route<L2, 0>(c, d, E, R, K, d.shift2, 2 * d.m, bounds, qs);
+        K2 *qr;
+        uint32_t *unused_c = nullptr;
+        const K2 *qarr[1] = {qs};
+        const uint64_t nq = exchange_runs<K2>(c, d, 1, qarr, nullptr, qoff, Workspace::QRECV, Workspace::XAC,
+                                         &qr, &unused_c);
+        uint8_t *qflag = (uint8_t *)c.ws.get(Workspace::QFLAG, nq + 1);
+        if (nq) {
+            query_answer_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(nq, 256), 65536)), dim3(256), 0,
+                                      c.stream>>>(E, R, bstart, bshift, qr, nq, in_flag, qflag);
+            HIP_CHECK(hipGetLastError());
+        }
+        // sinks of the missed queries: count + scan now, written once the buffer is sized
+        const uint64_t qtiles = ceil_div(nq, RT_TILE);
+        uint32_t *qtcnt = (uint32_t *)c.ws.get(Workspace::QTCNT, (qtiles + 1) * 4);
+        uint64_t *qtoff = (uint64_t *)c.ws.get(Workspace::QTOFF, (qtiles + 1) * 8);
+        uint64_t nsink = 0;
+        if (nq) {
+            sink_count_kernel<<<dim3((unsigned)qtiles), dim3(RT_BLOCK), 0, c.stream>>>(qflag, nq, qtcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t st = ceil_div(qtiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(qtcnt, qtiles, qtoff, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            nsink = read_u64(c, (const unsigned long long *)(qtoff + qtiles));
+        }
+        // sources of the owned edges (in_flag is complete: every rank's queries are answered)
+        const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
+        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
+        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (wtiles + 1) * 8);
+        uint64_t nsrc = 0;
+        if (R) {
+            dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, k_b, tcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t st = ceil_div(wtiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, wtiles, toff, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            nsrc = read_u64(c, (const unsigned long long *)(toff + wtiles));
+        }
+        K3 *src = (K3 *)c.ws.get(Workspace::DSRC, std::max<uint64_t>(nsrc, 1) * sizeof(K3));
+        if (nsrc) {
+            dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(E, flags, in_flag, R, K,
+                                                                                            toff, src);
+            HIP_CHECK(hipGetLastError());
+        }
+        K3 *ssend = (K3 *)c.ws.get(Workspace::DSEND, std::max<uint64_t>(nsrc, 1) * sizeof(K3));
+        std::vector<std::vector<uint64_t>> doff(1);
+        doff[0] = route<L3, 1>(c, d, src, nsrc, K, 3 * K - 3 * d.m, 3 * d.m, lifted_bounds(bounds, d.m), ssend);
+        K3 *drecv;
+        const K3 *darr[1] = {ssend};
+        const uint64_t nsrc_in = exchange_runs<K3>(c, d, 1, darr, nullptr, doff, Workspace::DRECV, Workspace::XAC,
+                                              &drecv, &unused_c);
+        const uint64_t Draw = nsink + nsrc_in;
+        if (Draw) {
+            K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
+            K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
+            if (nsink) {
+                sink_write_kernel<L2, L3><<<dim3((unsigned)qtiles), dim3(RT_BLOCK), 0, c.stream>>>(qr, qflag, nq, K,
+                                                                                                  qtoff, da);
+                HIP_CHECK(hipGetLastError());
+            }
+            if (nsrc_in)
+                HIP_CHECK(hipMemcpyAsync(da + nsink, drecv, nsrc_in * sizeof(K3), hipMemcpyDeviceToDevice,
+                                         c.stream));
+            D = sort_unique_dummies<L3>(c, K, da, db, Draw, &dk);
+        }
+    }
+    T.n_dummy = D + (d.me == 0 ? 1 : 0);
+    debug_check_sorted(c, "dummy k-mers (owned)", dk, D);
+    const int ev_dummy = tm.mark();
+
+    // ---- K7 + K8 on the owned range; rank 0 carries the main dummy row
+    int ev_merge;
+    stage_merge_emit<L2, L3, COUNTED>(c, tm, &ev_merge, k, bits, E, Ec, R, dk, D, d.me == 0, out);
+    const int ev_emit = tm.mark();
+    check_error_word(c);
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+
+    T.n_rows = out->n;
+    T.extract_ms = tm.ms(ev_start, ev_extract);
+    T.sort_ms = tm.ms(ev_extract, ev_sort);
+    T.unique_ms = tm.ms(ev_sort, ev_unique);
+    T.rc_ms = tm.ms(ev_unique, ev_rc);
+    T.dummy_ms = tm.ms(ev_rc, ev_dummy);
+    T.merge_ms = tm.ms(ev_dummy, ev_merge);
+    T.emit_ms = tm.ms(ev_merge, ev_emit);
+    T.total_ms = tm.ms(ev_start, ev_emit);
+    for (auto &p : d.xev) T.exchange_ms += tm.ms(p.first, p.second);
+    T.radix_launches = c.radix_launches;
+    T.radix_pass_ms = c.radix_launches ? c.radix_ms / c.radix_launches : 0;
+    T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
+}
+
 template <int L2, int L3>
-static void run_counted(Ctx &c, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
+static void run_counted(Ctx &c, Comm *comm, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
                         BuildOutput *out) {
-    if (bits) run_pipeline<L2, L3, true>(c, k, canonical, bits, in, out);
-    else run_pipeline<L2, L3, false>(c, k, canonical, bits, in, out);
+    if (comm) {
+        if (bits) run_pipeline_dist<L2, L3, true>(c, *comm, k, canonical, bits, in, out);
+        else run_pipeline_dist<L2, L3, false>(c, *comm, k, canonical, bits, in, out);
+    } else {
+        if (bits) run_pipeline<L2, L3, true>(c, k, canonical, bits, in, out);
+        else run_pipeline<L2, L3, false>(c, k, canonical, bits, in, out);
+    }
 }
 
 // word choice as boss_chunk_construct.cpp:1068-1079 (2-bit, by (k+1)*2) and :1030-1036
 // (lifted, by (k+1)*3)
-static void run_dispatch(Ctx &c, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
+static void run_dispatch(Ctx &c, Comm *comm, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
                          BuildOutput *out) {
     const unsigned K = k + 1;
-    if (3 * K <= 64) run_counted<1, 1>(c, k, canonical, bits, in, out);
-    else if (2 * K <= 64) run_counted<1, 2>(c, k, canonical, bits, in, out);
-    else if (3 * K <= 128) run_counted<2, 2>(c, k, canonical, bits, in, out);
-    else if (2 * K <= 128) run_counted<2, 4>(c, k, canonical, bits, in, out);
-    else run_counted<4, 4>(c, k, canonical, bits, in, out);
+    if (3 * K <= 64) run_counted<1, 1>(c, comm, k, canonical, bits, in, out);
+    else if (2 * K <= 64) run_counted<1, 2>(c, comm, k, canonical, bits, in, out);
+    else if (3 * K <= 128) run_counted<2, 2>(c, comm, k, canonical, bits, in, out);
+    else if (2 * K <= 128) run_counted<2, 4>(c, comm, k, canonical, bits, in, out);
+    else run_counted<4, 4>(c, comm, k, canonical, bits, in, out);
 }
-
 }  // namespace mtg
 
 // ============================================================================ C ABI
@@ -962,10 +1423,10 @@ int mtg_boss_ctor_add_packed(mtg_boss_ctor *c, const char *data, const uint64_t 
     return MTG_OK;
 }
 
-static int run_build(mtg_boss_ctor *c, const BuildInput &in, BuildOutput *out) {
+static int run_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {
     try {
         HIP_CHECK(hipSetDevice(c->device));
-        run_dispatch(c->ctx, (unsigned)c->params.k, c->params.both_strands != 0,
+        run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
                      c->params.bits_per_count, in, out);
         return MTG_OK;
     } catch (const std::exception &e) {
@@ -974,9 +1435,9 @@ static int run_build(mtg_boss_ctor *c, const BuildInput &in, BuildOutput *out) {
     }
 }
 
-int mtg_boss_build_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_len,
-                          const uint64_t *d_read_starts, const uint32_t *d_counts,
-                          uint64_t n_reads, void *stream, mtg_boss_device_chunk *out) {
+static int build_device_impl(mtg_boss_ctor *c, mtg::Comm *comm, const uint8_t *d_seq, uint64_t seq_len,
+                             const uint64_t *d_read_starts, const uint32_t *d_counts, uint64_t n_reads,
+                             void *stream, mtg_boss_device_chunk *out) {
     if (!c || !out || (seq_len && !d_seq) || (!d_read_starts != !d_counts)) {
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
@@ -986,7 +1447,7 @@ int mtg_boss_build_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_l
     if (stream) c->ctx.stream = (hipStream_t)stream;
     BuildInput in{d_seq, seq_len, d_read_starts, d_counts, d_counts ? n_reads : 0};
     BuildOutput o{};
-    int rc = run_build(c, in, &o);
+    int rc = run_build(c, comm, in, &o);
     c->ctx.stream = saved;
     if (rc != MTG_OK) return rc;
     out->k = c->params.k;
@@ -1000,7 +1461,7 @@ int mtg_boss_build_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_l
     return MTG_OK;
 }
 
-int mtg_boss_ctor_build_chunk(mtg_boss_ctor *c, mtg_boss_chunk *out) {
+static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *out) {
     if (!c || !out) {
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
@@ -1025,7 +1486,7 @@ int mtg_boss_ctor_build_chunk(mtg_boss_ctor *c, mtg_boss_chunk *out) {
         }
         BuildInput in{dseq, len, dstarts, dcounts, per_read ? nr : 0};
         BuildOutput o{};
-        run_dispatch(c->ctx, (unsigned)c->params.k, c->params.both_strands != 0,
+        run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
                      c->params.bits_per_count, in, &o);
         out->k = c->params.k;
         out->alph_size = 5;
@@ -1055,6 +1516,95 @@ int mtg_boss_ctor_build_chunk(mtg_boss_ctor *c, mtg_boss_chunk *out) {
         mtg_boss_chunk_free(out);
         return MTG_ERR_DEVICE;
     }
+}
+
+int mtg_boss_build_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_len,
+                          const uint64_t *d_read_starts, const uint32_t *d_counts,
+                          uint64_t n_reads, void *stream, mtg_boss_device_chunk *out) {
+    return build_device_impl(c, nullptr, d_seq, seq_len, d_read_starts, d_counts, n_reads, stream, out);
+}
+
+int mtg_boss_ctor_build_chunk(mtg_boss_ctor *c, mtg_boss_chunk *out) { return build_chunk_impl(c, nullptr, out); }
+
+// ---- multi-GPU build
+
+struct mtg_comm {
+    std::unique_ptr<mtg::Comm> comm;
+};
+
+int mtg_comm_get_unique_id(uint8_t *id) {
+    if (!id) return MTG_ERR_ARGUMENT;
+    try {
+        ncclUniqueId u;
+        RCCL_CHECK(RcclApi::get().GetUniqueId(&u));
+        std::memcpy(id, u.internal, MTG_COMM_ID_BYTES);
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_DEVICE;
+    }
+}
+
+mtg_comm *mtg_comm_create_rccl(const uint8_t *id, int world, int rank, int device_id) {
+    if (!id || world < 1 || rank < 0 || rank >= world || world > mtg::MAX_RANKS) {
+        set_error("bad arguments");
+        return nullptr;
+    }
+    try {
+        ncclUniqueId u;
+        std::memcpy(u.internal, id, MTG_COMM_ID_BYTES);
+        auto *c = new mtg_comm();
+        c->comm.reset(new mtg::RcclComm(u, world, rank, device_id));
+        return c;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return nullptr;
+    }
+}
+
+int mtg_comm_create_local(int world, mtg_comm **comms) {
+    if (world < 1 || world > mtg::MAX_RANKS || !comms) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    auto group = std::make_shared<mtg::LocalGroup>(world);
+    for (int r = 0; r < world; ++r) {
+        comms[r] = new mtg_comm();
+        comms[r]->comm.reset(new mtg::LocalComm(group, r));
+    }
+    return MTG_OK;
+}
+
+void mtg_comm_destroy(mtg_comm *comm) { delete comm; }
+
+int mtg_comm_rank(const mtg_comm *comm) { return comm ? comm->comm->rank() : -1; }
+
+int mtg_comm_size(const mtg_comm *comm) { return comm ? comm->comm->size() : -1; }
+
+int mtg_boss_build_device_dist(mtg_boss_ctor *c, mtg_comm *comm, const uint8_t *d_seq, uint64_t seq_len,
+                               const uint64_t *d_read_starts, const uint32_t *d_counts, uint64_t n_reads,
+                               void *stream, mtg_boss_device_chunk *out) {
+    if (!comm) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    return build_device_impl(c, comm->comm.get(), d_seq, seq_len, d_read_starts, d_counts, n_reads, stream,
+                             out);
+}
+
+int mtg_boss_ctor_build_chunk_dist(mtg_boss_ctor *c, mtg_comm *comm, mtg_boss_chunk *out) {
+    if (!comm) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    return build_chunk_impl(c, comm->comm.get(), out);
+}
+
+int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64_t *bounds) {
+    if (!hist || !bounds || world < 1) return MTG_ERR_ARGUMENT;
+    const std::vector<uint64_t> b = balanced_bounds(hist, n_prefixes, world);
+    std::memcpy(bounds, b.data(), b.size() * 8);
+    return MTG_OK;
 }
 
 void mtg_boss_chunk_free(mtg_boss_chunk *chunk) {

@@ -1,0 +1,238 @@
+// comm.hpp -- the exchange layer of the multi-GPU build: one rank per GPU.
+//
+// RcclComm drives RCCL (ROCm's NCCL) directly on device buffers over xGMI: an all-reduce of the
+// splitter histogram, an all-gather of the send-count matrix and grouped ncclSend/ncclRecv for
+// the all-to-all-v of k-mer runs.  RCCL is opened with dlopen on first use (soname
+// librccl.so.1, the one a PyTorch-ROCm process has already mapped), so the single-GPU library
+// has no link dependency on it.
+//
+// LocalComm runs P ranks as P host threads of one process on one device: the same exchange
+// semantics with device-to-device copies and a host barrier.  It is what the GPU tests use to
+// check the distributed build on a one-GPU box (RCCL refuses two ranks on one device).
+#pragma once
+
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace mtg {
+
+#define COMM_HIP(x)                                                                         \
+    do {                                                                                    \
+        hipError_t e_ = (x);                                                                \
+        if (e_ != hipSuccess)                                                               \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) +    \
+                                     " at " #x);                                            \
+    } while (0)
+
+class Comm {
+  public:
+    Comm(int rank, int size) : rank_(rank), size_(size) {}
+    virtual ~Comm() = default;
+    int rank() const { return rank_; }
+    int size() const { return size_; }
+    // in place, n u64 on the device, stream-ordered
+    virtual void allreduce_sum_u64(uint64_t *d, size_t n, hipStream_t s) = 0;
+    // d_recv[r * n + i] = rank r's d_send[i]
+    virtual void allgather_u64(const uint64_t *d_send, uint64_t *d_recv, size_t n, hipStream_t s) = 0;
+    // rank j receives scnt[j] elements from d_send + soff[j] (element units, host arrays of P);
+    // the elements from rank i land at d_recv + roff[i]
+    virtual void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff,
+                           void *d_recv, const uint64_t *rcnt, const uint64_t *roff, size_t esz,
+                           hipStream_t s) = 0;
+
+  protected:
+    int rank_, size_;
+};
+
+// ------------------------------------------------------------------------------------- RCCL
+struct RcclApi {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+
+    static RcclApi &get() {
+        static RcclApi api;
+        static std::once_flag once;
+        static std::string err;
+        std::call_once(once, [] {
+            void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) {
+                err = std::string("cannot load RCCL: ") + dlerror();
+                return;
+            }
+            auto sym = [&](const char *n) {
+                void *p = dlsym(h, n);
+                if (!p) err = std::string("RCCL symbol missing: ") + n;
+                return p;
+            };
+            api.GetUniqueId = (decltype(api.GetUniqueId))sym("ncclGetUniqueId");
+            api.CommInitRank = (decltype(api.CommInitRank))sym("ncclCommInitRank");
+            api.CommDestroy = (decltype(api.CommDestroy))sym("ncclCommDestroy");
+            api.AllReduce = (decltype(api.AllReduce))sym("ncclAllReduce");
+            api.AllGather = (decltype(api.AllGather))sym("ncclAllGather");
+            api.Send = (decltype(api.Send))sym("ncclSend");
+            api.Recv = (decltype(api.Recv))sym("ncclRecv");
+            api.GroupStart = (decltype(api.GroupStart))sym("ncclGroupStart");
+            api.GroupEnd = (decltype(api.GroupEnd))sym("ncclGroupEnd");
+            api.GetErrorString = (decltype(api.GetErrorString))sym("ncclGetErrorString");
+        });
+        if (!err.empty()) throw std::runtime_error(err);
+        return api;
+    }
+};
+
+#define RCCL_CHECK(x)                                                                       \
+    do {                                                                                    \
+        ncclResult_t r_ = (x);                                                              \
+        if (r_ != ncclSuccess)                                                              \
+            throw std::runtime_error(std::string("RCCL error ") +                           \
+                                     RcclApi::get().GetErrorString(r_) + " at " #x);        \
+    } while (0)
+
+class RcclComm : public Comm {
+  public:
+    RcclComm(const ncclUniqueId &id, int size, int rank, int device) : Comm(rank, size) {
+        COMM_HIP(hipSetDevice(device));
+        RCCL_CHECK(RcclApi::get().CommInitRank(&comm_, size, id, rank));
+    }
+    ~RcclComm() override {
+        if (comm_) (void)RcclApi::get().CommDestroy(comm_);
+    }
+    void allreduce_sum_u64(uint64_t *d, size_t n, hipStream_t s) override {
+        RCCL_CHECK(RcclApi::get().AllReduce(d, d, n, ncclUint64, ncclSum, comm_, s));
+    }
+    void allgather_u64(const uint64_t *d_send, uint64_t *d_recv, size_t n, hipStream_t s) override {
+        RCCL_CHECK(RcclApi::get().AllGather(d_send, d_recv, n, ncclUint64, comm_, s));
+    }
+    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                   const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
+        const RcclApi &api = RcclApi::get();
+        // messages go out in pieces of at most 1 GiB (counts are size_t, but bounded pieces keep
+        // every transfer inside RCCL's well-trodden sizes); pieces of one peer match in order
+        constexpr size_t PIECE = size_t(1) << 30;
+        const char *src = (const char *)d_send;
+        char *dst = (char *)d_recv;
+        // own slice: a device copy
+        if (scnt[rank_])
+            COMM_HIP(hipMemcpyAsync(dst + roff[rank_] * esz, src + soff[rank_] * esz, scnt[rank_] * esz,
+                                    hipMemcpyDeviceToDevice, s));
+        RCCL_CHECK(api.GroupStart());
+        for (int p = 0; p < size_; ++p) {
+            if (p == rank_) continue;
+            for (size_t o = 0; o < scnt[p] * esz; o += PIECE)
+                RCCL_CHECK(api.Send(src + soff[p] * esz + o, std::min(PIECE, scnt[p] * esz - o), ncclInt8, p,
+                                    comm_, s));
+            for (size_t o = 0; o < rcnt[p] * esz; o += PIECE)
+                RCCL_CHECK(api.Recv(dst + roff[p] * esz + o, std::min(PIECE, rcnt[p] * esz - o), ncclInt8, p,
+                                    comm_, s));
+        }
+        RCCL_CHECK(api.GroupEnd());
+    }
+
+  private:
+    ncclComm_t comm_ = nullptr;
+};
+
+// ------------------------------------------------------------------- in-process rank threads
+struct LocalGroup {
+    explicit LocalGroup(int n) : size(n), slots(n), host(n) {}
+    int size;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    struct Slot {
+        const void *ptr = nullptr;
+        std::vector<uint64_t> soff, scnt;
+    };
+    std::vector<Slot> slots;
+    std::vector<std::vector<uint64_t>> host;
+
+    // a rank that failed never arrives: the others give up after a minute instead of hanging
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = generation;
+        if (++arrived == size) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return generation != gen; })) {
+            --arrived;
+            throw std::runtime_error("local exchange group: a peer rank did not arrive");
+        }
+    }
+};
+
+class LocalComm : public Comm {
+  public:
+    LocalComm(std::shared_ptr<LocalGroup> g, int rank) : Comm(rank, g->size), g_(std::move(g)) {}
+    void allreduce_sum_u64(uint64_t *d, size_t n, hipStream_t s) override {
+        auto &mine = g_->host[rank_];
+        mine.resize(n);
+        COMM_HIP(hipMemcpyAsync(mine.data(), d, n * 8, hipMemcpyDeviceToHost, s));
+        COMM_HIP(hipStreamSynchronize(s));
+        g_->barrier();
+        std::vector<uint64_t> sum(n, 0);
+        for (int r = 0; r < size_; ++r)
+            for (size_t i = 0; i < n; ++i) sum[i] += g_->host[r][i];
+        g_->barrier();
+        COMM_HIP(hipMemcpyAsync(d, sum.data(), n * 8, hipMemcpyHostToDevice, s));
+        COMM_HIP(hipStreamSynchronize(s));
+    }
+    void allgather_u64(const uint64_t *d_send, uint64_t *d_recv, size_t n, hipStream_t s) override {
+        auto &mine = g_->host[rank_];
+        mine.resize(n);
+        COMM_HIP(hipMemcpyAsync(mine.data(), d_send, n * 8, hipMemcpyDeviceToHost, s));
+        COMM_HIP(hipStreamSynchronize(s));
+        g_->barrier();
+        std::vector<uint64_t> all(n * size_);
+        for (int r = 0; r < size_; ++r) std::copy(g_->host[r].begin(), g_->host[r].end(), all.begin() + r * n);
+        g_->barrier();
+        COMM_HIP(hipMemcpyAsync(d_recv, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+        COMM_HIP(hipStreamSynchronize(s));
+    }
+    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                   const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
+        COMM_HIP(hipStreamSynchronize(s));  // the send buffer is complete before peers read it
+        auto &slot = g_->slots[rank_];
+        slot.ptr = d_send;
+        slot.soff.assign(soff, soff + size_);
+        slot.scnt.assign(scnt, scnt + size_);
+        g_->barrier();
+        for (int i = 0; i < size_; ++i) {
+            const auto &src = g_->slots[i];
+            if (src.scnt[rank_] != rcnt[i])
+                throw std::runtime_error("local all-to-all: count mismatch");
+            if (rcnt[i])
+                COMM_HIP(hipMemcpyAsync((char *)d_recv + roff[i] * esz,
+                                        (const char *)src.ptr + src.soff[rank_] * esz, rcnt[i] * esz,
+                                        hipMemcpyDeviceToDevice, s));
+        }
+        COMM_HIP(hipStreamSynchronize(s));
+        g_->barrier();  // nobody reuses its send buffer while a peer still copies from it
+    }
+
+  private:
+    std::shared_ptr<LocalGroup> g_;
+};
+
+}  // namespace mtg

@@ -1,0 +1,141 @@
+"""Parity of the multi-GPU build with the single-build oracle (through the C ABI).
+
+P ranks run in one process on the one GPU of the box (include/mtg_boss.h: mtg_comm_create_local,
+one host thread per rank, the same exchange steps as RCCL with device copies).  Every rank
+builds from its own share of the reads; the rank chunks, concatenated in rank order with
+BOSS::Chunk::extend (boss_chunk.cpp:230-270), must equal the oracle's chunk of ALL reads bit for
+bit -- the range partition, the three exchanges (k-mers, sink / in-edge queries, dummy sources)
+and the per-rank emission together reproduce the single build.
+"""
+import importlib
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from test_gpu_parity import _random_reads, assert_same
+from test_oracle_goldens import CONSTRUCT_SEQS
+
+boss = importlib.import_module("projects2014-metagenome_amd.boss")
+
+pytestmark = pytest.mark.gpu
+
+
+def dist_chunks(k, shares, canonical=False, bits=0, counts=None):
+    """Per-rank chunks of one build: shares[r] = the reads of rank r."""
+    P = len(shares)
+    comms = boss.Comm.local_group(P)
+    ctors = [boss.IBOSSChunkConstructor.initialize(k, both_strands=canonical, bits_per_count=bits)
+             for _ in range(P)]
+    for r in range(P):
+        if counts is None:
+            if shares[r]:
+                ctors[r].add_sequences(shares[r])
+        elif shares[r]:
+            ctors[r].add_sequences(list(zip(shares[r], counts[r])))
+    out, errs = [None] * P, []
+
+    def run(r):
+        try:
+            out[r] = ctors[r].build_chunk(comm=comms[r])
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append((r, e))
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    assert all(c is not None for c in out)
+    return out
+
+
+def check_dist(k, seqs, P, canonical=False, bits=0, counts=None, split="round_robin"):
+    if split == "round_robin":
+        shares = [seqs[r::P] for r in range(P)]
+        cshares = None if counts is None else [counts[r::P] for r in range(P)]
+    else:  # everything on the last rank: the others only own ranges
+        shares = [[] for _ in range(P - 1)] + [list(seqs)]
+        cshares = None if counts is None else [[] for _ in range(P - 1)] + [list(counts)]
+    chunks = dist_chunks(k, shares, canonical, bits, cshares)
+    got = boss.concatenate(chunks)
+    want = O.build_chunk(k, seqs, canonical=canonical, bits_per_count=bits, counts=counts)
+    assert_same(got, want, "k=%d P=%d canonical=%s bits=%d" % (k, P, canonical, bits))
+    return chunks
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("canonical", [False, True])
+def test_dist_construct_seqs_every_k(P, canonical):
+    for k in range(1, 85):
+        check_dist(k, CONSTRUCT_SEQS, P, canonical, bits=8 if k % 3 == 0 else 0)
+
+
+@pytest.mark.parametrize("canonical,nodes", [(False, 591997), (True, 1159851)])
+def test_dist_transcripts_k20(transcripts_1000, canonical, nodes):
+    chunks = check_dist(19, transcripts_1000, 4, canonical, bits=8)
+    assert sum(c.n_real for c in chunks) == nodes
+    # the ranges are balanced: no rank owns more than twice its share of the real edges
+    assert max(c.n_real for c in chunks) < 2 * nodes / 4
+
+
+@pytest.mark.parametrize("k", [2, 15, 30, 31, 32, 45, 63, 64, 70])
+def test_dist_random_reads(k):
+    reads = _random_reads(100 + k, 400, 150, 4000, n_rate=0.01, lower=True)
+    check_dist(k, reads, 3, canonical=k % 2 == 1, bits=8 if k % 2 else 0)
+    check_dist(k, reads, 2, canonical=k % 2 == 0, bits=16)
+
+
+def test_dist_counts_saturate_across_ranks():
+    # the same k-mers on every rank: counts add across ranks and saturate at the owner
+    rng = np.random.default_rng(11)
+    seqs = _random_reads(9, 400, 12, 120)
+    counts = rng.integers(1, 200, size=len(seqs)).tolist()
+    for bits in (4, 8, 16):
+        for canonical in (False, True):
+            check_dist(11, seqs, 4, canonical, bits, counts)
+
+
+def test_dist_empty_and_lopsided_ranks():
+    reads = _random_reads(5, 300, 150, 3000)
+    for P in (2, 5, 8):
+        check_dist(30, reads, P, True, 8, split="last")
+    check_dist(30, [], 3, True, 8)
+    check_dist(5, ["ACGT" * 10], 4, False, 0)
+    check_dist(1, CONSTRUCT_SEQS, 4, True, 8)
+
+
+def test_dist_large_multi_tile():
+    reads = _random_reads(77, 30000, 150, 400000, n_rate=0.0005)
+    for P, canonical in ((2, True), (4, True), (8, False)):
+        check_dist(30, reads, P, canonical, bits=8)
+
+
+def test_dist_timings_report_exchange():
+    reads = _random_reads(3, 2000, 150, 20000)
+    P = 2
+    comms = boss.Comm.local_group(P)
+    ctors = [boss.IBOSSChunkConstructor.initialize(30, both_strands=True) for _ in range(P)]
+    for r in range(P):
+        ctors[r].add_sequences(reads[r::P])
+    ts = [threading.Thread(target=lambda r=r: ctors[r].build_chunk(comm=comms[r])) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    for c in ctors:
+        t = c.timings()
+        assert t.world == P and t.exchange_ms > 0 and t.n_sent > 0
+
+
+def test_dist_rccl_single_rank():
+    # the RCCL communicator itself (a one-rank group on this box's one GPU)
+    comm = boss.Comm.rccl(boss.Comm.unique_id(), 1, 0, 0)
+    assert comm.rank == 0 and comm.size == 1
+    reads = _random_reads(8, 500, 150, 5000)
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, bits_per_count=8)
+    ctor.add_sequences(reads)
+    got = ctor.build_chunk(comm=comm)
+    assert_same(got, O.build_chunk(30, reads, canonical=True, bits_per_count=8), "rccl P=1")
