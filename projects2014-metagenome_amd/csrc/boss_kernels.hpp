@@ -346,13 +346,42 @@ __global__ __launch_bounds__(256) void rc_map_kernel(const Key<L> *__restrict__ 
  * search inside one bucket (the probes of a wave land in a few neighbouring buckets).
  */
 template <int L>
-__global__ void bucket_index_kernel(const Key<L> *__restrict__ keys, uint64_t n, unsigned shift,
-                                    uint64_t nbuckets, uint64_t *__restrict__ start) {
+__global__ __launch_bounds__(256) void bucket_index_kernel(const Key<L> *__restrict__ keys, uint64_t n,
+                                                           unsigned shift, uint64_t nbuckets,
+                                                           uint64_t *__restrict__ start) {
+    // key i fills start[bucket(i-1)+1 .. bucket(i)] = i; a long run of empty buckets (keys
+    // clustered in part of the prefix space, e.g. one rank's range) is filled by the whole
+    // workgroup instead of one thread
+    constexpr int SHORT = 16;
+    __shared__ uint64_t s_lo[256], s_hi[256], s_v[256];
+    __shared__ uint32_t s_n;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
-        uint64_t b = i < n ? bits_at(shr(keys[i], shift), 0, 32) : nbuckets;
-        uint64_t bp = i > 0 ? bits_at(shr(keys[i - 1], shift), 0, 32) + 1 : 0;
-        for (uint64_t x = bp; x <= b && x <= nbuckets; ++x) start[x] = i;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 <= n; i0 += stride) {
+        const uint64_t i = i0 + threadIdx.x;
+        if (i <= n) {
+            const uint64_t b = i < n ? bits_at(shr(keys[i], shift), 0, 32) : nbuckets;
+            const uint64_t bp = i > 0 ? bits_at(shr(keys[i - 1], shift), 0, 32) + 1 : 0;
+            const uint64_t hi = min(b, nbuckets);
+            if (bp <= hi) {
+                if (hi - bp < SHORT) {
+                    for (uint64_t x = bp; x <= hi; ++x) start[x] = i;
+                } else {
+                    const uint32_t q = atomicAdd(&s_n, 1u);
+                    s_lo[q] = bp;
+                    s_hi[q] = hi;
+                    s_v[q] = i;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t cnt = s_n;
+        for (uint32_t q = 0; q < cnt; ++q)
+            for (uint64_t x = s_lo[q] + threadIdx.x; x <= s_hi[q]; x += blockDim.x) start[x] = s_v[q];
+        __syncthreads();
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
     }
 }
 

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -48,7 +49,7 @@ class Workspace {
         MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
-        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, NSLOTS
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -134,6 +135,7 @@ struct Ctx {
     bool dummy_msd = false;        // MTG_DUMMY_SORT=msd: MSD for the dummy k-mers (default LSD:
                                    // their $-padded keys crowd a few top-digit buckets)
     bool debug = false;            // MTG_DEBUG=1: host-side checks between stages
+    bool trace = false;            // MTG_TRACE=1: per-step wall times and sizes of the dist build
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -262,9 +264,12 @@ static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
 template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
-                                double dup, const uint32_t *hist1 = nullptr, bool distinct = false) {
+                                double dup, const uint32_t *hist1 = nullptr, bool distinct = false,
+                                const std::vector<uint64_t> *runs = nullptr) {
     // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them;
-    // distinct: the input has no duplicates (the local pass skips its hash table)
+    // distinct: the input has no duplicates (the local pass skips its hash table);
+    // runs: the input is runs->size() - 1 sorted runs at these offsets (one gather replaces
+    // the partition passes)
     if (n == 0) return 0;
     constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
     constexpr int TILE = MsdTraits<L>::TILE;
@@ -334,7 +339,37 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         if (COUNTED) std::swap(*vals, *valt);
         b = bb;
     };
-    for (unsigned lev = 1; lev <= levels; ++lev) run_level(lev);
+    if (runs && runs->size() > 2 && runs->size() <= 129 && levels) {
+        // bucket layout of the top T bits straight from the runs' own order
+        const unsigned T = digit_end[levels];
+        const uint32_t P = (uint32_t)runs->size() - 1;
+        nbuckets = 1ull << T;
+        uint64_t *idx = (uint64_t *)c.ws.get(Workspace::RUN_IDX, (uint64_t)P * (nbuckets + 1) * 8);
+        int64_t *delta = (int64_t *)c.ws.get(Workspace::RUN_DELTA, (uint64_t)P * nbuckets * 8);
+        for (uint32_t j = 0; j < P; ++j) {
+            const uint64_t r0 = (*runs)[j], rn = (*runs)[j + 1] - r0;
+            const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(rn + 1, 256), 8192));
+            bucket_index_kernel<L><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(
+                *keys + r0, rn, nbits - T, nbuckets, idx + (uint64_t)j * (nbuckets + 1));
+            HIP_CHECK(hipGetLastError());
+        }
+        bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nbuckets + 1) * 8);
+        runs_delta_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(nbuckets + 1, 256), 16384)), dim3(256), 0,
+                            c.stream>>>(idx, P, nbuckets, bstart, delta);
+        HIP_CHECK(hipGetLastError());
+        uint64_t *droff = (uint64_t *)c.ws.get(Workspace::RUN_OFF, (P + 1) * 8);
+        HIP_CHECK(hipMemcpyAsync(droff, runs->data(), (P + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        runs_gather_kernel<L, COUNTED><<<dim3((unsigned)std::min<uint64_t>(ceil_div(n, 256), 65536)), dim3(256), 0,
+                                         c.stream>>>(*keys, COUNTED ? *vals : nullptr, n, droff, P, delta,
+                                                     nbuckets, nbits, T, *alt, COUNTED ? *valt : nullptr);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // `runs` is the caller's host vector
+        std::swap(*keys, *alt);
+        if (COUNTED) std::swap(*vals, *valt);
+        b = T;
+    } else {
+        for (unsigned lev = 1; lev <= levels; ++lev) run_level(lev);
+    }
 
     while (true) {
         // groups of consecutive buckets holding <= G keys; bigger buckets stand alone
@@ -932,6 +967,21 @@ __global__ void gather_strided_kernel(const uint64_t *__restrict__ src, uint64_t
     if (j < cnt) dst[j] = src[(uint64_t)j * stride];
 }
 
+// MTG_TRACE: host wall time since the previous trace point (stream drained first)
+struct Tracer {
+    Ctx &c;
+    int rank;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void operator()(const char *what, uint64_t a = 0, uint64_t b = 0) {
+        if (!c.trace) return;
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[mtg trace r%d] %-22s %9.3f ms  %lu %lu\n", rank, what,
+                std::chrono::duration<double, std::milli>(now - t).count(), (unsigned long)a, (unsigned long)b);
+        t = now;
+    }
+};
+
 struct Dist {
     Comm &comm;
     int P, me;
@@ -984,7 +1034,8 @@ static std::vector<uint64_t> dist_ranges(Ctx &c, Dist &d, int na, const Key<L2> 
 template <typename T>
 static uint64_t exchange_runs(Ctx &c, Dist &d, int na, const T *const *arrs, const uint32_t *const *cnts,
                          const std::vector<std::vector<uint64_t>> &soff, Workspace::Slot rslot,
-                         Workspace::Slot rcslot, T **recv, uint32_t **recvc) {
+                         Workspace::Slot rcslot, T **recv, uint32_t **recvc,
+                         std::vector<uint64_t> *runs = nullptr) {
     const int P = d.P;
     std::vector<uint64_t> scnt(na * P);
     for (int a = 0; a < na; ++a)
@@ -1019,6 +1070,10 @@ static uint64_t exchange_runs(Ctx &c, Dist &d, int na, const T *const *arrs, con
     }
     HIP_CHECK(hipStreamSynchronize(c.stream));
     d.xev.push_back({e0, d.tm->mark()});
+    if (runs) {  // where every received run starts (array-major, then source rank) + the end
+        runs->assign(roff.begin(), roff.end());
+        runs->push_back(total);
+    }
     return total;
 }
 
@@ -1081,13 +1136,16 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     // ---- K1-K3 on this rank's reads
     K2 *ka, *kb;
     uint32_t *ca, *cb;
+    Tracer tr{c, d.me};
     const uint64_t N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
     const int ev_extract = tm.mark();
+    tr("extract", N);
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
     const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 8.0, true);
     const int ev_sort = tm.mark();
+    tr("local collect", Ul);
 
     // ---- exchange 1: the distinct k-mers by range of their own prefix, merged at the owner
     std::vector<std::vector<uint64_t>> soff;
@@ -1097,21 +1155,26 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         const uint64_t ns[1] = {Ul};
         b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff);
     }
+    tr("ranges 1");
     K2 *xa;
     uint32_t *xac = nullptr;
     {
         const K2 *arrs[1] = {ka};
         const uint32_t *cnts[1] = {ca};
+        std::vector<uint64_t> runs;
         const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA,
-                                         Workspace::XAC, &xa, &xac);
+                                              Workspace::XAC, &xa, &xac, &runs);
+        tr("exchange 1", n1);
         K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
         uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
         // the P runs are sorted and disjoint within a run; duplicates across runs collapse and
         // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover 1/P of
         // the prefix space, hence the denser plan.
-        T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, 1.0 / d.P, nullptr);
+        T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, 1.0 / d.P, nullptr,
+                                                  false, &runs);
     }
     const uint64_t U = T.n_unique;
+    tr("owner dedupe", U);
     debug_check_sorted(c, "owned k-mers", xa, U);
     const int ev_unique = tm.mark();
 
@@ -1130,21 +1193,27 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         const K2 *arrs[2] = {xa, rk};
         const uint32_t *cnts[2] = {xac, rkc};
         const uint64_t ns[2] = {U, Urc};
+        tr("rc", Urc);
         bounds = dist_ranges<L2>(c, d, 2, arrs, ns, &soff);
+        tr("ranges 2");
         K2 *ra;
         uint32_t *rac = nullptr;
+        std::vector<uint64_t> runs;
         const uint64_t n2 = exchange_runs<K2>(c, d, 2, arrs, COUNTED ? cnts : nullptr, soff, Workspace::REAL,
-                                         Workspace::REALC, &ra, &rac);
+                                              Workspace::REALC, &ra, &rac, &runs);
+        tr("exchange 2", n2);
         K2 *rb = (K2 *)c.ws.get(Workspace::KB, n2 * sizeof(K2));
         uint32_t *rbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, n2 * 4) : nullptr;
         // all 2P runs are distinct keys (a canonical k-mer and its rc are different edges)
-        R = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rac, &rbc, n2, 2 * K, cmax, 1.0 / d.P, nullptr, true);
+        R = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rac, &rbc, n2, 2 * K, cmax, 1.0 / d.P, nullptr, true,
+                                         &runs);
         E = ra;
         Ec = rac;
     } else {
         bounds = b1;  // basic mode: exchange 1 already placed every edge at its final owner
     }
     T.n_real = R;
+    tr("owner merge", R);
     debug_check_sorted(c, "real k-mers (owned)", E, R);
     const int ev_rc = tm.mark();
 
@@ -1172,17 +1241,20 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         K2 *qs = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(R, 1) * sizeof(K2));
         std::vector<std::vector<uint64_t>> qoff(1);
         qoff[0] = route<L2, 0>(c, d, E, R, K, d.shift2, 2 * d.m, bounds, qs);
+        tr("first flags + route q", R);
         K2 *qr;
         uint32_t *unused_c = nullptr;
         const K2 *qarr[1] = {qs};
         const uint64_t nq = exchange_runs<K2>(c, d, 1, qarr, nullptr, qoff, Workspace::QRECV, Workspace::XAC,
                                          &qr, &unused_c);
+        tr("exchange q", nq);
         uint8_t *qflag = (uint8_t *)c.ws.get(Workspace::QFLAG, nq + 1);
         if (nq) {
             query_answer_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(nq, 256), 65536)), dim3(256), 0,
                                       c.stream>>>(E, R, bstart, bshift, qr, nq, in_flag, qflag);
             HIP_CHECK(hipGetLastError());
         }
+        tr("answer q", nq);
         // sinks of the missed queries: count + scan now, written once the buffer is sized
         const uint64_t qtiles = ceil_div(nq, RT_TILE);
         uint32_t *qtcnt = (uint32_t *)c.ws.get(Workspace::QTCNT, (qtiles + 1) * 4);
@@ -1200,6 +1272,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
             HIP_CHECK(hipGetLastError());
             nsink = read_u64(c, (const unsigned long long *)(qtoff + qtiles));
         }
+        tr("sink count", nsink);
         // sources of the owned edges (in_flag is complete: every rank's queries are answered)
         const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
         uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
@@ -1223,6 +1296,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
                                                                                             toff, src);
             HIP_CHECK(hipGetLastError());
         }
+        tr("sources", nsrc);
         K3 *ssend = (K3 *)c.ws.get(Workspace::DSEND, std::max<uint64_t>(nsrc, 1) * sizeof(K3));
         std::vector<std::vector<uint64_t>> doff(1);
         doff[0] = route<L3, 1>(c, d, src, nsrc, K, 3 * K - 3 * d.m, 3 * d.m, lifted_bounds(bounds, d.m), ssend);
@@ -1231,6 +1305,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         const uint64_t nsrc_in = exchange_runs<K3>(c, d, 1, darr, nullptr, doff, Workspace::DRECV, Workspace::XAC,
                                               &drecv, &unused_c);
         const uint64_t Draw = nsink + nsrc_in;
+        tr("route + exchange src", nsrc_in);
         if (Draw) {
             K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
             K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
@@ -1242,7 +1317,9 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
             if (nsrc_in)
                 HIP_CHECK(hipMemcpyAsync(da + nsink, drecv, nsrc_in * sizeof(K3), hipMemcpyDeviceToDevice,
                                          c.stream));
+            tr("sink write", Draw);
             D = sort_unique_dummies<L3>(c, K, da, db, Draw, &dk);
+            tr("dummy sort", D);
         }
     }
     T.n_dummy = D + (d.me == 0 ? 1 : 0);
@@ -1253,6 +1330,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     int ev_merge;
     stage_merge_emit<L2, L3, COUNTED>(c, tm, &ev_merge, k, bits, E, Ec, R, dk, D, d.me == 0, out);
     const int ev_emit = tm.mark();
+    tr("merge + emit", out->n);
     check_error_word(c);
     HIP_CHECK(hipStreamSynchronize(c.stream));
 
@@ -1362,6 +1440,7 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         const char *emitenv = getenv("MTG_EMIT");
         c->ctx.emit_slow = emitenv && std::string(emitenv) == "slow";
         c->ctx.debug = getenv("MTG_DEBUG") != nullptr;
+        c->ctx.trace = getenv("MTG_TRACE") != nullptr;
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;

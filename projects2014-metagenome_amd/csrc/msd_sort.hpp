@@ -333,6 +333,53 @@ __global__ void group_scatter_kernel(const uint64_t *__restrict__ bstart,
     if (b == nbuckets) gstart[pos[nbuckets]] = n;
 }
 
+/*
+ * Sorted runs instead of partition passes: when the input is P sorted runs (the P slices a
+ * rank receives in the multi-GPU exchange), the bucket layout of the top T bits follows from
+ * one bucket index per run -- no histogram or partition pass.  runs_delta_kernel turns the
+ * per-run indexes idx[j][b] (keys of run j below bucket b) into the global bucket starts and,
+ * per (run, bucket), the shift from a key's run position to its bucket-major position (runs
+ * in order inside a bucket); runs_gather_kernel then moves every key once, streaming.
+ */
+__global__ void runs_delta_kernel(const uint64_t *__restrict__ idx, uint32_t P, uint64_t nb,
+                                  uint64_t *__restrict__ bstart, int64_t *__restrict__ delta) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= nb; b += stride) {
+        uint64_t s = 0;
+        for (uint32_t j = 0; j < P; ++j) s += idx[(uint64_t)j * (nb + 1) + b];
+        bstart[b] = s;
+        if (b == nb) continue;
+        uint64_t o = s;
+        for (uint32_t j = 0; j < P; ++j) {
+            const uint64_t lo = idx[(uint64_t)j * (nb + 1) + b], hi = idx[(uint64_t)j * (nb + 1) + b + 1];
+            delta[(uint64_t)j * nb + b] = (int64_t)o - (int64_t)lo;
+            o += hi - lo;
+        }
+    }
+}
+
+template <int L, bool HAS_VAL>
+__global__ __launch_bounds__(256) void runs_gather_kernel(const Key<L> *__restrict__ kin,
+                                                          const uint32_t *__restrict__ vin, uint64_t n,
+                                                          const uint64_t *__restrict__ roff, uint32_t P,
+                                                          const int64_t *__restrict__ delta, uint64_t nb,
+                                                          unsigned nbits, unsigned T, Key<L> *__restrict__ kout,
+                                                          uint32_t *__restrict__ vout) {
+    __shared__ uint64_t s_off[129];  // up to 128 runs (two arrays from 64 ranks)
+    for (uint32_t j = threadIdx.x; j <= P; j += blockDim.x) s_off[j] = roff[j];
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t j = 0;
+        while (j + 1 < P && s_off[j + 1] <= i) ++j;
+        const Key<L> k = kin[i];
+        const uint32_t b = key_prefix(k, nbits, T);
+        const uint64_t o = (uint64_t)((int64_t)(i - s_off[j]) + delta[(uint64_t)j * nb + b]);
+        kout[o] = k;
+        if (HAS_VAL) vout[o] = vin[i];
+    }
+}
+
 template <int L>
 struct LocalTraits {
     // hash slots per group: keys (+ state) (+ u32 counts) within the LDS budget

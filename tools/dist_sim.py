@@ -1,0 +1,86 @@
+"""Multi-rank build on ONE GPU (in-process rank group) vs the single build of the same reads.
+
+    python tools/dist_sim.py --ranks 2 --reads 5000000
+
+Each of P ranks holds --reads reads sampled from one shared genome (10x over all P ranks), as in
+bench.py --gpus P.  The P ranks share the device, so the wall time is roughly the SUM of their
+work; comparing it with one single-GPU build of all P * reads reads gives the work the
+distributed algorithm adds (exchanges here are device copies, not xGMI).
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=2)
+    ap.add_argument("--reads", type=int, default=5_000_000)
+    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--steps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    boss = importlib.import_module("projects2014-metagenome_amd.boss")
+    dev = torch.device("cuda", 0)
+    P = args.ranks
+    seqs = [bench.make_reads_device(torch, args.reads, 150, 1000 + r, "genome", 10.0, dev, P)
+            for r in range(P)]
+    whole = torch.cat(seqs)
+    torch.cuda.synchronize()
+    kb = args.k - 1
+    single = boss.IBOSSChunkConstructor.initialize(kb, both_strands=True)
+    for _ in range(2):
+        single.build_device(whole.data_ptr(), whole.numel())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dc = single.build_device(whole.data_ptr(), whole.numel())
+    t_single = (time.perf_counter() - t0) / args.steps
+    ts = single.timings().as_dict()
+    rows_single = dc.n
+
+    comms = boss.Comm.local_group(P)
+    ctors = [boss.IBOSSChunkConstructor.initialize(kb, both_strands=True) for _ in range(P)]
+    res = [None] * P
+
+    def run(r):
+        res[r] = ctors[r].build_device(seqs[r].data_ptr(), seqs[r].numel(), comm=comms[r])
+
+    def step():
+        th = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    step()
+    step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    t_dist = (time.perf_counter() - t0) / args.steps
+    rows_dist = sum(c.n for c in res) - (P - 1)
+    assert rows_dist == rows_single, (rows_dist, rows_single)
+    per_rank = [c.timings().as_dict() for c in ctors]
+    keys = ("extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms", "merge_ms", "emit_ms",
+            "total_ms", "exchange_ms")
+    print(json.dumps({
+        "ranks": P, "reads_per_rank": args.reads, "rows": rows_single,
+        "single_ms": t_single * 1e3, "dist_wall_ms": t_dist * 1e3,
+        "single_stages": {k: round(ts[k], 2) for k in keys if k in ts},
+        "rank_stages": [{k: round(t[k], 2) for k in keys} for t in per_rank],
+        "n_sent": [t["n_sent"] for t in per_rank],
+        "n_real": [t["n_real"] for t in per_rank],
+    }, indent=1))
+
+
+if __name__ == "__main__":
+    main()
