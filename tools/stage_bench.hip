@@ -113,6 +113,144 @@ __global__ __launch_bounds__(512) void hist_variant(const Key<1> *__restrict__ k
     }
 }
 
+/*
+ * EXPERIMENT (measured, not used by the library): persistent form of the partition pass: gridDim.x workgroups (one per CU) walk the tiles
+ * tile = blockIdx.x, blockIdx.x + gridDim.x, ... and keep the NEXT tile's keys in flight in
+ * registers while the current one is ranked, reserved (one cursor atomic per (tile, bucket)),
+ * reordered in LDS and written.  The reservation atomics are issued before the prefetch, so
+ * waiting for them does not wait for the prefetch; the LDS tile (16 K keys at 1024 threads)
+ * allows one workgroup per CU, whose phases would otherwise never overlap.
+ */
+template <int L, bool HAS_VAL, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void msd_partition_pipe_kernel(
+    const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
+    uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
+    unsigned long long *__restrict__ cursor, uint64_t ntiles,
+    const unsigned long long *__restrict__ fake_start = nullptr) {
+    // fake_start (microbenchmark only): no reservation atomics, runs land at a tile-dependent
+    // place inside their bucket -- the same write pattern without the atomics' cost
+    constexpr int ITEMS = MsdTraits<L>::ITEMS;
+    constexpr int TILE = ITEMS * BLOCK;
+    constexpr int WMAX = MSD_WIN << 8;
+    constexpr int PER = WMAX / BLOCK > 0 ? WMAX / BLOCK : 1;
+    __shared__ Key<L> s_keys[TILE];
+    __shared__ uint32_t s_vals[HAS_VAL ? TILE : 1];
+    __shared__ uint32_t s_cnt[WMAX];
+    __shared__ uint32_t s_loff[WMAX];
+    __shared__ unsigned long long s_gbase[WMAX];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    __shared__ uint32_t s_wbase;
+
+    const uint32_t tid = threadIdx.x;
+    const unsigned sub = b - bp;
+    const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);
+    uint64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+
+    Key<L> k[ITEMS];
+    uint32_t v[ITEMS];
+    auto load = [&](uint64_t t, Key<L> (&kk)[ITEMS], uint32_t (&vv)[ITEMS]) {
+        const uint64_t base = t * TILE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t i = base + (uint64_t)j * BLOCK + tid;
+            kk[j] = i < n ? kin[i] : Key<L>::zero();
+            if (HAS_VAL) vv[j] = i < n ? vin[i] : 0;
+        }
+    };
+    load(tile, k, v);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const uint64_t base = tile * TILE;
+        for (uint32_t i = tid; i < wsize; i += BLOCK) s_cnt[i] = 0;
+        if (tid == 0) s_wbase = key_prefix(k[0], nbits, bp) << sub;
+        __syncthreads();
+        const uint32_t wbase = s_wbase;
+        uint32_t r[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            r[j] = 0xFFFFFFFFu;
+            if (base + (uint64_t)j * BLOCK + tid < n) {
+                const uint32_t lb = key_prefix(k[j], nbits, b) - wbase;
+                if (lb < wsize) {
+                    r[j] = atomicAdd(&s_cnt[lb], 1u);
+                } else {
+                    const unsigned long long o = atomicAdd(&cursor[lb + wbase], 1ull);
+                    kout[o] = k[j];
+                    if (HAS_VAL) vout[o] = v[j];
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t c[PER];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t i = tid * PER + q;
+            c[q] = i < wsize ? s_cnt[i] : 0;
+            sum += c[q];
+        }
+        uint32_t total;
+        uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+        unsigned long long g[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t i = tid * PER + q;
+            g[q] = 0;
+            if (i < wsize) {
+                s_loff[i] = off;
+                if (c[q]) {
+                    if (fake_start) {
+                        const unsigned long long bs = fake_start[wbase + i], be = fake_start[wbase + i + 1];
+                        const unsigned long long room = be - bs > c[q] ? be - bs - c[q] : 0;
+                        g[q] = bs + (room ? (tile * c[q]) % room : 0);
+                    } else {
+                        g[q] = atomicAdd(&cursor[wbase + i], (unsigned long long)c[q]);
+                    }
+                }
+            }
+            off += c[q];
+        }
+        // the next tile's keys travel while this one is reordered and written
+        Key<L> kn[ITEMS];
+        uint32_t vn[ITEMS];
+        const uint64_t next = tile + gridDim.x;
+        if (next < ntiles) load(next, kn, vn);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            if (r[j] != 0xFFFFFFFFu) {
+                const uint32_t lb = key_prefix(k[j], nbits, b) - wbase;
+                const uint32_t pos = s_loff[lb] + r[j];
+                s_keys[pos] = k[j];
+                if (HAS_VAL) s_vals[pos] = v[j];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t i = tid * PER + q;
+            if (i < wsize) s_gbase[i] = g[q];
+        }
+        __syncthreads();
+        for (uint32_t p = tid; p < total; p += BLOCK) {
+            const Key<L> key = s_keys[p];
+            const uint32_t lb = key_prefix(key, nbits, b) - wbase;
+            const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
+            kout[o] = key;
+            if (HAS_VAL) vout[o] = s_vals[p];
+        }
+        __syncthreads();
+        if (next < ntiles) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                k[j] = kn[j];
+                if (HAS_VAL) v[j] = vn[j];
+            }
+        }
+    }
+}
+// Result on MI355X: no faster than msd_partition_kernel (bits 6/8/9: 4.29/5.01/5.32 ms vs
+// 3.89/4.81/5.27 ms); without the reservation atomics (fake_start) it is slower still.
+
 // level-1 MSD partition of n random keys: histogram, host scan, partition with cursor strides
 static void partition_bench(hipStream_t s, uint64_t n) {
     Key<1> *a, *b;
@@ -177,6 +315,58 @@ static void partition_bench(hipStream_t s, uint64_t n) {
                 });
                 printf("mode %d partition bits=%u block=%d: %.3f ms = %.0f GB/s\n", mode, bits, blk, t,
                        2.0 * n * 8 / 1e9 / (t * 1e-3));
+            }
+            int ncu = 0;
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+            for (int blk : {512, 1024}) {
+                for (int per_cu : {1, 2, 4}) {
+                    if (blk == 1024 && per_cu > 1) continue;
+                    const uint64_t ptiles = ceil_div(n, (uint64_t)MsdTraits<1>::ITEMS * blk);
+                    const unsigned grid = (unsigned)std::min<uint64_t>(ptiles, (uint64_t)ncu * per_cu);
+                    t = time_ms(s, 3, [&] {
+                        HIP_CHECK(hipMemcpyAsync(cur2, st2.data(), (1u << bits) * 8, hipMemcpyHostToDevice, s));
+                        if (blk == 512)
+                            msd_partition_pipe_kernel<1, false, 512><<<dim3(grid), dim3(512), 0, s>>>(
+                                a, b, nullptr, nullptr, n, 62, bits, 0, cur2, ptiles);
+                        else
+                            msd_partition_pipe_kernel<1, false, 1024><<<dim3(grid), dim3(1024), 0, s>>>(
+                                a, b, nullptr, nullptr, n, 62, bits, 0, cur2, ptiles);
+                    });
+                    printf("mode %d pipe partition bits=%u block=%d grid=%u: %.3f ms = %.0f GB/s\n", mode, bits, blk,
+                           grid, t, 2.0 * n * 8 / 1e9 / (t * 1e-3));
+                }
+            }
+            {   // the same write pattern without the reservation atomics
+                unsigned long long *fs;
+                std::vector<unsigned long long> st3(st2);
+                st3.push_back(n);
+                HIP_CHECK(hipMalloc(&fs, st3.size() * 8));
+                HIP_CHECK(hipMemcpy(fs, st3.data(), st3.size() * 8, hipMemcpyHostToDevice));
+                const uint64_t ptiles = ceil_div(n, (uint64_t)MsdTraits<1>::ITEMS * 1024);
+                t = time_ms(s, 3, [&] {
+                    msd_partition_pipe_kernel<1, false, 1024><<<dim3((unsigned)ncu), dim3(1024), 0, s>>>(
+                        a, b, nullptr, nullptr, n, 62, bits, 0, cur2, ptiles, fs);
+                });
+                printf("mode %d pipe partition bits=%u block=1024 NO ATOMICS: %.3f ms = %.0f GB/s\n", mode, bits, t,
+                       2.0 * n * 8 / 1e9 / (t * 1e-3));
+                HIP_CHECK(hipFree(fs));
+                HIP_CHECK(hipMemcpyAsync(cur2, st2.data(), (1u << bits) * 8, hipMemcpyHostToDevice, s));
+                msd_partition_pipe_kernel<1, false, 1024><<<dim3((unsigned)ncu), dim3(1024), 0, s>>>(
+                    a, b, nullptr, nullptr, n, 62, bits, 0, cur2, ptiles);
+                HIP_CHECK(hipStreamSynchronize(s));
+            }
+            {   // check the pipe kernel's output is a partition of the input (bucket counts + sum)
+                std::vector<unsigned long long> cend(1u << bits);
+                HIP_CHECK(hipMemcpy(cend.data(), cur2, (1u << bits) * 8, hipMemcpyDeviceToHost));
+                bool ok = true;
+                for (uint32_t i = 0; i < (1u << bits); ++i) ok &= cend[i] == st2[i] + hh[i];
+                std::vector<uint64_t> ho(n);
+                HIP_CHECK(hipMemcpy(ho.data(), b, n * 8, hipMemcpyDeviceToHost));
+                uint64_t badb = 0;
+                for (uint32_t i = 0; i < (1u << bits); ++i)
+                    for (uint64_t q = st2[i]; q < st2[i] + hh[i]; ++q) badb += (ho[q] >> (62 - bits)) != i;
+                printf("pipe partition bits=%u check: cursors %s, %lu keys in a wrong bucket\n", bits,
+                       ok ? "ok" : "BAD", (unsigned long)badb);
             }
             HIP_CHECK(hipFree(cur2));
         }
