@@ -136,6 +136,17 @@ int mtg_boss_ctor_add_sequence(mtg_boss_ctor *ctor, const char *seq, uint64_t le
 int mtg_boss_ctor_add_packed(mtg_boss_ctor *ctor, const char *data, const uint64_t *offsets,
                              const uint64_t *counts, size_t n);
 
+/*
+ * A KMC1 k-mer counter database (`<base>.kmc_pre` + `<base>.kmc_suf`; either name or the base) as
+ * input: seq_io::read_kmers (seq_io/kmc_parser.cpp:27-62) + the build's KMC branch
+ * (cli/parse_sequences.hpp:50-101).  Every k-mer with min_count <= count < max_count becomes a
+ * one-k-mer sequence with that count; with call_both_from_canonical and a database of canonical
+ * k-mers, its reverse complement too (the reference passes graph_mode != CANONICAL).  The
+ * records are decoded on the device at build time.  Reference defaults: 1, 2^32 - 1.
+ */
+int mtg_boss_ctor_add_kmc(mtg_boss_ctor *ctor, const char *kmc_path, uint64_t min_count,
+                          uint64_t max_count, int call_both_from_canonical);
+
 /* builds from everything added so far, returns host arrays; clears the added input */
 int mtg_boss_ctor_build_chunk(mtg_boss_ctor *ctor, mtg_boss_chunk *out);
 void mtg_boss_chunk_free(mtg_boss_chunk *chunk);

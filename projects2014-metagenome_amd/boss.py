@@ -69,7 +69,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_device_count", "mtg_device_synchronize", "mtg_comm_get_unique_id",
            "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
-           "mtg_dist_bounds")
+           "mtg_dist_bounds", "mtg_boss_ctor_add_kmc")
 
 COMM_ID_BYTES = 128
 
@@ -126,6 +126,8 @@ def lib():
                                                  ctypes.c_uint64, ctypes.c_void_p,
                                                  ctypes.c_void_p, ctypes.c_uint64,
                                                  ctypes.c_void_p, P(_DeviceChunk)]
+        L.mtg_boss_ctor_add_kmc.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_int]
         L.mtg_dist_bounds.argtypes = [P(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_int,
                                       P(ctypes.c_uint64)]
         for name in EXPORTS:
@@ -171,10 +173,11 @@ class Chunk:
 
 
 class BOSSChunkConstructor:
-    def __init__(self, handle, k, bits_per_count):
+    def __init__(self, handle, k, bits_per_count, canonical=False):
         self._h = handle
         self._k = k
         self._bits = bits_per_count
+        self._canonical = canonical
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
@@ -203,6 +206,15 @@ class BOSSChunkConstructor:
             self._h, b"".join(bs), offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
             cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None,
             len(bs)))
+
+    def add_kmc(self, kmc_path, min_count=1, max_count=2**32 - 1,
+                call_both_from_canonical=None):
+        """KMC1 database input (cli/parse_sequences.hpp:50-101, seq_io/kmc_parser.cpp:27-62).
+        call_both_from_canonical defaults to what `metagraph build` passes: not canonical."""
+        if call_both_from_canonical is None:
+            call_both_from_canonical = not self._canonical
+        _check(lib().mtg_boss_ctor_add_kmc(self._h, os.fsencode(kmc_path), min_count, max_count,
+                                           int(bool(call_both_from_canonical))))
 
     def build_chunk(self, comm=None):
         """BOSS::Chunk of everything added; with `comm`, this rank's range of the global build
@@ -262,7 +274,7 @@ class IBOSSChunkConstructor:
         h = lib().mtg_boss_ctor_create(ctypes.byref(p))
         if not h:
             raise RuntimeError(lib().mtg_last_error().decode())
-        return BOSSChunkConstructor(h, k, bits_per_count)
+        return BOSSChunkConstructor(h, k, bits_per_count, bool(both_strands))
 
 
 class BOSSConstructor(BOSSChunkConstructor):

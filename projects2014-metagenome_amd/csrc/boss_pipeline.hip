@@ -23,6 +23,7 @@
 #include "boss_kernels.hpp"
 #include "comm.hpp"
 #include "dist_kernels.hpp"
+#include "kmc.hpp"
 #include "msd_sort.hpp"
 #include "radix_sort.hpp"
 
@@ -49,7 +50,7 @@ class Workspace {
         MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
-        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, NSLOTS
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -1386,6 +1387,7 @@ struct mtg_boss_ctor {
     std::vector<uint64_t> starts;    // start offset of every read in `data`
     std::vector<uint32_t> counts;    // per-read counts (clamped to u32)
     bool any_count_not_one = false;
+    std::vector<mtg::KmcInput> kmc;  // KMC databases, decoded on the device at build time
 };
 
 using namespace mtg;
@@ -1502,6 +1504,23 @@ int mtg_boss_ctor_add_packed(mtg_boss_ctor *c, const char *data, const uint64_t 
     return MTG_OK;
 }
 
+int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_count, uint64_t max_count,
+                          int call_both_from_canonical) {
+    if (!c || !kmc_path) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    try {
+        KmcInput in = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0);
+        std::lock_guard<std::mutex> lock(c->mu);
+        if (in.total) c->kmc.push_back(std::move(in));
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_ARGUMENT;
+    }
+}
+
 static int run_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {
     try {
         HIP_CHECK(hipSetDevice(c->device));
@@ -1552,18 +1571,42 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         hipStream_t s = c->ctx.stream;
         const uint64_t len = c->data.size();
         const uint64_t nr = c->starts.size();
-        uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, len + 1);
+        uint64_t kmc_bytes = 0, kmc_reads = 0;
+        for (const auto &m : c->kmc) {
+            kmc_bytes += m.total * (m.k + 1) * (m.both ? 2 : 1);
+            kmc_reads += m.total * (m.both ? 2 : 1);
+        }
+        const uint64_t total_len = len + kmc_bytes, total_reads = nr + kmc_reads;
+        uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
         if (len) HIP_CHECK(hipMemcpyAsync(dseq, c->data.data(), len, hipMemcpyHostToDevice, s));
         uint64_t *dstarts = nullptr;
         uint32_t *dcounts = nullptr;
-        const bool per_read = c->params.bits_per_count && c->any_count_not_one && nr;
+        const bool per_read = c->params.bits_per_count && (c->any_count_not_one || kmc_reads) && total_reads;
         if (per_read) {
-            dstarts = (uint64_t *)c->ctx.ws.get(Workspace::STARTS, nr * 8);
-            dcounts = (uint32_t *)c->ctx.ws.get(Workspace::RCOUNTS, nr * 4);
-            HIP_CHECK(hipMemcpyAsync(dstarts, c->starts.data(), nr * 8, hipMemcpyHostToDevice, s));
-            HIP_CHECK(hipMemcpyAsync(dcounts, c->counts.data(), nr * 4, hipMemcpyHostToDevice, s));
+            dstarts = (uint64_t *)c->ctx.ws.get(Workspace::STARTS, total_reads * 8);
+            dcounts = (uint32_t *)c->ctx.ws.get(Workspace::RCOUNTS, total_reads * 4);
+            if (nr) {
+                HIP_CHECK(hipMemcpyAsync(dstarts, c->starts.data(), nr * 8, hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(dcounts, c->counts.data(), nr * 4, hipMemcpyHostToDevice, s));
+            }
         }
-        BuildInput in{dseq, len, dstarts, dcounts, per_read ? nr : 0};
+        // KMC records -> reads, on the device (kmc.hpp)
+        uint64_t seq_base = len, read_base = nr;
+        for (const auto &m : c->kmc) {
+            uint64_t *dlut = (uint64_t *)c->ctx.ws.get(Workspace::KMC_LUT, m.lut.size() * 8);
+            uint8_t *drec = (uint8_t *)c->ctx.ws.get(Workspace::KMC_REC, m.records.size() + 1);
+            HIP_CHECK(hipMemcpyAsync(dlut, m.lut.data(), m.lut.size() * 8, hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipMemcpyAsync(drec, m.records.data(), m.records.size(), hipMemcpyHostToDevice, s));
+            kmc_decode_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m.total, 256), 65536))),
+                                dim3(256), 0, s>>>(drec, dlut, m.lut.size(), m.total, m.k, m.lut_len,
+                                                   m.counter_size, m.min_count, m.max_count, m.both ? 1 : 0,
+                                                   dseq, seq_base, dstarts, dcounts, read_base);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipStreamSynchronize(s));  // the slots are reused by the next database
+            seq_base += m.total * (m.k + 1) * (m.both ? 2 : 1);
+            read_base += m.total * (m.both ? 2 : 1);
+        }
+        BuildInput in{dseq, total_len, dstarts, dcounts, per_read ? total_reads : 0};
         BuildOutput o{};
         run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
                      c->params.bits_per_count, in, &o);
@@ -1589,6 +1632,7 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         c->starts.clear();
         c->counts.clear();
         c->any_count_not_one = false;
+        c->kmc.clear();
         return MTG_OK;
     } catch (const std::exception &e) {
         set_error(e.what());

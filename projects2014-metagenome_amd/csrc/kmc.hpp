@@ -1,0 +1,173 @@
+// kmc.hpp -- KMC1 k-mer counter databases as build input (BASELINE config 5, `metagraph build`
+// on a `.kmc_suf` / `.kmc_pre` pair).
+//
+// The reference reads them through the KMC API (seq_io/kmc_parser.cpp:27-62, CKMCFile in the
+// KMC submodule, absent here) and hands every k-mer to the constructor as a one-k-mer sequence
+// with its count (cli/parse_sequences.hpp:50-101), plus its reverse complement when the database
+// counted canonical k-mers and the graph is not canonical.  Here the host only reads the two
+// files; the records are decoded on the device, straight into the read buffer of the build
+// (k bases + '$' per record, per-read counts), so the rest of the path is the FASTA path.
+//
+// KMC1 layout (decoded from the reference's fixtures, tests/data/transcripts_1000_kmc_counters*):
+//   .kmc_pre  "KMCP" | u64 lut[4^lut_len] (first record of every prefix) | header | u32 header
+//             size | "KMCP";  header = u32 k, mode, counter_size, lut_len, min_count, max_count,
+//             u64 total, u32 flags (bit 0 = single strand: both_strands = !(flags & 1)), ...
+//   .kmc_suf  "KMCS" | total records of (k - lut_len) / 4 suffix bytes (2-bit A,C,G,T, first base
+//             in the high bits) + counter_size little-endian count bytes | "KMCS"
+// A record's k-mer is its prefix (lut_len bases, the index into lut) followed by its suffix.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace mtg {
+
+struct KmcInput {
+    unsigned k = 0, lut_len = 0, counter_size = 0;
+    uint32_t min_count = 0, max_count = 0;  // effective inclusive bounds
+    bool both = false;                     // also emit the reverse complement
+    uint64_t total = 0;
+    std::vector<uint64_t> lut;
+    std::vector<uint8_t> records;          // the suffix file without its markers
+};
+
+static std::string kmc_strip(const std::string &p) {
+    for (const char *suf : {".kmc_suf", ".kmc_pre"}) {
+        const size_t n = strlen(suf);
+        if (p.size() >= n && p.compare(p.size() - n, n, suf) == 0) return p.substr(0, p.size() - n);
+    }
+    return p;
+}
+
+static std::vector<uint8_t> read_file(const std::string &path) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("cannot open " + path);
+    std::vector<uint8_t> buf;
+    if (fseek(f, 0, SEEK_END) == 0) {
+        const long n = ftell(f);
+        if (n > 0) {
+            buf.resize((size_t)n);
+            fseek(f, 0, SEEK_SET);
+            if (fread(buf.data(), 1, buf.size(), f) != buf.size()) buf.clear();
+        }
+    }
+    fclose(f);
+    return buf;
+}
+
+// seq_io::read_kmers (kmc_parser.cpp:27-62): min/max as the reference passes them (max
+// exclusive), combined with the database's own cut-offs as CKMCFile::SetMin/MaxCount do
+static KmcInput kmc_open(const std::string &path, uint64_t min_count, uint64_t max_count,
+                         bool call_both_from_canonical) {
+    const std::string base = kmc_strip(path);
+    auto bad = [&](const char *why) {
+        return std::runtime_error("Error: Can't open KMC database " + base + " (" + why + ")");
+    };
+    std::vector<uint8_t> pre, suf;
+    try {
+        pre = read_file(base + ".kmc_pre");
+        suf = read_file(base + ".kmc_suf");
+    } catch (const std::exception &) {
+        throw bad("missing file");
+    }
+    if (pre.size() < 16 || memcmp(pre.data(), "KMCP", 4) || memcmp(pre.data() + pre.size() - 4, "KMCP", 4))
+        throw bad("no KMCP markers");
+    if (suf.size() < 8 || memcmp(suf.data(), "KMCS", 4) || memcmp(suf.data() + suf.size() - 4, "KMCS", 4))
+        throw bad("no KMCS markers");
+    uint32_t hsize;
+    memcpy(&hsize, pre.data() + pre.size() - 8, 4);
+    if (hsize < 36 || hsize + 12 > pre.size()) throw bad("header size");
+    const uint8_t *h = pre.data() + pre.size() - 8 - hsize;
+    uint32_t f[6];
+    memcpy(f, h, 24);
+    KmcInput in;
+    in.k = f[0];
+    in.counter_size = f[2];
+    in.lut_len = f[3];
+    memcpy(&in.total, h + 24, 8);
+    uint32_t flags;
+    memcpy(&flags, h + 32, 4);
+    uint32_t version = 0;
+    if (hsize >= 64) memcpy(&version, h + hsize - 4, 4);
+    if (version != 0) throw bad("only the KMC1 database layout is supported");
+    if (f[1] != 0) throw bad("quality-value (mode 1) databases are not supported");
+    if (in.k == 0 || in.k > 256 || in.lut_len > 16 || in.lut_len > in.k || (in.k - in.lut_len) % 4 ||
+        in.counter_size > 4)
+        throw bad("layout");
+    const uint64_t nlut = 1ull << (2 * in.lut_len);
+    if (4 + nlut * 8 + hsize + 8 > pre.size()) throw bad("prefix table");
+    in.lut.resize(nlut);
+    memcpy(in.lut.data(), pre.data() + 4, nlut * 8);
+    const uint64_t rec = (in.k - in.lut_len) / 4 + in.counter_size;
+    if (suf.size() - 8 != in.total * rec) throw bad("record count");
+    suf.erase(suf.end() - 4, suf.end());
+    suf.erase(suf.begin(), suf.begin() + 4);
+    in.records = std::move(suf);
+    const bool both_strands = (flags & 1) == 0;
+    in.both = call_both_from_canonical && both_strands;
+    // SetMinCount / SetMaxCount only narrow the database's own [min, max]
+    const uint64_t lo = std::max<uint64_t>(min_count, f[4]);
+    const uint64_t hi = max_count ? std::min<uint64_t>(max_count - 1, f[5]) : 0;
+    in.min_count = (uint32_t)std::min<uint64_t>(lo, 0xFFFFFFFFull);
+    in.max_count = (uint32_t)std::min<uint64_t>(hi, 0xFFFFFFFFull);
+    if (min_count >= max_count) in.total = 0;  // read_kmers returns without reading
+    return in;
+}
+
+/*
+ * One thread per record: its prefix (binary search of the prefix table), suffix and count;
+ * writes the k-mer as k ASCII bases + '$' (and its reverse complement after it when `both`),
+ * and the per-read start / count.  Records outside [min, max] become k 'N's: no k-mer.
+ */
+__global__ void kmc_decode_kernel(const uint8_t *__restrict__ rec, const uint64_t *__restrict__ lut,
+                                  uint64_t nlut, uint64_t total, unsigned k, unsigned lut_len,
+                                  unsigned counter_size, uint32_t min_count, uint32_t max_count,
+                                  int both, uint8_t *__restrict__ seq, uint64_t seq_base,
+                                  uint64_t *__restrict__ starts, uint32_t *__restrict__ counts,
+                                  uint64_t read_base) {
+    const unsigned slen = (k - lut_len) / 4, rsize = slen + counter_size;
+    const uint64_t stride = (uint64_t)(k + 1) * (both ? 2 : 1);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < total; r += gs) {
+        uint64_t lo = 0, hi = nlut;  // last prefix whose first record is <= r
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (lut[mid] <= r) lo = mid; else hi = mid;
+        }
+        const uint8_t *p = rec + r * rsize;
+        uint32_t cnt = 0;
+        for (unsigned b = 0; b < counter_size; ++b) cnt |= (uint32_t)p[slen + b] << (8 * b);
+        const bool keep = cnt >= min_count && cnt <= max_count;
+        uint8_t *o = seq + seq_base + r * stride;
+        const char *acgt = "ACGT";
+        for (unsigned i = 0; i < lut_len; ++i) o[i] = keep ? acgt[(lo >> (2 * (lut_len - 1 - i))) & 3] : 'N';
+        for (unsigned i = 0; i < k - lut_len; ++i)
+            o[lut_len + i] = keep ? acgt[(p[i >> 2] >> (6 - 2 * (i & 3))) & 3] : 'N';
+        o[k] = '$';
+        if (both) {
+            uint8_t *q = o + k + 1;
+            for (unsigned i = 0; i < k; ++i) {
+                const uint8_t c = o[k - 1 - i];
+                q[i] = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : c == 'T' ? 'A' : 'N';
+            }
+            q[k] = '$';
+        }
+        if (starts) {
+            const uint64_t rr = read_base + r * (both ? 2 : 1);
+            starts[rr] = seq_base + r * stride;
+            counts[rr] = cnt;
+            if (both) {
+                starts[rr + 1] = seq_base + r * stride + k + 1;
+                counts[rr + 1] = cnt;
+            }
+        }
+    }
+}
+
+}  // namespace mtg
