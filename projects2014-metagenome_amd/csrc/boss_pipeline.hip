@@ -50,7 +50,7 @@ class Workspace {
         MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
-        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, NSLOTS
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -234,6 +234,58 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
 __global__ void set_pair_kernel(uint64_t *p, uint64_t a, uint64_t b) {
     p[0] = a;
     p[1] = b;
+}
+
+// Duplication estimate for the MSD plan: m evenly spaced sample keys go into a hash table of
+// 64-bit fingerprints; the number of samples that find their fingerprint already present is
+// C ~ m^2 / (2 n) * E_w[mult] (E_w: multiplicity seen by a random occurrence).  Reads arrive in
+// random genome order, so evenly spaced samples are as good as random ones.
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    return x ^ (x >> 33);
+}
+
+template <int L>
+__global__ void dup_sample_kernel(const Key<L> *__restrict__ keys, uint64_t n, uint32_t m,
+                                  unsigned long long *__restrict__ table, uint32_t mask,
+                                  unsigned long long *__restrict__ hits) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const Key<L> k = keys[(uint64_t)((double)j * ((double)n / m))];
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+#pragma unroll
+    for (int i = 0; i < L; ++i) h = mix64(h ^ k.w[i]);
+    h |= 1;  // 0 marks an empty slot
+    uint32_t slot = (uint32_t)(h >> 32) & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&table[slot], 0ull, (unsigned long long)h);
+        if (prev == 0) return;
+        if (prev == h) {
+            atomicAdd(hits, 1ull);
+            return;
+        }
+        slot = (slot + 1) & mask;
+    }
+}
+
+// expected copies per distinct key of keys[0..n), conservative (it may err low, which costs a
+// planned bit, never an overflowing plan); `fallback` below the sampling size
+template <int L>
+static double estimate_dup(Ctx &c, const Key<L> *keys, uint64_t n, double fallback) {
+    constexpr uint32_t M = 1u << 20, SLOTS = 1u << 22;
+    if (n < 8ull * M) return fallback;
+    unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 1) * 8ull);
+    HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 1) * 8ull, c.stream));
+    dup_sample_kernel<L><<<dim3(M / 256), dim3(256), 0, c.stream>>>(keys, n, M, table, SLOTS - 1, table + SLOTS);
+    HIP_CHECK(hipGetLastError());
+    const double hits = (double)read_u64(c, table + SLOTS);
+    const double ew = 2.0 * (double)n * hits / ((double)M * M);  // E_w[multiplicity]
+    const double dup = std::max(1.0, ew / 1.2);  // E_w / mean: 1.17 at 10x, 1.29 at 1.25x
+    if (c.debug) fprintf(stderr, "[mtg debug] dup estimate n=%lu hits=%.0f E_w=%.2f -> %.2f\n", (unsigned long)n, hits, ew, dup);
+    return dup;
 }
 
 // Sort + unique (+ saturating count merge) of keys[0..n) over their low nbits by MSD
@@ -653,6 +705,7 @@ static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, K
         std::swap(*ca, *cb);
     } else {
         c.track_partition = track;
+        if (dup <= 0) dup = estimate_dup<L2>(c, *ka, N, 8.0);
         U = msd_sort_unique<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, cmax, dup, nullptr);
         c.track_partition = false;
     }
@@ -868,7 +921,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
-    const uint64_t U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 8.0, true);
+    const uint64_t U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 0.0, true);
     const int ev_sort = tm.mark();
     T.n_unique = U;
     debug_check_sorted(c, "collected k-mers", ka, U);
@@ -1144,7 +1197,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
-    const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 8.0, true);
+    const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 0.0, true);
     const int ev_sort = tm.mark();
     tr("local collect", Ul);
 
@@ -1171,7 +1224,9 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         // the P runs are sorted and disjoint within a run; duplicates across runs collapse and
         // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover 1/P of
         // the prefix space, hence the denser plan.
-        T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, 1.0 / d.P, nullptr,
+        // the keys cover ~1/P of the prefix space: P times denser buckets than their count says
+        const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / d.P;
+        T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
                                                   false, &runs);
     }
     const uint64_t U = T.n_unique;
