@@ -39,6 +39,76 @@ __device__ __forceinline__ Key<L> plain_to_boss(const Key<L> &P, unsigned K, con
 }
 
 /*
+ * One thread's PPT consecutive windows starting at p0 (tile-relative code offset r0 in s_code):
+ * slides the forward and reverse-complement plain words, skips windows with an invalid char
+ * (drag_and_mark_segments, common/algorithms.hpp:50-67), canonicalises (fwd <= rc in BOSS
+ * integer order, kmer_extractor.cpp:165-196) and clamps per-read counts (kmer_collector.cpp:92).
+ * Returns the valid mask; with KEYS = false only the mask (the counting passes).
+ */
+template <int L, bool COUNTED, int PPT, bool KEYS>
+__device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_t r0, uint64_t p0, uint64_t npos,
+                                                  unsigned K, int canonical,
+                                                  const uint64_t *__restrict__ read_starts,
+                                                  const uint32_t *__restrict__ read_counts, uint64_t n_reads,
+                                                  uint32_t cmax, Key<L> (&kk)[PPT], uint32_t (&cc)[PPT]) {
+    uint32_t valid_mask = 0;
+    if (p0 >= npos) return 0;
+    const Key<L> low = Key<L>::lowmask(2 * (K - 1));
+    const Key<L> full = Key<L>::lowmask(2 * K);
+    Key<L> P = Key<L>::zero(), R = Key<L>::zero();
+    int64_t last_bad = -1;
+    for (unsigned i = 0; i < K; ++i) {
+        uint32_t c = s_code[r0 + i];
+        if (c == 4) { last_bad = i; c = 0; }
+        P = P | shl(Key<L>::from(c), 2 * i);
+        R = R | shl(Key<L>::from(3 - c), 2 * (K - 1 - i));
+    }
+    uint64_t rid = 0;
+    if (KEYS && COUNTED && read_counts) {
+        uint64_t lo = 0, hi = n_reads;  // last read with start <= p0
+        while (hi - lo > 1) {
+            uint64_t mid = (lo + hi) / 2;
+            if (read_starts[mid] <= p0) lo = mid; else hi = mid;
+        }
+        rid = lo;
+    }
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const uint64_t p = p0 + j;
+        if (p < npos) {
+            if (last_bad < (int64_t)j) {
+                if (KEYS) {
+                    Key<L> f = plain_to_boss(P, K, low);
+                    if (canonical) {
+                        Key<L> r = plain_to_boss(R, K, low);
+                        if (r < f) f = r;
+                    }
+                    kk[j] = f;
+                    if (COUNTED) {
+                        uint32_t c = 1;
+                        if (read_counts) {
+                            while (rid + 1 < n_reads && read_starts[rid + 1] <= p) ++rid;
+                            c = read_counts[rid];
+                        }
+                        cc[j] = c < cmax ? c : cmax;
+                    }
+                }
+                valid_mask |= 1u << j;
+            }
+            if (j + 1 < PPT && p + 1 < npos) {
+                uint32_t c = s_code[r0 + j + K];
+                if (c == 4) { last_bad = j + K; c = 0; }
+                if (KEYS) {
+                    P = shr(P, 2) | shl(Key<L>::from(c), 2 * (K - 1));
+                    R = (shl(R, 2) & full) | Key<L>::from(3 - c);
+                }
+            }
+        }
+    }
+    return valid_mask;
+}
+
+/*
  * K1: extract_pack_canon.  Replaces KmerExtractorT<2>::sequence_to_kmers
  * (kmer/kmer_extractor.cpp:472-507; slides :86-108 / :165-196; skip rule from
  * utils::drag_and_mark_segments, common/algorithms.hpp:50-67) and the per-read count clamp of
@@ -80,65 +150,12 @@ __global__ __launch_bounds__(256) void extract_kernel(
     for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
     __syncthreads();
 
-    const Key<L> low = Key<L>::lowmask(2 * (K - 1));
-    const Key<L> full = Key<L>::lowmask(2 * K);
     const uint64_t p0 = base + (uint64_t)tid * PPT;
     Key<L> kk[PPT];
     uint32_t cc[PPT];
-    uint32_t nvalid = 0;
-    uint32_t valid_mask = 0;
-    if (p0 < npos) {
-        const uint32_t r0 = tid * PPT;
-        Key<L> P = Key<L>::zero(), R = Key<L>::zero();
-        int64_t last_bad = -1;
-        for (unsigned i = 0; i < K; ++i) {
-            uint32_t c = s_code[r0 + i];
-            if (c == 4) { last_bad = i; c = 0; }
-            P = P | shl(Key<L>::from(c), 2 * i);
-            R = R | shl(Key<L>::from(3 - c), 2 * (K - 1 - i));
-        }
-        uint64_t rid = 0;
-        if (COUNTED && read_counts) {
-            uint64_t lo = 0, hi = n_reads;  // last read with start <= p0
-            while (hi - lo > 1) {
-                uint64_t mid = (lo + hi) / 2;
-                if (read_starts[mid] <= p0) lo = mid; else hi = mid;
-            }
-            rid = lo;
-        }
-#pragma unroll
-        for (int j = 0; j < PPT; ++j) {
-            const uint64_t p = p0 + j;
-            if (p < npos) {
-                if (last_bad < (int64_t)j && COUNT_ONLY) {
-                    ++nvalid;
-                } else if (last_bad < (int64_t)j) {
-                    Key<L> f = plain_to_boss(P, K, low);
-                    if (canonical) {
-                        Key<L> r = plain_to_boss(R, K, low);
-                        if (r < f) f = r;
-                    }
-                    kk[j] = f;
-                    if (COUNTED) {
-                        uint32_t c = 1;
-                        if (read_counts) {
-                            while (rid + 1 < n_reads && read_starts[rid + 1] <= p) ++rid;
-                            c = read_counts[rid];
-                        }
-                        cc[j] = c < cmax ? c : cmax;
-                    }
-                    valid_mask |= 1u << j;
-                    ++nvalid;
-                }
-                if (j + 1 < PPT && p + 1 < npos) {
-                    uint32_t c = s_code[r0 + j + K];
-                    if (c == 4) { last_bad = j + K; c = 0; }
-                    P = shr(P, 2) | shl(Key<L>::from(c), 2 * (K - 1));
-                    R = (shl(R, 2) & full) | Key<L>::from(3 - c);
-                }
-            }
-        }
-    }
+    const uint32_t valid_mask = slide_windows<L, COUNTED, PPT, !COUNT_ONLY>(
+        s_code, tid * PPT, p0, npos, K, canonical, read_starts, read_counts, n_reads, cmax, kk, cc);
+    const uint32_t nvalid = __popc(valid_mask);
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nvalid, s_scan, &tile_total);
     if constexpr (COUNT_ONLY) {

@@ -23,6 +23,7 @@
 #include "boss_kernels.hpp"
 #include "comm.hpp"
 #include "dist_kernels.hpp"
+#include "extract_partition.hpp"
 #include "kmc.hpp"
 #include "msd_sort.hpp"
 #include "radix_sort.hpp"
@@ -50,7 +51,7 @@ class Workspace {
         MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
-        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, NSLOTS
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -137,6 +138,9 @@ struct Ctx {
                                    // their $-padded keys crowd a few top-digit buckets)
     bool debug = false;            // MTG_DEBUG=1: host-side checks between stages
     bool trace = false;            // MTG_TRACE=1: per-step wall times and sizes of the dist build
+    bool fused = true;             // MTG_FUSED=0: K1 writes in window order, K2 partitions after
+    uint64_t fused_min = 1ull << 22;  // MTG_FUSED_MIN: fewest window starts for the fused K1
+    double fused_ms = 0;           // device time of the last fused extract+partition launch
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -318,7 +322,9 @@ template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
                                 double dup, const uint32_t *hist1 = nullptr, bool distinct = false,
-                                const std::vector<uint64_t> *runs = nullptr) {
+                                const std::vector<uint64_t> *runs = nullptr, bool level1_done = false) {
+    // level1_done: the producer already scattered the keys by the plan's level-1 digit
+    // (extract_partition_kernel); hist1 holds that level's counts
     // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them;
     // distinct: the input has no duplicates (the local pass skips its hash table);
     // runs: the input is runs->size() - 1 sorted runs at these offsets (one gather replaces
@@ -362,6 +368,10 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(cnt, nbuckets, bstart, desc, ep,
                                                                       &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
+        if (lev == 1 && level1_done) {
+            b = bb;
+            return;
+        }
         auto *cur = (unsigned long long *)c.ws.get(Workspace::MSD_CURSOR, nbuckets * 8);
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
         EventTimer tm(c.stream);
@@ -382,7 +392,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         }
         HIP_CHECK(hipGetLastError());
         tm.mark();
-        if (c.track_partition && lev == 1) {
+        if (c.track_partition && c.radix_launches == 0) {  // first partition launch of the sort
             HIP_CHECK(hipStreamSynchronize(c.stream));
             c.radix_ms += tm.ms(0, 1);
             c.radix_launches += 1;
@@ -673,11 +683,100 @@ static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax,
     return N;
 }
 
+// K1 fused with K2's first partition level (extract_partition.hpp), for 2-bit u64 keys on
+// inputs big enough to have one.  Returns false (nothing done) when it does not apply; else N,
+// the duplication estimate, and the level-1 counts in *hist1 (device) with *ka scattered.
+template <int L2, bool COUNTED>
+static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                                Key<L2> **ka, Key<L2> **kb, uint32_t **ca, uint32_t **cb, uint64_t *N_out,
+                                double *dup_out, const uint32_t **hist1_out) {
+    if constexpr (L2 != 1) {
+        return false;
+    } else {
+        const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+        if (!c.fused || c.use_lsd || npos < c.fused_min || npos < 4096) return false;
+        // the duplication estimate from a sample of windows
+        constexpr uint32_t M = 1u << 20, SLOTS = 1u << 22;
+        unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
+        HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
+        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                            M, table, SLOTS - 1, table + SLOTS);
+        HIP_CHECK(hipGetLastError());
+        // pass A: histogram of the top bits of every valid k-mer
+        constexpr int TILE = ExtractTraits<1>::TILE;
+        const uint64_t tiles = ceil_div(npos, TILE);
+        const uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, 2048);
+        const unsigned hb = std::min(FUSED_HB, 2 * K);
+        const uint32_t nbh = 1u << hb;
+        uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
+        uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, nbh * 4);
+        HIP_CHECK(hipMemsetAsync(h12, 0, nbh * 4, c.stream));
+        extract_hist_kernel<1><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                     tiles, rows);
+        HIP_CHECK(hipGetLastError());
+        hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
+                                  c.stream>>>(rows, nrows, nbh, h12);
+        HIP_CHECK(hipGetLastError());
+        std::vector<uint32_t> h(nbh);
+        unsigned long long st[2];
+        HIP_CHECK(hipMemcpyAsync(h.data(), h12, nbh * 4, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(st, table + SLOTS, 16, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        uint64_t N = 0;
+        for (uint32_t v : h) N += v;
+        const double mv = (double)std::max<unsigned long long>(st[1], 1);
+        const double ew = 2.0 * (double)N * (double)st[0] / (mv * mv);
+        const double dup = N >= 8ull * M ? std::max(1.0, ew / 1.2) : 8.0;
+        const MsdPlan plan = msd_plan<1>(c, N, 2 * K, dup);
+        if (c.debug)
+            fprintf(stderr, "[mtg debug] fused extract N=%lu dup=%.2f levels=%u digit1=%u\n", (unsigned long)N, dup,
+                    plan.levels, plan.levels ? plan.digit_end[1] : 0);
+        if (!plan.levels) return false;  // nothing to partition: the plain extraction path
+        const unsigned b1 = plan.digit_end[1];
+        // level-1 counts (fold of the pass-A histogram) and bucket starts = the scatter cursors
+        std::vector<uint32_t> h1(1u << b1, 0);
+        for (uint32_t i = 0; i < nbh; ++i) h1[i >> (hb - b1)] += h[i];
+        std::vector<unsigned long long> cur(1u << b1);
+        unsigned long long acc = 0;
+        for (uint32_t i = 0; i < (1u << b1); ++i) {
+            cur[i] = acc;
+            acc += h1[i];
+        }
+        uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, h1.size() * 4);
+        unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
+        HIP_CHECK(hipMemcpyAsync(dh1, h1.data(), h1.size() * 4, hipMemcpyHostToDevice, c.stream));
+        HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
+        *ka = (Key<1> *)c.ws.get(Workspace::KA, std::max<uint64_t>(N, 1) * 8);
+        *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(N, 1) * 8);
+        *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
+        *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(N, 1) * 4) : nullptr;
+        // pass B
+        const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED>::TILE);
+        EventTimer tm(c.stream);
+        tm.mark();
+        extract_partition_kernel<COUNTED><<<dim3((unsigned)ftiles), dim3(FusedTraits<COUNTED>::BLOCK), 0, c.stream>>>(
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1, dcur, *ka,
+            COUNTED ? *ca : nullptr);
+        HIP_CHECK(hipGetLastError());
+        tm.mark();
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // `h1` / `cur` are host locals
+        c.fused_ms = tm.ms(0, 1);
+        c.timings.n_positions = npos;
+        c.timings.n_extracted = N;
+        *N_out = N;
+        *dup_out = dup;
+        *hist1_out = dh1;
+        return true;
+    }
+}
+
 // K2 + K3: sort + unique (saturating count merge) of *ka[0..N) -> *ka[0..U).  `dup` is the
 // expected number of copies per distinct key (plans the MSD depth only).
 template <int L2, bool COUNTED>
 static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, Key<L2> **kb,
-                              uint32_t **ca, uint32_t **cb, uint64_t N, double dup, bool track) {
+                              uint32_t **ca, uint32_t **cb, uint64_t N, double dup, bool track,
+                              const uint32_t *hist1 = nullptr) {
+    // hist1 != nullptr: *ka is already scattered by the level-1 digit (stage_extract_fused)
     uint64_t U = 0;
     if (c.use_lsd) {
         radix_sort<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, track);
@@ -706,7 +805,8 @@ static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, K
     } else {
         c.track_partition = track;
         if (dup <= 0) dup = estimate_dup<L2>(c, *ka, N, 8.0);
-        U = msd_sort_unique<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, cmax, dup, nullptr);
+        U = msd_sort_unique<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, cmax, dup, hist1, false, nullptr,
+                                         hist1 != nullptr);
         c.track_partition = false;
     }
     return U;
@@ -911,17 +1011,21 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     EventTimer tm(c.stream);
     const int ev_start = tm.mark();
 
-    // ---- K1 extract
+    // ---- K1 extract (fused with K2's first partition level when it applies)
     K2 *ka, *kb;
     uint32_t *ca, *cb;
-    const uint64_t N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
-    const int ev_extract = tm.mark();
-
-    // ---- K2 sort + K3 unique / saturating count merge (ka)
+    uint64_t N = 0;
+    double dup = 0;
+    const uint32_t *hist1 = nullptr;
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
-    const uint64_t U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 0.0, true);
+    if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+        N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
+    const int ev_extract = tm.mark();
+
+    // ---- K2 sort + K3 unique / saturating count merge (ka)
+    const uint64_t U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
     const int ev_sort = tm.mark();
     T.n_unique = U;
     debug_check_sorted(c, "collected k-mers", ka, U);
@@ -1191,13 +1295,17 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     K2 *ka, *kb;
     uint32_t *ca, *cb;
     Tracer tr{c, d.me};
-    const uint64_t N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
-    const int ev_extract = tm.mark();
-    tr("extract", N);
+    uint64_t N = 0;
+    double dup = 0;
+    const uint32_t *hist1 = nullptr;
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
-    const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, 0.0, true);
+    if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+        N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
+    const int ev_extract = tm.mark();
+    tr("extract", N);
+    const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
     const int ev_sort = tm.mark();
     tr("local collect", Ul);
 
@@ -1498,6 +1606,10 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         c->ctx.emit_slow = emitenv && std::string(emitenv) == "slow";
         c->ctx.debug = getenv("MTG_DEBUG") != nullptr;
         c->ctx.trace = getenv("MTG_TRACE") != nullptr;
+        const char *fenv = getenv("MTG_FUSED");
+        c->ctx.fused = !(fenv && atoi(fenv) == 0);
+        const char *fmenv = getenv("MTG_FUSED_MIN");
+        if (fmenv) c->ctx.fused_min = strtoull(fmenv, nullptr, 10);
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;

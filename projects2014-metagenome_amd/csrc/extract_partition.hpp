@@ -1,0 +1,183 @@
+// extract_partition.hpp -- K1 fused with the first MSD partition level of K2 (2-bit u64 keys).
+//
+// The unfused path writes every extracted k-mer in window order (K1) and then reads and scatters
+// it again by its top digit (K2 level 1): 2 x 9.6 GB of HBM traffic at the bench size.  Here the
+// extraction kernel itself scatters the k-mers into their level-1 buckets, so that pass and its
+// histogram pass disappear.  Bucket starts must be known before the scatter, hence two passes
+// over the read bytes (1.5 GB each at the bench size):
+//   A  extract_hist_kernel      -- extract, histogram of the top HB bits (HB = 12), no writes;
+//   B  extract_partition_kernel -- extract again, rank by bucket in LDS, reserve one run per
+//                                  (tile, bucket) with a cursor atomic, write the runs.
+// The window logic is slide_windows (boss_kernels.hpp), shared with extract_kernel, so both
+// produce the same k-mers (kmer_extractor.cpp:165-237, 472-507).
+#pragma once
+
+#include "boss_kernels.hpp"
+#include "msd_sort.hpp"
+
+namespace mtg {
+
+constexpr unsigned FUSED_HB = 12;  // histogram bits of pass A (>= any level-1 digit)
+
+// A: one LDS histogram per workgroup over its tiles (grid-stride), one row per workgroup
+template <int L>
+__global__ __launch_bounds__(256) void extract_hist_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
+                                                           unsigned K, int canonical, uint64_t ntiles,
+                                                           uint32_t *__restrict__ rows) {
+    using T = ExtractTraits<L>;
+    constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
+    constexpr uint32_t NB = 1u << FUSED_HB;
+    __shared__ uint8_t s_code[TILE + T::MAXK];
+    __shared__ uint32_t s_h[NB];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
+    const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
+    const unsigned hb = min(FUSED_HB, 2 * K);
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t base = tile * TILE;
+        const uint64_t span_end = min(seq_len, base + TILE + K - 1);
+        __syncthreads();
+        for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
+        __syncthreads();
+        Key<L> kk[PPT];
+        uint32_t cc[PPT];
+        const uint32_t m = slide_windows<L, false, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos,
+                                                              K, canonical, nullptr, nullptr, 0, 0, kk, cc);
+#pragma unroll
+        for (int j = 0; j < PPT; ++j)
+            if (m & (1u << j)) atomicAdd(&s_h[key_prefix(kk[j], 2 * K, hb)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < (1u << hb); i += BLOCK) rows[(uint64_t)blockIdx.x * (1u << hb) + i] = s_h[i];
+}
+
+template <bool COUNTED>
+struct FusedTraits {
+    static constexpr int BLOCK = COUNTED ? 512 : 1024;  // the LDS tile: 16 K keys, 8 K with counts
+    static constexpr int PPT = ExtractTraits<1>::PPT;
+    static constexpr int TILE = BLOCK * PPT;
+};
+
+// B: extract one tile, order its k-mers by the top b bits in LDS, write one run per bucket at
+// cursor[bucket] (the bucket starts of pass A's histogram)
+template <bool COUNTED>
+__global__ __launch_bounds__(FusedTraits<COUNTED>::BLOCK) void extract_partition_kernel(
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
+    const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
+    uint32_t cmax, unsigned b, unsigned long long *__restrict__ cursor, Key<1> *__restrict__ kout,
+    uint32_t *__restrict__ vout) {
+    using F = FusedTraits<COUNTED>;
+    constexpr int BLOCK = F::BLOCK, PPT = F::PPT, TILE = F::TILE;
+    constexpr int NBMAX = 512;
+    constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
+    __shared__ uint8_t s_code[TILE + ExtractTraits<1>::MAXK];
+    __shared__ Key<1> s_keys[TILE];
+    __shared__ uint32_t s_vals[COUNTED ? TILE : 1];
+    __shared__ uint32_t s_cnt[NBMAX];
+    __shared__ uint32_t s_loff[NBMAX];
+    __shared__ unsigned long long s_gbase[NBMAX];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nb = 1u << b;
+    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t span_end = min(seq_len, base + TILE + K - 1);
+    for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
+    __syncthreads();
+    Key<1> kk[PPT];
+    uint32_t cc[PPT];
+    const uint32_t m = slide_windows<1, COUNTED, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos, K,
+                                                            canonical, read_starts, read_counts, n_reads, cmax, kk, cc);
+    uint32_t r[PPT];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+        r[j] = (m & (1u << j)) ? atomicAdd(&s_cnt[key_prefix(kk[j], 2 * K, b)], 1u) : 0u;
+    __syncthreads();
+    uint32_t c[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        c[q] = i < nb ? s_cnt[i] : 0;
+        sum += c[q];
+    }
+    uint32_t total;
+    uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nb) {
+            s_loff[i] = off;
+            s_gbase[i] = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
+        }
+        off += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        if (m & (1u << j)) {
+            const uint32_t pos = s_loff[key_prefix(kk[j], 2 * K, b)] + r[j];
+            s_keys[pos] = kk[j];
+            if (COUNTED) s_vals[pos] = cc[j];
+        }
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < total; p += BLOCK) {
+        const Key<1> key = s_keys[p];
+        const uint32_t lb = key_prefix(key, 2 * K, b);
+        const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
+        kout[o] = key;
+        if (COUNTED) vout[o] = s_vals[p];
+    }
+}
+
+// duplication estimate straight from the read bytes (the keys do not exist yet): the k-mer at
+// m evenly spaced window starts, when valid, into the fingerprint table of estimate_dup
+template <int L>
+__global__ void dup_sample_reads_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K,
+                                        int canonical, uint32_t m, unsigned long long *__restrict__ table,
+                                        uint32_t mask, unsigned long long *__restrict__ stats) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint64_t npos = seq_len - K + 1;
+    const uint64_t p = (uint64_t)((double)j * ((double)npos / m));
+    Key<L> P = Key<L>::zero(), R = Key<L>::zero();
+    for (unsigned i = 0; i < K; ++i) {
+        const uint32_t c = encode_dna(seq[p + i]);
+        if (c == 4) return;
+        P = P | shl(Key<L>::from(c), 2 * i);
+        R = R | shl(Key<L>::from(3 - c), 2 * (K - 1 - i));
+    }
+    const Key<L> low = Key<L>::lowmask(2 * (K - 1));
+    Key<L> f = plain_to_boss(P, K, low);
+    if (canonical) {
+        const Key<L> r = plain_to_boss(R, K, low);
+        if (r < f) f = r;
+    }
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        h ^= f.w[i];
+        h ^= h >> 33;
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+        h *= 0xc4ceb9fe1a85ec53ull;
+        h ^= h >> 33;
+    }
+    h |= 1;
+    atomicAdd(&stats[1], 1ull);  // valid samples
+    uint32_t slot = (uint32_t)(h >> 32) & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&table[slot], 0ull, (unsigned long long)h);
+        if (prev == 0) return;
+        if (prev == h) {
+            atomicAdd(&stats[0], 1ull);  // repeats
+            return;
+        }
+        slot = (slot + 1) & mask;
+    }
+}
+
+}  // namespace mtg
