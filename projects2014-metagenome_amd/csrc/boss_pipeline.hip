@@ -694,9 +694,9 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         return false;
     } else {
         const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
-        if (!c.fused || c.use_lsd || npos < c.fused_min || npos < 4096) return false;
+        if (!c.fused || c.use_lsd || npos < c.fused_min || npos < 4096 || K - 1 < FUSED_HB / 2) return false;
         // the duplication estimate from a sample of windows
-        constexpr uint32_t M = 1u << 20, SLOTS = 1u << 22;
+        constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
         unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
         HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
         dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
@@ -706,13 +706,13 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         constexpr int TILE = ExtractTraits<1>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
         const uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, 2048);
-        const unsigned hb = std::min(FUSED_HB, 2 * K);
+        const unsigned hb = FUSED_HB;
         const uint32_t nbh = 1u << hb;
         uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
         uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, nbh * 4);
         HIP_CHECK(hipMemsetAsync(h12, 0, nbh * 4, c.stream));
-        extract_hist_kernel<1><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
-                                                                     tiles, rows);
+        extract_hist_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                  tiles, rows);
         HIP_CHECK(hipGetLastError());
         hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
                                   c.stream>>>(rows, nrows, nbh, h12);
@@ -726,7 +726,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         for (uint32_t v : h) N += v;
         const double mv = (double)std::max<unsigned long long>(st[1], 1);
         const double ew = 2.0 * (double)N * (double)st[0] / (mv * mv);
-        const double dup = N >= 8ull * M ? std::max(1.0, ew / 1.2) : 8.0;
+        const double dup = N >= 16ull * M ? std::max(1.0, ew / 1.2) : 8.0;
         const MsdPlan plan = msd_plan<1>(c, N, 2 * K, dup);
         if (c.debug)
             fprintf(stderr, "[mtg debug] fused extract N=%lu dup=%.2f levels=%u digit1=%u\n", (unsigned long)N, dup,

@@ -19,36 +19,54 @@ namespace mtg {
 
 constexpr unsigned FUSED_HB = 12;  // histogram bits of pass A (>= any level-1 digit)
 
-// A: one LDS histogram per workgroup over its tiles (grid-stride), one row per workgroup
-template <int L>
+// A: one LDS histogram per workgroup over its tiles (grid-stride), one row per workgroup.
+// The top HB bits of a 2-bit BOSS key are its node's last HB/2 chars a_{K-1} .. a_{K-HB/2}
+// (kmer_boss.hpp:58-72), and top(min(fwd, rc)) = min(top(fwd), top(rc)) (the tops decide the
+// comparison unless they are equal), so a window needs only those chars of each strand: rc's
+// top chars are comp(a_2) .. comp(a_{HB/2+1}).  Needs K - 1 >= HB/2 (callers check).
 __global__ __launch_bounds__(256) void extract_hist_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
                                                            unsigned K, int canonical, uint64_t ntiles,
                                                            uint32_t *__restrict__ rows) {
-    using T = ExtractTraits<L>;
+    using T = ExtractTraits<1>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
     constexpr uint32_t NB = 1u << FUSED_HB;
+    constexpr unsigned C = FUSED_HB / 2;  // chars per top
     __shared__ uint8_t s_code[TILE + T::MAXK];
     __shared__ uint32_t s_h[NB];
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    const unsigned hb = min(FUSED_HB, 2 * K);
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t base = tile * TILE;
         const uint64_t span_end = min(seq_len, base + TILE + K - 1);
         __syncthreads();
         for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
         __syncthreads();
-        Key<L> kk[PPT];
-        uint32_t cc[PPT];
-        const uint32_t m = slide_windows<L, false, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos,
-                                                              K, canonical, nullptr, nullptr, 0, 0, kk, cc);
+        const uint64_t p0 = base + (uint64_t)tid * PPT;
+        if (p0 >= npos) continue;
+        const uint32_t r0 = tid * PPT;
+        int64_t last_bad = -1;  // window-relative index of the last invalid char seen
+        for (unsigned i = 0; i < K; ++i)
+            if (s_code[r0 + i] == 4) last_bad = i;
 #pragma unroll
-        for (int j = 0; j < PPT; ++j)
-            if (m & (1u << j)) atomicAdd(&s_h[key_prefix(kk[j], 2 * K, hb)], 1u);
+        for (int j = 0; j < PPT; ++j) {
+            if (p0 + j >= npos) break;
+            if (j) {
+                if (s_code[r0 + j + K - 1] == 4) last_bad = j + K - 1;
+            }
+            if (last_bad >= (int64_t)j) continue;
+            const uint8_t *w = s_code + r0 + j;  // a_i = w[i - 1]
+            uint32_t f = 0, r = 0;
+#pragma unroll
+            for (unsigned q = 0; q < C; ++q) {
+                f = (f << 2) | w[K - 2 - q];
+                r = (r << 2) | (3u - w[1 + q]);
+            }
+            atomicAdd(&s_h[canonical && r < f ? r : f], 1u);
+        }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < (1u << hb); i += BLOCK) rows[(uint64_t)blockIdx.x * (1u << hb) + i] = s_h[i];
+    for (uint32_t i = tid; i < NB; i += BLOCK) rows[(uint64_t)blockIdx.x * NB + i] = s_h[i];
 }
 
 template <bool COUNTED>
