@@ -132,6 +132,15 @@ def test_large_multi_tile():
     reads = _random_reads(77, 30000, 150, 400000, n_rate=0.0005)
     for canonical in (False, True):
         check(30, reads, canonical, bits=8)
+        check(30, reads, canonical, bits=0)
+
+
+def test_fused_extract_small_inputs(monkeypatch):
+    # K1 fused with the first partition level on inputs it would skip by size, u64 k >= 7
+    monkeypatch.setenv("MTG_FUSED_MIN", "0")
+    reads = _random_reads(41, 2000, 150, 30000, n_rate=0.002, lower=True)
+    for k in range(6, 32):
+        check(k, reads, canonical=k % 2 == 1, bits=8 if k % 3 else 0)
 
 
 def test_device_build_matches_host_build():
@@ -158,7 +167,8 @@ def test_device_build_matches_host_build():
 
 
 @pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_DUMMY_SORT": "msd"},
-                                 {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_FUSED": "0"}])
+                                 {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_FUSED": "0"},
+                                 {"MTG_MERGE": "insert"}])
 def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
     # the compacting emit kernel, the MSD dummy sort and the LSD sorts stay bit-exact too
     for key, val in env.items():

@@ -83,6 +83,19 @@ def _oracle_kmc(k, path, canonical, bits, call_both=None, **kw):
                          counts=[c for _, c in recs])
 
 
+# test_build_weighted.py:155-273: --count-kmers (width 8) => nnz weights and avg weight
+@pytest.mark.parametrize("path,canonical,nodes,avg", [(SINGLE, False, 469983, "3.15029"),
+                                                      (BOTH, False, 802920, "3.68754"),
+                                                      (SINGLE, True, 802920, "3.68754"),
+                                                      (BOTH, True, 802920, "3.68754")])
+def test_oracle_kmc_weighted_goldens(path, canonical, nodes, avg):
+    c = _oracle_kmc(10, path, canonical, 8)
+    assert c.n_real == nodes
+    w = c.weights[1:].astype(np.float64)
+    nz = w[w > 0]
+    assert (len(nz), "{:.6g}".format(nz.mean())) == (nodes, avg)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("path,canonical,nodes", [(SINGLE, False, 469983), (BOTH, False, 802920),
                                                   (SINGLE, True, 802920), (BOTH, True, 802920)])
