@@ -203,8 +203,9 @@ def main():
     assert dc.F[4] <= dc.n - 1
 
     # roofline of the sort's partition pass (the radix-pass target is judged on
-    # K2): K2's first MSD partition launch reads and scatters every extracted k-mer once,
-    # 2 * N * 8 algorithmic bytes; its duration comes from HIP events on the build stream
+    # K2): the sort's first stand-alone MSD partition launch (level 2; level 1 is fused into K1)
+    # reads and scatters every extracted k-mer once, 2 * N * 8 algorithmic bytes; its duration
+    # comes from HIP events on the build stream
     pass_ms = sum(t["radix_pass_ms"] for t in timings) / len(timings)
     pass_bytes = last["radix_bytes"]
     achieved = pass_bytes / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
@@ -241,7 +242,8 @@ def main():
                                    % world) if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "msd_partition_kernel (K2 first MSD partition pass)",
+                     "kernel": "msd_partition_kernel (K2 level-2 MSD partition pass; level 1 runs "
+                               "inside the fused K1 extract_partition_kernel)",
                      "pass_ms": pass_ms, "bytes_per_launch": pass_bytes},
         "stages_ms": {k2: last[k2] for k2 in ("extract_ms", "sort_ms", "unique_ms", "rc_ms",
                                               "dummy_ms", "merge_ms", "emit_ms", "total_ms")},
