@@ -12,6 +12,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <omp.h>
 #include <string.h>
 
 static __thread char g_err[256];
@@ -49,31 +50,67 @@ __attribute__((constructor)) static void init_tables(void) {
 
 /*
  * Stable LSD radix sort over little-endian key bytes, with an optional u32 payload.
- * Passes whose byte is constant over all keys are skipped.
+ * Passes whose byte is constant over all keys are skipped.  Large inputs run each pass on all
+ * OpenMP threads: per-thread digit counts over contiguous chunks, offsets digit-major then
+ * thread-minor, scatter in chunk order -- the same stable order as the serial pass, so the
+ * result does not depend on the thread count (this is the CPU baseline's stand-in for
+ * ips4o::parallel::sort; any correct sort gives the same sets).
  */
 #define DEFINE_RADIX(ESZ)                                                                   \
     static void radix_sort_##ESZ(uint8_t *keys, uint32_t *cnt, size_t n) {                 \
         if (n < 2) return;                                                                 \
         uint8_t *tmp = (uint8_t *)xmalloc(n * ESZ);                                        \
         uint32_t *tcnt = cnt ? (uint32_t *)xmalloc(n * sizeof(uint32_t)) : NULL;           \
-        size_t hist[ESZ][256];                                                             \
-        memset(hist, 0, sizeof(hist));                                                     \
-        for (size_t i = 0; i < n; ++i)                                                     \
-            for (int b = 0; b < ESZ; ++b) hist[b][keys[i * ESZ + b]]++;                    \
+        int nt = 1;                                                                        \
+        if (n >= ((size_t)1 << 20)) nt = omp_get_max_threads();                            \
+        if (nt > 256) nt = 256;                                                            \
+        size_t(*th)[256] = (size_t(*)[256])xmalloc((size_t)nt * ESZ * 256 * sizeof(size_t)); \
+        memset(th, 0, (size_t)nt * ESZ * 256 * sizeof(size_t));                            \
+        _Pragma("omp parallel num_threads(nt)")                                            \
+        {                                                                                  \
+            const int t = omp_get_thread_num();                                            \
+            const size_t lo = n * t / nt, hi = n * (t + 1) / nt;                           \
+            for (size_t i = lo; i < hi; ++i)                                               \
+                for (int b = 0; b < ESZ; ++b) th[t * ESZ + b][keys[i * ESZ + b]]++;        \
+        }                                                                                  \
         uint8_t *src = keys, *dst = tmp;                                                   \
         uint32_t *csrc = cnt, *cdst = tcnt;                                                \
         for (int b = 0; b < ESZ; ++b) {                                                    \
             int trivial = 0;                                                               \
-            for (int d = 0; d < 256; ++d)                                                  \
-                if (hist[b][d] == n) trivial = 1;                                          \
-            if (trivial) continue;                                                         \
-            size_t off[256], s = 0;                                                        \
-            for (int d = 0; d < 256; ++d) { off[d] = s; s += hist[b][d]; }                 \
-            for (size_t i = 0; i < n; ++i) {                                               \
-                size_t o = off[src[i * ESZ + b]]++;                                        \
-                memcpy(dst + o * ESZ, src + i * ESZ, ESZ);                                 \
-                if (cnt) cdst[o] = csrc[i];                                                \
+            for (int d = 0; d < 256 && !trivial; ++d) {                                    \
+                size_t tot = 0;                                                            \
+                for (int t = 0; t < nt; ++t) tot += th[t * ESZ + b][d];                    \
+                if (tot == n) trivial = 1;                                                 \
             }                                                                              \
+            if (trivial) continue;                                                         \
+            /* this pass's per-thread digit counts over the CURRENT order */              \
+            size_t(*pc)[256] = (size_t(*)[256])xmalloc((size_t)nt * 256 * sizeof(size_t)); \
+            memset(pc, 0, (size_t)nt * 256 * sizeof(size_t));                              \
+            _Pragma("omp parallel num_threads(nt)")                                        \
+            {                                                                              \
+                const int t = omp_get_thread_num();                                        \
+                const size_t lo = n * t / nt, hi = n * (t + 1) / nt;                       \
+                for (size_t i = lo; i < hi; ++i) pc[t][src[i * ESZ + b]]++;                \
+            }                                                                              \
+            size_t s = 0;                                                                  \
+            for (int d = 0; d < 256; ++d)                                                  \
+                for (int t = 0; t < nt; ++t) {                                             \
+                    const size_t c = pc[t][d];                                             \
+                    pc[t][d] = s;                                                          \
+                    s += c;                                                                \
+                }                                                                          \
+            _Pragma("omp parallel num_threads(nt)")                                        \
+            {                                                                              \
+                const int t = omp_get_thread_num();                                        \
+                const size_t lo = n * t / nt, hi = n * (t + 1) / nt;                       \
+                size_t *off = pc[t];                                                       \
+                for (size_t i = lo; i < hi; ++i) {                                         \
+                    size_t o = off[src[i * ESZ + b]]++;                                    \
+                    memcpy(dst + o * ESZ, src + i * ESZ, ESZ);                             \
+                    if (cnt) cdst[o] = csrc[i];                                            \
+                }                                                                          \
+            }                                                                              \
+            free(pc);                                                                      \
             uint8_t *t = src; src = dst; dst = t;                                          \
             uint32_t *ct = csrc; csrc = cdst; cdst = ct;                                   \
         }                                                                                  \
@@ -81,6 +118,7 @@ __attribute__((constructor)) static void init_tables(void) {
             memcpy(keys, src, n * ESZ);                                                    \
             if (cnt) memcpy(cnt, csrc, n * sizeof(uint32_t));                              \
         }                                                                                  \
+        free(th);                                                                          \
         free(tmp);                                                                         \
         free(tcnt);                                                                        \
     }
