@@ -817,6 +817,169 @@ __global__ __launch_bounds__(256) void merge_insert_kernel(const Key<LA> *__rest
     }
 }
 
+/*
+ * K7 + K8 fused: the merge-path tile of merge(lift(A), B) is built in LDS exactly as merge_kernel
+ * does, and the rows are emitted from there (emit_fast_kernel's rules, initialize_chunk,
+ * boss_chunk.cpp:32-133) instead of writing the lifted stream and reading it back.  Stream row
+ * r = off + d for merge position d (off = 1 behind the main dummy row, which emit_root_kernel
+ * writes); output row r + 1.  The row after the tile is the merge's next element; the W "minus"
+ * look-back continues past the tile start by merging A and B backwards (groups hold <= 25 rows).
+ * A redundant dummy sink sets *skip and the caller redoes K7 + K8 unfused (compacting emit).
+ */
+template <int LO, int LA>
+__device__ __forceinline__ bool merged_at(const Key<LA> *__restrict__ a, uint64_t na, const Key<LO> *__restrict__ b,
+                                          uint64_t nb, uint64_t ia, uint64_t ib, unsigned K, Key<LO> *out) {
+    // smallest of A[ia..] (lifted) and B[ib..]; false past both ends
+    const bool ha = ia < na, hb = ib < nb;
+    if (!ha && !hb) return false;
+    if (ha) {
+        const Key<LO> x = lift_fast<LO>(a[ia], K);
+        *out = (!hb || x < b[ib]) ? x : b[ib];
+    } else {
+        *out = b[ib];
+    }
+    return true;
+}
+
+template <int LO, int LA, bool COUNTED>
+__global__ __launch_bounds__(256) void merge_emit_kernel(const Key<LA> *__restrict__ a,
+                                                         const uint32_t *__restrict__ ac, uint64_t na,
+                                                         const Key<LO> *__restrict__ b, uint64_t nb, unsigned K,
+                                                         const uint64_t *__restrict__ splits, uint64_t off,
+                                                         uint32_t wmax, uint8_t *__restrict__ W,
+                                                         uint8_t *__restrict__ last, uint32_t *__restrict__ weights,
+                                                         uint32_t *__restrict__ skip) {
+    constexpr int TILE = MergeTraits<LO>::TILE, ITEMS = TILE / 256;
+    __shared__ Key<LO> s_in[TILE];
+    __shared__ Key<LO> s_out[TILE + 1];  // + the row after the tile
+    __shared__ uint32_t s_cin[COUNTED ? TILE : 1];
+    __shared__ uint32_t s_cout[COUNTED ? TILE : 1];
+    __shared__ uint8_t s_w[TILE], s_l[TILE];
+    __shared__ uint64_t s_split[2];
+    __shared__ int s_hasnext;
+    const unsigned k = K - 1;
+    const uint64_t total = na + nb;
+    const uint64_t d0 = (uint64_t)blockIdx.x * TILE;
+    const uint64_t d1 = min(total, d0 + TILE);
+    if (threadIdx.x < 2) s_split[threadIdx.x] = splits[blockIdx.x + threadIdx.x];
+    __syncthreads();
+    const uint64_t a0 = s_split[0], a1 = s_split[1];
+    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
+    const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0), n = la + lb;
+    for (uint32_t i = threadIdx.x; i < la; i += 256) {
+        s_in[i] = lift_fast<LO>(a[a0 + i], K);
+        if (COUNTED) s_cin[i] = ac[a0 + i];
+    }
+    for (uint32_t i = threadIdx.x; i < lb; i += 256) {
+        s_in[la + i] = b[b0 + i];
+        if (COUNTED) s_cin[la + i] = 0;
+    }
+    if (threadIdx.x == 0) {
+        Key<LO> nx;
+        s_hasnext = merged_at<LO, LA>(a, na, b, nb, a1, b1, K, &nx) ? 1 : 0;
+        if (s_hasnext) s_out[n] = nx;
+    }
+    __syncthreads();
+    const uint32_t t0 = min((uint32_t)threadIdx.x * ITEMS, n);
+    const uint32_t t1 = min(t0 + ITEMS, n);
+    uint32_t lo = t0 > lb ? t0 - lb : 0, hi = min(t0, la);
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_in[mid] < s_in[la + t0 - mid - 1]) lo = mid + 1; else hi = mid;
+    }
+    uint32_t i = lo, j = t0 - lo;
+    for (uint32_t o = t0; o < t1; ++o) {
+        const bool take_a = i < la && (j >= lb || s_in[i] < s_in[la + j]);
+        const uint32_t src = take_a ? i : la + j;
+        s_out[o] = s_in[src];
+        if (COUNTED) s_cout[o] = s_cin[src];
+        if (take_a) ++i; else ++j;
+    }
+    __syncthreads();
+    bool skipped = false;
+    for (uint32_t t = threadIdx.x; t < n; t += 256) {
+        const Key<LO> key = s_out[t];
+        const uint32_t c = (uint32_t)(key.w[0] & 7);
+        const Key<LO> node = shr(key, 3);
+        const bool has_next = t + 1 < n || s_hasnext;
+        const bool same_next = has_next && shr(s_out[t + 1], 3) == node;
+        if (same_next && c == 0 && char_at(key, k, 3) > 0) skipped = true;
+        uint32_t ww = c;
+        if (c) {
+            const Key<LO> grp = shr(key, 6);
+            bool done = false;
+            for (int64_t p = (int64_t)t - 1; p >= 0; --p) {
+                const Key<LO> y = s_out[p];
+                if (shr(y, 6) != grp) { done = true; break; }
+                if ((uint32_t)(y.w[0] & 7) == c) { ww = c + 5; done = true; break; }
+            }
+            if (!done) {  // the group continues before the tile: merge A, B backwards
+                uint64_t ia = a0, ib = b0;
+                while (ia > 0 || ib > 0) {
+                    Key<LO> y;
+                    if (ia > 0 && ib > 0) {
+                        const Key<LO> x = lift_fast<LO>(a[ia - 1], K);
+                        if (b[ib - 1] < x) { y = x; --ia; } else { y = b[ib - 1]; --ib; }
+                    } else if (ia > 0) {
+                        y = lift_fast<LO>(a[--ia], K);
+                    } else {
+                        y = b[--ib];
+                    }
+                    if (shr(y, 6) != grp) break;
+                    if ((uint32_t)(y.w[0] & 7) == c) { ww = c + 5; break; }
+                }
+            }
+        }
+        s_w[t] = (uint8_t)ww;
+        s_l[t] = same_next ? 0 : 1;
+        if (COUNTED) {
+            const uint32_t cnt = s_cout[t];
+            weights[off + d0 + t + 1] = (cnt && ww && char_at(key, 1, 3)) ? (cnt < wmax ? cnt : wmax) : 0;
+        }
+    }
+    if (skipped) atomicOr(skip, 1u);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n; t += 256) {
+        W[off + d0 + t + 1] = s_w[t];
+        last[off + d0 + t + 1] = s_l[t];
+    }
+}
+
+// the main dummy row (stream row 0, all $) when the fused K7 + K8 runs: output row 1
+template <int LO, int LA, bool COUNTED>
+__global__ void emit_root_kernel(const Key<LA> *__restrict__ a, uint64_t na, const Key<LO> *__restrict__ b,
+                                 uint64_t nb, unsigned K, uint8_t *__restrict__ W, uint8_t *__restrict__ last,
+                                 uint32_t *__restrict__ weights) {
+    Key<LO> nx;
+    const bool has = merged_at<LO, LA>(a, na, b, nb, 0, 0, K, &nx);
+    W[1] = 0;  // label $
+    last[1] = has && shr(nx, 3) == Key<LO>::zero() ? 0 : 1;
+    if (COUNTED) weights[1] = 0;
+}
+
+// F[c] = #stream rows whose last node char < c: the root ($), lifted A (char + 1) and B, by
+// binary search on each sorted array (f_bounds_kernel without the materialised stream)
+template <int LO, int LA>
+__global__ void f_bounds_split_kernel(const Key<LA> *__restrict__ a, uint64_t na, const Key<LO> *__restrict__ b,
+                                      uint64_t nb, unsigned K, uint64_t root, unsigned long long *__restrict__ F) {
+    const uint32_t c = threadIdx.x;
+    if (c >= 5) return;
+    const unsigned k = K - 1;
+    uint64_t lo = 0, hi = na;  // A: 2-bit char k + 1 < c
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (char_at(a[mid], k, 2) + 1 < c) lo = mid + 1; else hi = mid;
+    }
+    uint64_t fa = lo;
+    lo = 0;
+    hi = nb;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (char_at(b[mid], k, 3) < c) lo = mid + 1; else hi = mid;
+    }
+    F[c] = fa + lo + (root && c > 0 ? 1 : 0);
+}
+
 __global__ void set_root_row_kernel(uint64_t *key_words, int limbs, uint32_t *count) {
     for (int i = 0; i < limbs; ++i) key_words[i] = 0;  // the main dummy KMER(0)
     if (count) *count = 0;

@@ -141,6 +141,7 @@ struct Ctx {
     bool fused = true;             // MTG_FUSED=0: K1 writes in window order, K2 partitions after
     uint64_t fused_min = 1ull << 22;  // MTG_FUSED_MIN: fewest window starts for the fused K1
     double fused_ms = 0;           // device time of the last fused extract+partition launch
+    bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it
     bool merge_insert = false;     // MTG_MERGE=insert: K7 by merge_insert_kernel when the dummies are
                                    // few (measured 5.2 ms vs 4.1 ms for merge path at the bench size)
 };
@@ -939,6 +940,46 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
     const unsigned K = k + 1;
     const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
     const uint64_t M = (root ? 1 : 0) + R + D;
+    if (c.fused_emit && !c.emit_slow && M) {
+        // K7 + K8 in one pass over A and B (merge_emit_kernel); a redundant sink falls through
+        uint8_t *W = (uint8_t *)c.ws.get(Workspace::OW, M + 1);
+        uint8_t *last = (uint8_t *)c.ws.get(Workspace::OLAST, M + 1);
+        uint32_t *weights = COUNTED ? (uint32_t *)c.ws.get(Workspace::OWEIGHTS, (M + 1) * 4) : nullptr;
+        HIP_CHECK(hipMemsetAsync(W, 0, 1, c.stream));
+        HIP_CHECK(hipMemsetAsync(last, 0, 1, c.stream));
+        if (COUNTED) HIP_CHECK(hipMemsetAsync(weights, 0, 4, c.stream));
+        reset_small(c);
+        if (root) {
+            emit_root_kernel<L3, L2, COUNTED><<<1, 1, 0, c.stream>>>(real, R, dk, D, K, W, last, weights);
+            HIP_CHECK(hipGetLastError());
+        }
+        const uint64_t ntiles = ceil_div(R + D, MergeTraits<L3>::TILE);
+        if (ntiles) {
+            uint64_t *splits = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
+            merge_partition_kernel<L3, L2, true><<<dim3((unsigned)ceil_div(ntiles + 1, 256)), dim3(256), 0, c.stream>>>(
+                real, R, dk, D, K, ntiles, splits);
+            HIP_CHECK(hipGetLastError());
+            merge_emit_kernel<L3, L2, COUNTED><<<dim3((unsigned)ntiles), dim3(256), 0, c.stream>>>(
+                real, realc, R, dk, D, K, splits, root ? 1 : 0, wmax, W, last, weights, &c.small->skip);
+            HIP_CHECK(hipGetLastError());
+        }
+        f_bounds_split_kernel<L3, L2><<<1, 64, 0, c.stream>>>(real, R, dk, D, K, root ? 1 : 0, c.small->fhist);
+        HIP_CHECK(hipGetLastError());
+        *ev_merge = tm.mark();
+        Small h;
+        HIP_CHECK(hipMemcpyAsync(&h, c.small, sizeof(Small), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (!h.skip) {
+            for (int ch = 0; ch < 5; ++ch) out->F[ch] = h.fhist[ch];
+            out->W = W;
+            out->last = last;
+            out->weights = weights;
+            out->n = M + 1;
+            out->n_real = R;
+            out->n_dummy = M - R;
+            return;
+        }
+    }
     K3 *sk = (K3 *)c.ws.get(Workspace::STREAM, M * sizeof(K3));
     uint32_t *sc = COUNTED ? (uint32_t *)c.ws.get(Workspace::SCOUNT, M * 4) : nullptr;
     if (root) {
@@ -1629,6 +1670,8 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         c->ctx.trace = getenv("MTG_TRACE") != nullptr;
         const char *fenv = getenv("MTG_FUSED");
         c->ctx.fused = !(fenv && atoi(fenv) == 0);
+        const char *feenv = getenv("MTG_FUSED_EMIT");
+        c->ctx.fused_emit = !(feenv && atoi(feenv) == 0);
         const char *menv = getenv("MTG_MERGE");
         c->ctx.merge_insert = menv && std::string(menv) == "insert";
         const char *fmenv = getenv("MTG_FUSED_MIN");
