@@ -144,9 +144,10 @@ def _check(rc):
 class Chunk:
     """BOSS::Chunk (boss_chunk.hpp:19-104): W (0..9), last (0/1), F[5], weights, k."""
 
-    def __init__(self, k, W, last, F, weights=None, n_real=None, n_dummy=None):
+    def __init__(self, k, W, last, F, weights=None, n_real=None, n_dummy=None, bits_per_count=0):
         self.k = k
         self.alph_size = 5
+        self.bits_per_count = bits_per_count
         self.W = W
         self.last = last
         self.F = F
@@ -156,6 +157,20 @@ class Chunk:
 
     def size(self):
         return len(self.W)
+
+    def serialize(self, outbase):
+        """BOSS::Chunk::serialize (boss_chunk.cpp:372-386): <outbase>.dbg.chunk{,.W,.last,.weights}."""
+        from . import chunk_io
+        return chunk_io.serialize(self, outbase)
+
+    @classmethod
+    def load(cls, infbase):
+        """BOSS::Chunk::load (boss_chunk.cpp:330-370); raises ValueError on a corrupted chunk."""
+        from . import chunk_io
+        k, alph, W, last, F, weights, bits = chunk_io.load(infbase)
+        if alph != 5:
+            raise ValueError("ERROR: only the DNA alphabet of size 5 is supported")
+        return cls(k, W, last, F, weights, bits_per_count=bits)
 
     def extend(self, other):
         """BOSS::Chunk::extend (boss_chunk.cpp:230-270): append rows after index 0, sum F."""
@@ -229,7 +244,7 @@ class BOSSChunkConstructor:
         last = np.ctypeslib.as_array(c.last, shape=(n,)).copy()
         weights = np.ctypeslib.as_array(c.weights, shape=(n,)).copy() if c.weights else None
         F = np.array(list(c.F), dtype=np.uint64)
-        out = Chunk(c.k, W, last, F, weights, c.n_real, c.n_dummy)
+        out = Chunk(c.k, W, last, F, weights, c.n_real, c.n_dummy, self._bits)
         lib().mtg_boss_chunk_free(ctypes.byref(c))
         return out
 
@@ -343,12 +358,27 @@ def concatenate(chunks):
     first = chunks[0]
     out = Chunk(first.k, first.W.copy(), first.last.copy(), first.F.copy(),
                 None if first.weights is None else first.weights.copy(), first.n_real,
-                first.n_dummy)
+                first.n_dummy, first.bits_per_count)
     for ch in chunks[1:]:
         out.extend(ch)
         out.n_real += ch.n_real
         out.n_dummy += ch.n_dummy
     return out
+
+
+def concatenate_files(chunk_filenames):
+    """BOSS::Chunk::build_boss_from_chunks (boss_chunk.cpp:286-327) up to initialize_boss: load
+    the `.dbg.chunk` files in order and extend the first with the rest."""
+    if not chunk_filenames:
+        raise ValueError("no graph chunks")
+    full = None
+    for name in chunk_filenames:
+        ch = Chunk.load(name)
+        if full is None:
+            full = ch
+        else:
+            full.extend(ch)
+    return full
 
 
 def device_count():

@@ -176,3 +176,17 @@ def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
     for k, canonical, bits in [(19, True, 8), (30, False, 0), (40, True, 16), (3, False, 8)]:
         check(k, transcripts_1000[:400], canonical, bits)
     check(5, CONSTRUCT_SEQS, True, 8)
+
+
+def test_chunk_files_roundtrip(tmp_path, transcripts_1000):
+    # the device-built chunk through <base>.dbg.chunk{,.W,.last,.weights} and back
+    # (BOSS::Chunk::serialize / load, boss_chunk.cpp:330-386)
+    for k, canonical, bits in [(19, True, 8), (30, False, 0)]:
+        got = gpu_chunk(k, transcripts_1000[:300], canonical, bits)
+        name = got.serialize(str(tmp_path / ("g%d" % k)))
+        back = boss.Chunk.load(name)
+        want = O.build_chunk(k, transcripts_1000[:300], canonical=canonical, bits_per_count=bits)
+        assert back.k == k and back.bits_per_count == bits
+        assert np.array_equal(back.W, want.W) and np.array_equal(back.last, want.last)
+        assert list(back.F) == list(want.F)
+        assert (back.weights is None) if not bits else np.array_equal(back.weights, want.weights)
