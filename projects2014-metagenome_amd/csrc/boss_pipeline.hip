@@ -140,6 +140,7 @@ struct Ctx {
     bool trace = false;            // MTG_TRACE=1: per-step wall times and sizes of the dist build
     bool fused = true;             // MTG_FUSED=0: K1 writes in window order, K2 partitions after
     uint64_t fused_min = 1ull << 22;  // MTG_FUSED_MIN: fewest window starts for the fused K1
+    int fused_block = 512;            // MTG_FUSED_BLOCK: threads per fused K1 tile (256, 512, 1024); 512 = 2 tiles per CU
     double fused_ms = 0;           // device time of the last fused extract+partition launch
     bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it
     bool merge_insert = false;     // MTG_MERGE=insert: K7 by merge_insert_kernel when the dummies are
@@ -754,12 +755,23 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
         *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(N, 1) * 4) : nullptr;
         // pass B
-        const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED>::TILE);
         EventTimer tm(c.stream);
         tm.mark();
-        extract_partition_kernel<COUNTED><<<dim3((unsigned)ftiles), dim3(FusedTraits<COUNTED>::BLOCK), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1, dcur, *ka,
-            COUNTED ? *ca : nullptr);
+        auto launch = [&](auto blk) {
+            constexpr int B = decltype(blk)::value;
+            const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, B>::TILE);
+            extract_partition_kernel<COUNTED, B><<<dim3((unsigned)ftiles), dim3(B), 0, c.stream>>>(
+                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1, dcur,
+                *ka, COUNTED ? *ca : nullptr);
+        };
+        if (c.fused_block == 256) {
+            launch(std::integral_constant<int, 256>());
+        } else if constexpr (COUNTED) {
+            launch(std::integral_constant<int, 512>());
+        } else {
+            if (c.fused_block == 512) launch(std::integral_constant<int, 512>());
+            else launch(std::integral_constant<int, 1024>());
+        }
         HIP_CHECK(hipGetLastError());
         tm.mark();
         HIP_CHECK(hipStreamSynchronize(c.stream));  // `h1` / `cur` are host locals
@@ -1676,6 +1688,7 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         c->ctx.merge_insert = menv && std::string(menv) == "insert";
         const char *fmenv = getenv("MTG_FUSED_MIN");
         if (fmenv) c->ctx.fused_min = strtoull(fmenv, nullptr, 10);
+        if (const char *fb = getenv("MTG_FUSED_BLOCK")) c->ctx.fused_block = atoi(fb);
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;

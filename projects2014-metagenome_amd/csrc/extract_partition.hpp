@@ -69,30 +69,29 @@ __global__ __launch_bounds__(256) void extract_hist_kernel(const uint8_t *__rest
     for (uint32_t i = tid; i < NB; i += BLOCK) rows[(uint64_t)blockIdx.x * NB + i] = s_h[i];
 }
 
-template <bool COUNTED>
+template <bool COUNTED, int BLOCK_ = COUNTED ? 512 : 1024>
 struct FusedTraits {
-    static constexpr int BLOCK = COUNTED ? 512 : 1024;  // the LDS tile: 16 K keys, 8 K with counts
+    static constexpr int BLOCK = BLOCK_;  // the LDS tile: BLOCK * PPT keys (16 K at 1024 threads)
     static constexpr int PPT = ExtractTraits<1>::PPT;
     static constexpr int TILE = BLOCK * PPT;
 };
 
 // B: extract one tile, order its k-mers by the top b bits in LDS, write one run per bucket at
 // cursor[bucket] (the bucket starts of pass A's histogram)
-template <bool COUNTED>
-__global__ __launch_bounds__(FusedTraits<COUNTED>::BLOCK) void extract_partition_kernel(
+template <bool COUNTED, int BLOCK_>
+__global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
     uint32_t cmax, unsigned b, unsigned long long *__restrict__ cursor, Key<1> *__restrict__ kout,
     uint32_t *__restrict__ vout) {
-    using F = FusedTraits<COUNTED>;
+    using F = FusedTraits<COUNTED, BLOCK_>;
     constexpr int BLOCK = F::BLOCK, PPT = F::PPT, TILE = F::TILE;
     constexpr int NBMAX = 512;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
     __shared__ uint8_t s_code[TILE + ExtractTraits<1>::MAXK];
     __shared__ Key<1> s_keys[TILE];
     __shared__ uint32_t s_vals[COUNTED ? TILE : 1];
-    __shared__ uint32_t s_cnt[NBMAX];
-    __shared__ uint32_t s_loff[NBMAX];
+    __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
     __shared__ unsigned long long s_gbase[NBMAX];
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
 
@@ -123,11 +122,12 @@ __global__ __launch_bounds__(FusedTraits<COUNTED>::BLOCK) void extract_partition
     }
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+    __syncthreads();  // every count is read before the offsets overwrite them
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
         if (i < nb) {
-            s_loff[i] = off;
+            s_cnt[i] = off;
             s_gbase[i] = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
         }
         off += c[q];
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(FusedTraits<COUNTED>::BLOCK) void extract_partition
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         if (m & (1u << j)) {
-            const uint32_t pos = s_loff[key_prefix(kk[j], 2 * K, b)] + r[j];
+            const uint32_t pos = s_cnt[key_prefix(kk[j], 2 * K, b)] + r[j];
             s_keys[pos] = kk[j];
             if (COUNTED) s_vals[pos] = cc[j];
         }
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(FusedTraits<COUNTED>::BLOCK) void extract_partition
     for (uint32_t p = tid; p < total; p += BLOCK) {
         const Key<1> key = s_keys[p];
         const uint32_t lb = key_prefix(key, 2 * K, b);
-        const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
+        const uint64_t o = s_gbase[lb] + (p - s_cnt[lb]);
         kout[o] = key;
         if (COUNTED) vout[o] = s_vals[p];
     }

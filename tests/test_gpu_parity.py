@@ -168,7 +168,9 @@ def test_device_build_matches_host_build():
 
 @pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_DUMMY_SORT": "msd"},
                                  {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_FUSED": "0"},
-                                 {"MTG_MERGE": "insert"}, {"MTG_FUSED_EMIT": "0"}])
+                                 {"MTG_MERGE": "insert"}, {"MTG_FUSED_EMIT": "0"},
+                                 {"MTG_FUSED_MIN": "0", "MTG_FUSED_BLOCK": "256"},
+                                 {"MTG_FUSED_MIN": "0", "MTG_FUSED_BLOCK": "1024"}])
 def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
     # the compacting emit kernel, the MSD dummy sort and the LSD sorts stay bit-exact too
     for key, val in env.items():
