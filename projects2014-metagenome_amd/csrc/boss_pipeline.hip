@@ -140,6 +140,7 @@ struct Ctx {
     bool trace = false;            // MTG_TRACE=1: per-step wall times and sizes of the dist build
     bool fused = true;             // MTG_FUSED=0: K1 writes in window order, K2 partitions after
     uint64_t fused_min = 1ull << 22;  // MTG_FUSED_MIN: fewest window starts for the fused K1
+    int part_wide_block = 1024;       // MTG_PART_WIDE_BLOCK: threads per tile of 9-bit partition passes
     int fused_block = 512;            // MTG_FUSED_BLOCK: threads per fused K1 tile (256, 512, 1024); 512 = 2 tiles per CU
     double fused_ms = 0;           // device time of the last fused extract+partition launch
     bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it
@@ -380,7 +381,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
         EventTimer tm(c.stream);
         tm.mark();
-        if (!COUNTED && bb - bp > 8) {  // wide digits: 1024-thread tiles keep the bucket runs long
+        if (!COUNTED && bb - bp > 8 && c.part_wide_block == 1024) {  // wide digits: 1024-thread tiles keep the bucket runs long
             if constexpr (!COUNTED) {
                 constexpr int TILE2 = MsdTraits<L>::ITEMS * 1024;
                 msd_partition_kernel<L, false, false, 1024><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
@@ -1689,6 +1690,7 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         const char *fmenv = getenv("MTG_FUSED_MIN");
         if (fmenv) c->ctx.fused_min = strtoull(fmenv, nullptr, 10);
         if (const char *fb = getenv("MTG_FUSED_BLOCK")) c->ctx.fused_block = atoi(fb);
+        if (const char *pw = getenv("MTG_PART_WIDE_BLOCK")) c->ctx.part_wide_block = atoi(pw);
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;
