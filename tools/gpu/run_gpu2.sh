@@ -9,4 +9,4 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py > gpurun_out/$TAG/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/$TAG/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash run_prof.sh $TAG/prof
+bash tools/gpu/run_prof.sh $TAG/prof

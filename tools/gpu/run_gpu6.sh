@@ -5,4 +5,4 @@ TAG=${1:-x}; mkdir -p gpurun_out/$TAG
 timeout -k 10 300 ./tools/msd_test > gpurun_out/$TAG/msd_test.log 2>&1
 rc=$?; echo "msd_test rc=$rc"; tail -3 gpurun_out/$TAG/msd_test.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash run_gpu5.sh $TAG
+bash tools/gpu/run_gpu5.sh $TAG

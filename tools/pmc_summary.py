@@ -1,4 +1,4 @@
-"""Summarise a run_pmc.sh output directory into profiles/: per-kernel HBM bytes per launch.
+"""Summarise a tools/gpu/prof_round.sh output directory into profiles/: per-kernel HBM bytes per launch.
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  The 8-byte-lane copy of a known byte count calibrates the
 counters at the partition pass's access width (MI355X_MICROARCH.md: FETCH_SIZE reports half of
@@ -49,6 +49,6 @@ part = [r for r in rows if r["kernel"].startswith("mtg::msd_partition_kernel<1, 
 json.dump({"kernel": part["kernel"], "hbm_bytes_per_launch": part["read_bytes"] + part["write_bytes"],
            "read_bytes": part["read_bytes"], "write_bytes": part["write_bytes"],
            "fetch_scale": fetch_scale, "write_scale": write_scale,
-           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (run_pmc.sh), calibrated by copy8_kernel"},
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (tools/gpu/prof_round.sh), calibrated by copy8_kernel"},
           open(prefix + "_partition_traffic.json", "w"), indent=1)
 print("\n".join(lines))
