@@ -13,14 +13,13 @@ namespace mtg {
 
 // kmer/alphabets.hpp:127-143 -- A/a 0, C/c 1, G/g 2, T/t/U/u 3, anything else invalid (4);
 // negative chars map like '\0' (kmer_extractor.cpp:31-34), i.e. invalid.
+// Branchless: OR-ing 0x20 folds upper onto lower case (its preimages are exactly {x, x ^ 0x20}),
+// then a 3-bit-per-entry table indexed by (c | 0x20) - 'a' for 'a' .. 'u' (21 entries); anything
+// outside that range is invalid.  Exhaustively equal to the switch over all 256 byte values.
 __device__ __forceinline__ uint32_t encode_dna(uint32_t c) {
-    switch (c) {
-        case 'A': case 'a': return 0;
-        case 'C': case 'c': return 1;
-        case 'G': case 'g': return 2;
-        case 'T': case 't': case 'U': case 'u': return 3;
-        default: return 4;
-    }
+    constexpr uint64_t TAB = 0x37249249248a4860ull;  // a 0, c 1, g 2, t 3, u 3, others 4
+    const uint32_t idx = (c | 0x20u) - 0x61u;
+    return idx > 20u ? 4u : (uint32_t)(TAB >> (3u * idx)) & 7u;
 }
 
 template <int L>
