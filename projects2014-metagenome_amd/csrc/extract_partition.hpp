@@ -19,6 +19,26 @@ namespace mtg {
 
 constexpr unsigned FUSED_HB = 12;  // histogram bits of pass A (>= any level-1 digit)
 
+// Stage a tile's read bytes as 2-bit codes (4 = invalid) in LDS: one dword load, four encodes and
+// one dword LDS store per thread step when the bytes are 4-aligned, byte loads for the tail.
+template <int BLOCK>
+__device__ __forceinline__ void stage_codes(const uint8_t *__restrict__ seq, uint64_t base, uint64_t span_end,
+                                            uint8_t *s_code, uint32_t tid) {
+    const uint32_t n = span_end > base ? (uint32_t)(span_end - base) : 0u;
+    uint32_t done = 0;
+    if ((((uintptr_t)(seq + base)) & 3) == 0) {
+        const uint32_t nw = n >> 2;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(seq + base);
+        for (uint32_t i = tid; i < nw; i += BLOCK) {
+            const uint32_t v = src[i];
+            reinterpret_cast<uint32_t *>(s_code)[i] = encode_dna(v & 0xff) | encode_dna((v >> 8) & 0xff) << 8 |
+                                                      encode_dna((v >> 16) & 0xff) << 16 | encode_dna(v >> 24) << 24;
+        }
+        done = nw << 2;
+    }
+    for (uint32_t i = done + tid; i < n; i += BLOCK) s_code[i] = encode_dna(seq[base + i]);
+}
+
 // A: one LDS histogram per workgroup over its tiles (grid-stride), one row per workgroup.
 // The top HB bits of a 2-bit BOSS key are its node's last HB/2 chars a_{K-1} .. a_{K-HB/2}
 // (kmer_boss.hpp:58-72), and top(min(fwd, rc)) = min(top(fwd), top(rc)) (the tops decide the
@@ -31,18 +51,18 @@ __global__ __launch_bounds__(256) void extract_hist_kernel(const uint8_t *__rest
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
     constexpr uint32_t NB = 1u << FUSED_HB;
     constexpr unsigned C = FUSED_HB / 2;  // chars per top
-    __shared__ uint8_t s_code[TILE + T::MAXK];
+    __shared__ __align__(16) uint8_t s_code[TILE + T::MAXK];
     __shared__ uint32_t s_h[NB];
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    // (a register prefetch of the next tile's bytes, one 16-byte load per thread, measured slower:
-    // 9.4 -> 12.1 ms for the extract stage)
+    // (a register prefetch of the next tile's bytes, one 16-byte load per thread, measured slower
+    // with the switch-based encode: 9.4 -> 12.1 ms for the extract stage)
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t base = tile * TILE;
         const uint64_t span_end = min(seq_len, base + TILE + K - 1);
         __syncthreads();
-        for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
+        stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
         __syncthreads();
         const uint64_t p0 = base + (uint64_t)tid * PPT;
         if (p0 >= npos) continue;
@@ -99,7 +119,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     constexpr int BLOCK = F::BLOCK, PPT = F::PPT, TILE = F::TILE;
     constexpr int NBMAX = 512;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
-    __shared__ uint8_t s_code[TILE + ExtractTraits<1>::MAXK];
+    __shared__ __align__(16) uint8_t s_code[TILE + ExtractTraits<1>::MAXK];
     __shared__ Key<1> s_keys[TILE];
     __shared__ uint32_t s_vals[COUNTED ? TILE : 1];
     __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
@@ -112,7 +132,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
-    for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
+    stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
     __syncthreads();
     Key<1> kk[PPT];
     uint32_t cc[PPT];
