@@ -56,13 +56,38 @@ __global__ __launch_bounds__(256) void extract_hist_kernel(const uint8_t *__rest
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    // (a register prefetch of the next tile's bytes, one 16-byte load per thread, measured slower
-    // with the switch-based encode: 9.4 -> 12.1 ms for the extract stage)
+    // The grid strides over tiles, so the next tile's bytes are prefetched into registers (one
+    // 16-byte load per thread).  With the old switch-based encode this was slower (16 divergent
+    // switches per thread); with the table encode it saves 0.15 ms.
+    static_assert(TILE == 16 * BLOCK, "one 16-byte load per thread covers a tile");
+    const bool vec = ((uintptr_t)seq & 15) == 0;
+    uint4 pre = make_uint4(0, 0, 0, 0);
+    auto fetch = [&](uint64_t t) {  // prefetch the next tile's bytes while this one is histogrammed
+        const uint64_t b = t * TILE;
+        if (t < ntiles && vec && b + TILE + T::MAXK <= seq_len) {
+            pre = reinterpret_cast<const uint4 *>(seq + b)[tid];
+            return true;
+        }
+        return false;
+    };
+    bool have = fetch(blockIdx.x);
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t base = tile * TILE;
         const uint64_t span_end = min(seq_len, base + TILE + K - 1);
         __syncthreads();
-        stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
+        if (have) {
+            const uint32_t in[4] = {pre.x, pre.y, pre.z, pre.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                o[q] = encode_dna(in[q] & 0xff) | encode_dna((in[q] >> 8) & 0xff) << 8 |
+                       encode_dna((in[q] >> 16) & 0xff) << 16 | encode_dna(in[q] >> 24) << 24;
+            reinterpret_cast<uint4 *>(s_code)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
+            stage_codes<BLOCK>(seq, base + TILE, span_end, s_code + TILE, tid);
+        } else {
+            stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
+        }
+        have = fetch(tile + gridDim.x);
         __syncthreads();
         const uint64_t p0 = base + (uint64_t)tid * PPT;
         if (p0 >= npos) continue;
