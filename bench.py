@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--coverage", type=float, default=10.0)
     ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-steps", type=int, default=3,
+                    help="steps of the host-buffer leg (0 = skip)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -85,8 +87,8 @@ def make_reads_device(torch, n_reads, read_len, seed, data, coverage, device, wo
     return out
 
 
-def make_reads_host(n_reads, read_len, seed, data, coverage):
-    """The same generator family on the host (numpy), for the CPU baseline sample."""
+def make_reads_host_codes(n_reads, read_len, seed, data, coverage):
+    """The same generator family on the host (numpy): ASCII reads as an (n_reads, read_len) array."""
     import numpy as np
     rng = np.random.default_rng(seed)
     lut = np.frombuffer(b"ACGT", dtype=np.uint8)
@@ -102,7 +104,11 @@ def make_reads_host(n_reads, read_len, seed, data, coverage):
         codes = np.where(sub, alt, codes).astype(np.uint8)
     else:
         codes = rng.integers(0, 4, size=(n_reads, read_len), dtype=np.uint8)
-    asc = lut[codes]
+    return lut[codes]
+
+
+def make_reads_host(n_reads, read_len, seed, data, coverage):
+    asc = make_reads_host_codes(n_reads, read_len, seed, data, coverage)
     return [asc[i].tobytes() for i in range(n_reads)]
 
 
@@ -114,22 +120,91 @@ def cpu_threads():
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(args, kb):
+def cpu_baseline(args, kb, boss):
     """Oracle (C restatement: OpenMP extraction + parallel LSD radix sort, serial dummy and
-    emission passes) on a bounded sample of the same workload."""
+    emission passes) on a bounded sample of the same workload.  The same sample is then built on
+    the GPU through the host C ABI and compared with the oracle's chunk bit for bit (W, last, F,
+    weights): the `parity` field of the bench line."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
     import oracle_ctypes
-    reads = make_reads_host(args.cpu_sample_reads, args.read_len, 12345, args.data,
-                            args.coverage)
+    asc = make_reads_host_codes(args.cpu_sample_reads, args.read_len, 12345, args.data,
+                                args.coverage)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    canonical = args.mode == "canonical"
     t0 = time.perf_counter()
-    c = oracle_ctypes.build_chunk(kb, reads, canonical=args.mode == "canonical",
-                                  bits_per_count=args.count_width)
+    c = oracle_ctypes.build_chunk(kb, reads, canonical=canonical, bits_per_count=args.count_width)
     dt = time.perf_counter() - t0
     n = args.cpu_sample_reads * (args.read_len - args.k + 1)
-    return {"value": n / dt, "unit": "k-mers/s", "cores": cpu_threads(), "kind": "port",
+    base = {"value": n / dt, "unit": "k-mers/s", "cores": cpu_threads(), "kind": "port",
             "sample": "%d synthetic %d bp reads (%s, %gx coverage), k=%d %s, %.1f s, %d rows"
                       % (args.cpu_sample_reads, args.read_len, args.data, args.coverage,
                          args.k, args.mode, dt, len(c.W))}
+    ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=canonical,
+                                                 bits_per_count=args.count_width,
+                                                 num_threads=cpu_threads())
+    ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * args.read_len)
+    g = ctor.build_chunk()
+    same = (len(g.W) == len(c.W) and np.array_equal(g.W, c.W) and np.array_equal(g.last, c.last)
+            and np.array_equal(g.F, c.F) and
+            (c.weights is None if g.weights is None else np.array_equal(g.weights, c.weights)))
+    parity = {"ok": bool(same), "rows": int(len(c.W)),
+              "what": "GPU build (host C ABI) of the cpu_baseline sample vs the oracle: W, last, F, "
+                      "weights bit for bit"}
+    return base, parity
+
+
+def host_path(args, kb, boss, seq, steps):
+    """extract-start -> Chunk arrays on the HOST.  The bench's reads
+    (copied to host memory once, outside the timing) go through the reference's interface:
+    add_packed (staging into pinned memory, num_threads host threads), then build_chunk (one H2D
+    of the reads, the device path, D2H of W / packed last / weights into pinned blocks)."""
+    import numpy as np
+    L = args.read_len
+    host = seq.view(-1, L + 1)[:, :L].contiguous().cpu().numpy()
+    n_reads = host.shape[0]
+    offsets = np.arange(n_reads + 1, dtype=np.uint64) * L
+    flat = host.reshape(-1)
+    ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=args.mode == "canonical",
+                                                 bits_per_count=args.count_width,
+                                                 num_threads=cpu_threads())
+    rows = []
+    for it in range(steps + 1):  # the first build sizes the pinned buffers (untimed)
+        t0 = time.perf_counter()
+        ctor.add_packed(flat, offsets)
+        ch = ctor.build_chunk()
+        dt = time.perf_counter() - t0
+        t = ctor.timings()
+        if it:
+            rows.append((dt, t.stage_ms, t.h2d_ms, t.total_ms, t.d2h_ms, t.host_total_ms))
+        del ch
+    m = [sum(r[i] for r in rows) / len(rows) for i in range(6)]
+    kmers = n_reads * (L - args.k + 1)
+    return {"value": kmers / m[0], "unit": "k-mers/s", "ms_per_step": m[0] * 1e3,
+            "stages_ms": {"stage_into_pinned": m[1], "h2d_reads": m[2], "device_path": m[3],
+                          "d2h_W_last_weights": m[4], "build_chunk_call": m[5]},
+            "steps": steps, "staging_threads": cpu_threads(),
+            "what": "add_packed + build_chunk through the C ABI on the same reads, host arrays out"}
+
+
+def measured_copy_peak(torch, device, nbytes=4 << 30, reps=5):
+    """Achievable HBM bandwidth on this GPU: a device-to-device copy of `nbytes` (read + write),
+    timed with HIP events; the second roofline denominator BASELINE.md asks for."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    dst = torch.empty_like(src)
+    src.fill_(1)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del src, dst
+    torch.cuda.empty_cache()
+    return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
 def share_comm_id(rank, make_id):
@@ -210,6 +285,8 @@ def main():
     # size-independent sanity of the result
     assert dc.n == last["n_rows"] and dc.n == 1 + dc.n_real + dc.n_dummy
     assert dc.F[4] <= dc.n - 1
+    # the rate counts offered windows; every one of them must have been extracted (no N here)
+    assert last["n_extracted"] == kmers_per_rank, (last["n_extracted"], kmers_per_rank)
 
     # roofline of the sort's partition pass (the radix-pass target is judged on
     # K2): the sort's first stand-alone MSD partition launch (level 2; level 1 is fused into K1)
@@ -218,13 +295,19 @@ def main():
     pass_ms = sum(t["radix_pass_ms"] for t in timings) / len(timings)
     pass_bytes = last["radix_bytes"]
     achieved = pass_bytes / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "r1_partition_traffic.json")
-    if os.path.exists(prof):
-        try:
-            traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    # traffic: PMC HBM bytes of that launch from the committed rocprofv3 --pmc summary (a stored
+    # profile of the same command, not measured in this process)
+    traffic, traffic_src = None, None
+    for tag in ("r2", "r1"):
+        prof = os.path.join(ROOT, "profiles", "%s_partition_traffic.json" % tag)
+        if os.path.exists(prof):
+            try:
+                traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
+                traffic_src = "profiles/%s_partition_traffic.json (rocprofv3 --pmc, stored)" % tag
+                break
+            except (OSError, ValueError):
+                traffic = None
+    copy_peak = measured_copy_peak(torch, device) if rank == 0 else None
 
     result = {
         "metric": "k-mers/s ingested into BOSS (k=31, 150 bp reads)",
@@ -251,6 +334,10 @@ def main():
                                    % world) if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "peak_measured": copy_peak,
+                     "frac_measured": achieved / copy_peak if copy_peak else None,
+                     "peak_measured_how": "device-to-device copy of 4 GiB (read + write), HIP events",
                      "kernel": "msd_partition_kernel (K2 level-2 MSD partition pass; level 1 runs "
                                "inside the fused K1 extract_partition_kernel)",
                      "pass_ms": pass_ms, "bytes_per_launch": pass_bytes},
@@ -260,8 +347,10 @@ def main():
                                            "n_rows", "radix_launches", "n_sent")},
         "exchange_ms": last["exchange_ms"],
     }
+    if rank == 0 and args.host_steps > 0 and world == 1:
+        result["host_path"] = host_path(args, kb, boss, seq, args.host_steps)
     if rank == 0 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, kb)
+        result["cpu_baseline"], result["parity"] = cpu_baseline(args, kb, boss)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

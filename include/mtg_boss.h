@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 2
+#define MTG_BOSS_ABI_VERSION 3
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -62,7 +62,8 @@ typedef struct mtg_boss_params {
     uint8_t bits_per_count;      /* 0 = no weights; else --count-width (<= 32) */
     const char *filter_suffix;   /* must be NULL or "" on this path */
     uint64_t num_threads;        /* host threads for input staging */
-    double memory_preallocated;  /* bytes; advisory (HBM is sized from the input) */
+    double memory_preallocated;  /* bytes of device memory the build may use (0 = all free HBM);
+                                    larger inputs are built in key-range batches */
     int container_type;          /* MTG_CONTAINER_VECTOR */
     const char *swap_dir;        /* unused on the in-memory path */
     uint64_t disk_cap_bytes;     /* unused on the in-memory path */
@@ -71,13 +72,15 @@ typedef struct mtg_boss_params {
 
 typedef struct mtg_boss_ctor mtg_boss_ctor;
 
-/* BOSS::Chunk in host memory (arrays of n entries including the leading row 0) */
+/* BOSS::Chunk in host memory (arrays of n entries including the leading row 0).  The arrays are
+   pinned host blocks owned by the chunk: release them with mtg_boss_chunk_free. */
 typedef struct mtg_boss_chunk {
     uint64_t k;
     uint64_t alph_size;          /* 5: $ACGT */
     uint64_t n;
     uint8_t *W;                  /* n labels 0..9 (int_vector width 4 in the reference) */
-    uint8_t *last;               /* n flags 0/1 */
+    uint64_t *last;              /* n bits, packed: row i is bit i % 64 of word i / 64 (the
+                                    sdsl::bit_vector layout of the reference's last_) */
     uint32_t *weights;           /* n weights or NULL (bits_per_count == 0) */
     uint64_t F[5];
     uint8_t bits_per_count;
@@ -118,6 +121,13 @@ typedef struct mtg_boss_timings {
     double exchange_ms;          /* multi-GPU: time inside the exchanges (RCCL) */
     uint64_t n_sent;             /* multi-GPU: elements sent to other ranks */
     uint64_t world;              /* ranks of the build (1 = single GPU) */
+    /* host-buffer builds (mtg_boss_ctor_build_chunk): wall times of the host-side stages */
+    double stage_ms;             /* add_* calls since the previous build (copy into pinned memory) */
+    double h2d_ms;               /* reads -> HBM */
+    double d2h_ms;               /* W, packed last, weights -> pinned host blocks */
+    double host_total_ms;        /* the whole build_chunk call */
+    uint64_t n_batches;          /* key-range batches of the build (1 = the input fit at once) */
+    uint64_t peak_bytes;         /* device workspace held at the end of the build */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);
@@ -187,6 +197,10 @@ int mtg_boss_build_device_dist(mtg_boss_ctor *ctor, mtg_comm *comm, const uint8_
                                mtg_boss_device_chunk *out);
 /* the range split: bounds[0..world] over n_prefixes buckets, balanced on hist (host) */
 int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64_t *bounds);
+
+/* encode table of the extractor (kmer/alphabets.hpp:127-143) evaluated by the device function on
+   the host: out[c] in {0, 1, 2, 3, 4 = invalid} for every byte c (256 entries) */
+void mtg_dna_encode_table(uint8_t *out);
 
 /* device-memory helpers for callers without their own HIP runtime (ctypes, cgo, JNI) */
 void *mtg_device_alloc(int device_id, uint64_t bytes);

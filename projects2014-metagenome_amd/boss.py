@@ -33,7 +33,7 @@ class _Params(ctypes.Structure):
 
 class _Chunk(ctypes.Structure):
     _fields_ = [("k", ctypes.c_uint64), ("alph_size", ctypes.c_uint64), ("n", ctypes.c_uint64),
-                ("W", ctypes.POINTER(ctypes.c_uint8)), ("last", ctypes.POINTER(ctypes.c_uint8)),
+                ("W", ctypes.POINTER(ctypes.c_uint8)), ("last", ctypes.POINTER(ctypes.c_uint64)),
                 ("weights", ctypes.POINTER(ctypes.c_uint32)), ("F", ctypes.c_uint64 * 5),
                 ("bits_per_count", ctypes.c_uint8), ("n_real", ctypes.c_uint64),
                 ("n_dummy", ctypes.c_uint64)]
@@ -54,7 +54,10 @@ class Timings(ctypes.Structure):
                 ("radix_launches", "n_positions", "n_extracted", "n_unique", "n_real",
                  "n_dummy", "n_rows")] + \
                [("exchange_ms", ctypes.c_double), ("n_sent", ctypes.c_uint64),
-                ("world", ctypes.c_uint64)]
+                ("world", ctypes.c_uint64)] + \
+               [(name, ctypes.c_double) for name in
+                ("stage_ms", "h2d_ms", "d2h_ms", "host_total_ms")] + \
+               [("n_batches", ctypes.c_uint64), ("peak_bytes", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -69,7 +72,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_device_count", "mtg_device_synchronize", "mtg_comm_get_unique_id",
            "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
-           "mtg_dist_bounds", "mtg_boss_ctor_add_kmc")
+           "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table")
 
 COMM_ID_BYTES = 128
 
@@ -130,6 +133,7 @@ def lib():
                                              ctypes.c_uint64, ctypes.c_int]
         L.mtg_dist_bounds.argtypes = [P(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_int,
                                       P(ctypes.c_uint64)]
+        L.mtg_dna_encode_table.argtypes = [ctypes.c_char_p]
         for name in EXPORTS:
             getattr(L, name)
         _lib = L
@@ -222,6 +226,20 @@ class BOSSChunkConstructor:
             cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None,
             len(bs)))
 
+    def add_packed(self, data, offsets, counts=None):
+        """n sequences back to back in one buffer (bytes or uint8 array), offsets[n + 1]."""
+        buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8)
+                                   if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(off) - 1
+        if n <= 0:
+            return
+        cnt = None if counts is None else np.ascontiguousarray(counts, dtype=np.uint64)
+        _check(lib().mtg_boss_ctor_add_packed(
+            self._h, buf.ctypes.data_as(ctypes.c_char_p),
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None, n))
+
     def add_kmc(self, kmc_path, min_count=1, max_count=2**32 - 1,
                 call_both_from_canonical=None):
         """KMC1 database input (cli/parse_sequences.hpp:50-101, seq_io/kmc_parser.cpp:27-62).
@@ -241,7 +259,7 @@ class BOSSChunkConstructor:
             _check(lib().mtg_boss_ctor_build_chunk_dist(self._h, comm.handle, ctypes.byref(c)))
         n = c.n
         W = np.ctypeslib.as_array(c.W, shape=(n,)).copy()
-        last = np.ctypeslib.as_array(c.last, shape=(n,)).copy()
+        last = unpack_last(np.ctypeslib.as_array(c.last, shape=((n + 63) // 64,)), n)
         weights = np.ctypeslib.as_array(c.weights, shape=(n,)).copy() if c.weights else None
         F = np.array(list(c.F), dtype=np.uint64)
         out = Chunk(c.k, W, last, F, weights, c.n_real, c.n_dummy, self._bits)
@@ -379,6 +397,26 @@ def concatenate_files(chunk_filenames):
         else:
             full.extend(ch)
     return full
+
+
+def unpack_last(words, n):
+    """Packed `last` (bit i of word i // 64, sdsl::bit_vector layout) -> n flags 0/1 (uint8)."""
+    bits = np.unpackbits(np.ascontiguousarray(words, dtype="<u8").view(np.uint8), bitorder="little")
+    return bits[:n].copy()
+
+
+def pack_last(last):
+    """n flags 0/1 -> packed words (inverse of unpack_last)."""
+    b = np.packbits(np.asarray(last, dtype=np.uint8) & 1, bitorder="little")
+    b = np.concatenate([b, np.zeros((-len(b)) % 8, dtype=np.uint8)])
+    return b.view("<u8").copy()
+
+
+def dna_encode_table():
+    """The extractor's encode table as the library's device function computes it (256 bytes)."""
+    buf = ctypes.create_string_buffer(256)
+    lib().mtg_dna_encode_table(buf)
+    return np.frombuffer(buf.raw, dtype=np.uint8).copy()
 
 
 def device_count():

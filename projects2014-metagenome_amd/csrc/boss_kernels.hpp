@@ -16,7 +16,7 @@ namespace mtg {
 // Branchless: OR-ing 0x20 folds upper onto lower case (its preimages are exactly {x, x ^ 0x20}),
 // then a 3-bit-per-entry table indexed by (c | 0x20) - 'a' for 'a' .. 'u' (21 entries); anything
 // outside that range is invalid.  Exhaustively equal to the switch over all 256 byte values.
-__device__ __forceinline__ uint32_t encode_dna(uint32_t c) {
+__host__ __device__ __forceinline__ uint32_t encode_dna(uint32_t c) {
     constexpr uint64_t TAB = 0x37249249248a4860ull;  // a 0, c 1, g 2, t 3, u 3, others 4
     const uint32_t idx = (c | 0x20u) - 0x61u;
     return idx > 20u ? 4u : (uint32_t)(TAB >> (3u * idx)) & 7u;
@@ -753,66 +753,6 @@ __global__ __launch_bounds__(256) void merge_kernel(const Key<LA> *__restrict__ 
     for (uint32_t o = threadIdx.x; o < la + lb; o += 256) {
         out[off + d0 + o] = s_out[o];
         if (COUNTED) oc[off + d0 + o] = s_cout[o];
-    }
-}
-
-/*
- * K7 when B is sparse (the dummies are a few % of the stream): every A element goes straight from
- * global memory to out[d0 + (i - a0) + #B < a] (the tile's B run staged in LDS and
- * binary-searched), every B element to out[d0 + j + #A < b] (binary search over the tile's A run,
- * cache-resident).  No A staging and no per-thread merge: the pass streams A once.  Tiles and
- * their splits are the merge-path ones (merge_partition_kernel with TILE), keys are distinct.
- */
-template <int LO>
-struct InsertTraits {
-    static constexpr int TILE = LO <= 2 ? 2048 : 1024;  // B run in LDS: <= 32 KB
-};
-
-template <int LO, int LA, bool LIFT, bool COUNTED, bool BCOUNTS>
-__global__ __launch_bounds__(256) void merge_insert_kernel(const Key<LA> *__restrict__ a,
-                                                           const uint32_t *__restrict__ ac, uint64_t na,
-                                                           const Key<LO> *__restrict__ b,
-                                                           const uint32_t *__restrict__ bc, uint64_t nb,
-                                                           unsigned K, const uint64_t *__restrict__ splits,
-                                                           Key<LO> *__restrict__ out, uint32_t *__restrict__ oc,
-                                                           uint64_t off) {
-    constexpr int TILE = InsertTraits<LO>::TILE;
-    __shared__ Key<LO> s_b[TILE];
-    __shared__ uint32_t s_lo[TILE];
-    __shared__ uint64_t s_split[2];
-    const uint64_t total = na + nb;
-    const uint64_t d0 = (uint64_t)blockIdx.x * TILE;
-    const uint64_t d1 = min(total, d0 + TILE);
-    if (threadIdx.x < 2) s_split[threadIdx.x] = splits[blockIdx.x + threadIdx.x];
-    __syncthreads();
-    const uint64_t a0 = s_split[0], a1 = s_split[1];
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-    const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0);
-    for (uint32_t j = threadIdx.x; j < lb; j += 256) s_b[j] = b[b0 + j];
-    __syncthreads();
-    // A element i: lo_i = #B < a_i, output d0 + i + lo_i
-    for (uint32_t i = threadIdx.x; i < la; i += 256) {
-        const Key<LO> key = merge_key<LO, LA, LIFT>(a[a0 + i], K);
-        uint32_t lo = 0, hi = lb;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_b[mid] < key) lo = mid + 1; else hi = mid;
-        }
-        s_lo[i] = lo;
-        const uint64_t o = off + d0 + i + lo;
-        out[o] = key;
-        if (COUNTED) oc[o] = ac[a0 + i];
-    }
-    __syncthreads();
-    // B element j sits after the A elements with lo_i <= j: lo is nondecreasing, so A element i
-    // places B elements [lo_{i-1}, lo_i) right before itself, the tail follows the last A
-    for (uint32_t i = threadIdx.x; i <= la; i += 256) {
-        const uint32_t from = i ? s_lo[i - 1] : 0u, to = i < la ? s_lo[i] : lb;
-        for (uint32_t j = from; j < to; ++j) {
-            const uint64_t o = off + d0 + j + i;
-            out[o] = s_b[j];
-            if (COUNTED) oc[o] = BCOUNTS ? bc[b0 + j] : 0;
-        }
     }
 }
 

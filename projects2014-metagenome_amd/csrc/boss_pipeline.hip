@@ -24,6 +24,7 @@
 #include "comm.hpp"
 #include "dist_kernels.hpp"
 #include "extract_partition.hpp"
+#include "host_stage.hpp"
 #include "kmc.hpp"
 #include "msd_sort.hpp"
 #include "radix_sort.hpp"
@@ -51,7 +52,8 @@ class Workspace {
         MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
-        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, NSLOTS
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR,
+        LAST_BITS, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -75,6 +77,11 @@ class Workspace {
         return b.ptr;
     }
     void swap(Slot a, Slot b) { std::swap(bufs_[a], bufs_[b]); }
+    uint64_t held() const {
+        uint64_t t = 0;
+        for (const auto &b : bufs_) t += b.cap;
+        return t;
+    }
 
   private:
     struct Buf {
@@ -128,27 +135,39 @@ struct Ctx {
     double radix_ms = 0, radix_bytes = 0;
     uint64_t radix_launches = 0;
     bool track_partition = false;  // time the msd_partition launches of the real-k-mer sorts
-    bool use_lsd = false;          // MTG_SORT=lsd: LSD onesweep + unique instead of MSD
-    bool part_vec = false;         // MTG_PART_VEC=1: 16-byte partition I/O (measured slower)
-    unsigned max_digit = MSD_DBITS;  // MTG_DIGIT_BITS: widest partition digit
-    bool small_table = true;       // MTG_SMALL_TABLE=0: full-size LDS tables in local unique
-    double plan_div = 2.5;         // MTG_PLAN_DIV: planned distinct keys per bucket = LIMIT / div
-    bool emit_slow = false;        // MTG_EMIT=slow: always the compacting emit kernel
-    bool dummy_msd = false;        // MTG_DUMMY_SORT=msd: MSD for the dummy k-mers (default LSD:
-                                   // their $-padded keys crowd a few top-digit buckets)
+    bool use_lsd = false;          // MTG_SORT=lsd: LSD onesweep + unique instead of MSD (the fallback
+                                   // sort of overflowing groups, selectable for the parity tests)
+    bool emit_slow = false;        // MTG_EMIT=slow: always the compacting emit kernel (the redundant-sink path)
     bool debug = false;            // MTG_DEBUG=1: host-side checks between stages
     bool trace = false;            // MTG_TRACE=1: per-step wall times and sizes of the dist build
     bool fused = true;             // MTG_FUSED=0: K1 writes in window order, K2 partitions after
     uint64_t fused_min = 1ull << 22;  // MTG_FUSED_MIN: fewest window starts for the fused K1
-    int part_wide_block = 1024;       // MTG_PART_WIDE_BLOCK: threads per tile of 9-bit partition passes
-    int fused_block = 512;            // MTG_FUSED_BLOCK: threads per fused K1 tile (256, 512, 1024); 512 = 2 tiles per CU
+    uint32_t hist_rows = 2048;     // MTG_HIST_ROWS: workgroups of the fused K1 histogram pass (tests
+                                   // lower it so the grid-stride + prefetch loop runs on small inputs)
     double fused_ms = 0;           // device time of the last fused extract+partition launch
-    bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it
-    bool merge_insert = false;     // MTG_MERGE=insert: K7 by merge_insert_kernel when the dummies are
-                                   // few (measured 5.2 ms vs 4.1 ms for merge path at the bench size)
+    bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it (the
+                                   // redundant-sink path)
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// The few environment switches, read once per constructor.  All but MTG_DEBUG / MTG_TRACE select
+// alternate device paths that exist for correctness (fallbacks the parity tests force on small
+// inputs), never a faster configuration.
+static void load_knobs(Ctx &c) {
+    auto is = [](const char *name, const char *val) {
+        const char *e = getenv(name);
+        return e && std::string(e) == val;
+    };
+    c.use_lsd = is("MTG_SORT", "lsd");
+    c.emit_slow = is("MTG_EMIT", "slow");
+    c.fused = !is("MTG_FUSED", "0");
+    c.fused_emit = !is("MTG_FUSED_EMIT", "0");
+    c.debug = getenv("MTG_DEBUG") != nullptr;
+    c.trace = getenv("MTG_TRACE") != nullptr;
+    if (const char *e = getenv("MTG_FUSED_MIN")) c.fused_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("MTG_HIST_ROWS")) c.hist_rows = (uint32_t)std::max(1L, std::min(2048L, atol(e)));
+}
 
 // zero the per-stage words; the error word is sticky for the whole build (checked at the end)
 static void reset_small(Ctx &c) {
@@ -166,7 +185,9 @@ static void check_error_word(Ctx &c) {
     uint32_t e = 0;
     HIP_CHECK(hipMemcpyAsync(&e, &c.small->error, sizeof(e), hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
-    if (e) throw std::runtime_error("device look-back timed out (error word " + std::to_string(e) + ")");
+    if (e & 1u) throw std::runtime_error("device look-back timed out (error word " + std::to_string(e) + ")");
+    if (e) throw std::runtime_error("device partition counts disagree with the histogram pass (error word " +
+                                    std::to_string(e) + ")");
 }
 
 // Descriptor array for one look-back launch plus its epoch.  Granules of older epochs read as
@@ -310,12 +331,14 @@ struct MsdPlan {
 // partition depth: enough top bits T that an average final bucket holds <= LIMIT/3 distinct
 // keys (canonical k-mers are up to 2x denser at small prefixes), in levels of <= max_digit
 // bits (one full read + scatter each)
+constexpr double kPlanDiv = 2.5;  // planned distinct keys per final bucket = LIMIT / kPlanDiv
+
 template <int L>
 static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
-    const double LIMIT = (double)LocalTraits<L>::LIMIT / (c.small_table ? 2 : 1);
-    const unsigned dmax = c.max_digit;
+    const double LIMIT = (double)LocalTraits<L>::LIMIT / 2;  // half-size LDS tables
+    const unsigned dmax = MSD_DBITS;
     unsigned T = 0;
-    while (T < nbits && T < 3 * dmax && (double)n / dup / (double)(1ull << T) > LIMIT / c.plan_div)
+    while (T < nbits && T < 3 * dmax && (double)n / dup / (double)(1ull << T) > LIMIT / kPlanDiv)
         ++T;
     MsdPlan p{};
     p.levels = (T + dmax - 1) / dmax;
@@ -381,18 +404,15 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
         EventTimer tm(c.stream);
         tm.mark();
-        if (!COUNTED && bb - bp > 8 && c.part_wide_block == 1024) {  // wide digits: 1024-thread tiles keep the bucket runs long
+        if (!COUNTED && bb - bp > 8) {  // wide digits: 1024-thread tiles keep the bucket runs long
             if constexpr (!COUNTED) {
                 constexpr int TILE2 = MsdTraits<L>::ITEMS * 1024;
-                msd_partition_kernel<L, false, false, 1024><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
-                                                              c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits,
-                                                                          bb, bp, cur);
+                msd_partition_kernel<L, false, 1024><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
+                                                       c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits, bb, bp,
+                                                                   cur);
             }
-        } else if (c.part_vec) {
-            msd_partition_kernel<L, COUNTED, true><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
-                *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
         } else {
-            msd_partition_kernel<L, COUNTED, false><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
+            msd_partition_kernel<L, COUNTED><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
                 *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
         }
         HIP_CHECK(hipGetLastError());
@@ -441,7 +461,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
 
     while (true) {
         // groups of consecutive buckets holding <= G keys; bigger buckets stand alone
-        const uint64_t G = (c.small_table ? LIMIT / 2 : LIMIT) / 2;
+        const uint64_t G = LIMIT / 4;
         uint64_t ngroups = 1;
         uint64_t *gstart;
         if (b == 0) {
@@ -484,16 +504,11 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             };
             using T_ = std::true_type;
             using F_ = std::false_type;
-            using SFull = std::integral_constant<int, LocalTraits<L>::SLOTS>;
             using SHalf = std::integral_constant<int, LocalTraits<L>::SLOTS / 2>;
             const bool keycas = L == 1 && nbits < 64;
-            if (distinct) {
-                if (c.small_table) go(F_{}, SHalf{}, T_{}); else go(F_{}, SFull{}, T_{});
-            } else if (c.small_table) {
-                if (keycas) go(T_{}, SHalf{}, F_{}); else go(F_{}, SHalf{}, F_{});
-            } else {
-                if (keycas) go(T_{}, SFull{}, F_{}); else go(F_{}, SFull{}, F_{});
-            }
+            if (distinct) go(F_{}, SHalf{}, T_{});
+            else if (keycas) go(T_{}, SHalf{}, F_{});
+            else go(F_{}, SHalf{}, F_{});
             HIP_CHECK(hipGetLastError());
             uint32_t nov = 0;
             HIP_CHECK(hipMemcpyAsync(&nov, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
@@ -710,7 +725,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         // pass A: histogram of the top bits of every valid k-mer
         constexpr int TILE = ExtractTraits<1>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
-        const uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, 2048);
+        const uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
         const unsigned hb = FUSED_HB;
         const uint32_t nbh = 1u << hb;
         uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
@@ -747,6 +762,10 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
             cur[i] = acc;
             acc += h1[i];
         }
+        // cursors, then the bucket ends pass B checks its reservations against
+        const uint32_t nb1 = 1u << b1;
+        cur.resize(2 * nb1);
+        for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
         uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, h1.size() * 4);
         unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
         HIP_CHECK(hipMemcpyAsync(dh1, h1.data(), h1.size() * 4, hipMemcpyHostToDevice, c.stream));
@@ -763,16 +782,12 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
             const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, B>::TILE);
             extract_partition_kernel<COUNTED, B><<<dim3((unsigned)ftiles), dim3(B), 0, c.stream>>>(
                 in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1, dcur,
-                *ka, COUNTED ? *ca : nullptr);
+                dcur + nb1, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
-        if (c.fused_block == 256) {
-            launch(std::integral_constant<int, 256>());
-        } else if constexpr (COUNTED) {
-            launch(std::integral_constant<int, 512>());
-        } else {
-            if (c.fused_block == 512) launch(std::integral_constant<int, 512>());
-            else launch(std::integral_constant<int, 1024>());
-        }
+        launch(std::integral_constant<int, 512>());
+        HIP_CHECK(hipGetLastError());
+        cursor_check_kernel<<<dim3((unsigned)ceil_div(nb1, 256)), dim3(256), 0, c.stream>>>(dcur, dcur + nb1, nb1,
+                                                                                           &c.small->error);
         HIP_CHECK(hipGetLastError());
         tm.mark();
         HIP_CHECK(hipStreamSynchronize(c.stream));  // `h1` / `cur` are host locals
@@ -879,7 +894,7 @@ static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db
                                     Key<L3> **dk) {
     uint64_t D = 0;
     uint32_t *nv = nullptr;
-    if (c.use_lsd || !c.dummy_msd) {
+    {
         radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
         reset_small(c);
         const uint64_t ut = ceil_div(Draw, 2048);
@@ -890,9 +905,6 @@ static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db
             &c.small->error);
         HIP_CHECK(hipGetLastError());
         D = read_u64(c, &c.small->total);
-    } else {
-        D = msd_sort_unique<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, 0, 2.0);
-        std::swap(da, db);
     }
     *dk = db;
     return D;
@@ -999,10 +1011,7 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
         set_root_row_kernel<<<1, 1, 0, c.stream>>>((uint64_t *)sk, L3, COUNTED ? sc : nullptr);
         HIP_CHECK(hipGetLastError());
     }
-    if (c.merge_insert && D * 8 < R)  // the dummies are a few % of the stream
-        merge_insert<L3, L2, true, COUNTED, false>(c, real, realc, R, dk, nullptr, D, K, sk, sc, root ? 1 : 0);
-    else
-        merge_sorted<L3, L2, true, COUNTED, false>(c, real, realc, R, dk, nullptr, D, K, sk, sc, root ? 1 : 0);
+    merge_sorted<L3, L2, true, COUNTED, false>(c, real, realc, R, dk, nullptr, D, K, sk, sc, root ? 1 : 0);
     debug_check_sorted(c, "merged stream", sk, M);
     *ev_merge = tm.mark();
 
@@ -1056,22 +1065,6 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
     out->n_dummy = rows - R;
 }
 
-// merge of a sorted array with a much shorter one (merge_insert_kernel)
-template <int LO, int LA, bool LIFT, bool COUNTED, bool BCOUNTS>
-static void merge_insert(Ctx &c, const Key<LA> *a, const uint32_t *ac, uint64_t na, const Key<LO> *b,
-                         const uint32_t *bc, uint64_t nb, unsigned K, Key<LO> *out, uint32_t *oc, uint64_t off) {
-    constexpr int TILE = InsertTraits<LO>::TILE;
-    const uint64_t ntiles = ceil_div(na + nb, TILE);
-    if (!ntiles) return;
-    uint64_t *splits = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
-    merge_partition_kernel<LO, LA, LIFT, TILE><<<dim3((unsigned)ceil_div(ntiles + 1, 256)), dim3(256), 0, c.stream>>>(
-        a, na, b, nb, K, ntiles, splits);
-    HIP_CHECK(hipGetLastError());
-    merge_insert_kernel<LO, LA, LIFT, COUNTED, BCOUNTS><<<dim3((unsigned)ntiles), dim3(256), 0, c.stream>>>(
-        a, ac, na, b, bc, nb, K, splits, out, oc, off);
-    HIP_CHECK(hipGetLastError());
-}
-
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
                          const BuildInput &in, BuildOutput *out) {
@@ -1082,6 +1075,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     mtg_boss_timings &T = c.timings;
     T = mtg_boss_timings{};
     T.world = 1;
+    T.n_batches = 1;
     HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
     EventTimer tm(c.stream);
     const int ev_start = tm.mark();
@@ -1150,6 +1144,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     T.radix_launches = c.radix_launches;
     T.radix_pass_ms = c.radix_launches ? c.radix_ms / c.radix_launches : 0;
     T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
+    T.peak_bytes = c.ws.held();
 }
 
 // ------------------------------------------------------------------------ multi-GPU pipeline
@@ -1586,6 +1581,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     T.radix_launches = c.radix_launches;
     T.radix_pass_ms = c.radix_launches ? c.radix_ms / c.radix_launches : 0;
     T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
+    T.peak_bytes = c.ws.held();
 }
 
 template <int L2, int L3>
@@ -1620,13 +1616,31 @@ struct mtg_boss_ctor {
     std::string suffix;
     int device = 0;
     mtg::Ctx ctx;
-    std::mutex mu;
-    std::vector<char> data;          // staged reads, each followed by a '$' separator
-    std::vector<uint64_t> starts;    // start offset of every read in `data`
-    std::vector<uint32_t> counts;    // per-read counts (clamped to u32)
-    bool any_count_not_one = false;
+    std::mutex mu;                   // one build at a time; adds run concurrently (HostStage)
+    mtg::HostStage stage;            // staged reads in pinned memory, each followed by '$'
+    std::mutex kmc_mu;
     std::vector<mtg::KmcInput> kmc;  // KMC databases, decoded on the device at build time
+    std::atomic<uint64_t> stage_ns{0};  // host time spent staging since the last build
 };
+
+// one packed `last` word per thread: bit j of word w = last[64 w + j] (sdsl bit_vector layout)
+__global__ void pack_bits_kernel(const uint8_t *__restrict__ bytes, uint64_t n, uint64_t *__restrict__ words) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i0 = w * 64;
+    if (i0 >= n) return;
+    uint64_t v = 0;
+    if (i0 + 64 <= n && ((uintptr_t)(bytes + i0) & 7) == 0) {
+        const uint64_t *p = reinterpret_cast<const uint64_t *>(bytes + i0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t x = p[q];  // 8 flag bytes (0/1) -> 8 bits
+            v |= ((x * 0x0102040810204080ull) >> 56 & 0xFFull) << (8 * q);
+        }
+    } else {
+        for (uint64_t j = 0; j < 64 && i0 + j < n; ++j) v |= (uint64_t)(bytes[i0 + j] & 1) << j;
+    }
+    words[w] = v;
+}
 
 using namespace mtg;
 
@@ -1665,32 +1679,7 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
-        const char *sortenv = getenv("MTG_SORT");
-        c->ctx.use_lsd = sortenv && std::string(sortenv) == "lsd";
-        const char *dsortenv = getenv("MTG_DUMMY_SORT");
-        c->ctx.dummy_msd = dsortenv && std::string(dsortenv) == "msd";
-        const char *pv = getenv("MTG_PART_VEC");
-        c->ctx.part_vec = pv && std::string(pv) == "1";
-        const char *db = getenv("MTG_DIGIT_BITS");
-        if (db) c->ctx.max_digit = std::max(1, std::min(MSD_DBITS, atoi(db)));
-        const char *stenv = getenv("MTG_SMALL_TABLE");
-        c->ctx.small_table = !(stenv && atoi(stenv) == 0);
-        const char *pdenv = getenv("MTG_PLAN_DIV");
-        if (pdenv) c->ctx.plan_div = std::max(1.0, atof(pdenv));
-        const char *emitenv = getenv("MTG_EMIT");
-        c->ctx.emit_slow = emitenv && std::string(emitenv) == "slow";
-        c->ctx.debug = getenv("MTG_DEBUG") != nullptr;
-        c->ctx.trace = getenv("MTG_TRACE") != nullptr;
-        const char *fenv = getenv("MTG_FUSED");
-        c->ctx.fused = !(fenv && atoi(fenv) == 0);
-        const char *feenv = getenv("MTG_FUSED_EMIT");
-        c->ctx.fused_emit = !(feenv && atoi(feenv) == 0);
-        const char *menv = getenv("MTG_MERGE");
-        c->ctx.merge_insert = menv && std::string(menv) == "insert";
-        const char *fmenv = getenv("MTG_FUSED_MIN");
-        if (fmenv) c->ctx.fused_min = strtoull(fmenv, nullptr, 10);
-        if (const char *fb = getenv("MTG_FUSED_BLOCK")) c->ctx.fused_block = atoi(fb);
-        if (const char *pw = getenv("MTG_PART_WIDE_BLOCK")) c->ctx.part_wide_block = atoi(pw);
+        load_knobs(c->ctx);
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;
@@ -1710,13 +1699,17 @@ void mtg_boss_ctor_destroy(mtg_boss_ctor *c) {
 
 uint64_t mtg_boss_ctor_get_k(const mtg_boss_ctor *c) { return c ? c->params.k : 0; }
 
-static void stage_one(mtg_boss_ctor *c, const char *s, uint64_t len, uint64_t count) {
-    c->starts.push_back(c->data.size());
-    c->data.insert(c->data.end(), s, s + len);
-    c->data.push_back('$');
-    uint32_t cnt = count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)count;
-    c->counts.push_back(cnt);
-    if (cnt != 1) c->any_count_not_one = true;
+struct StageTimer {
+    std::atomic<uint64_t> &acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~StageTimer() {
+        acc += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                   .count();
+    }
+};
+
+static unsigned stage_threads(const mtg_boss_ctor *c) {
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(c->params.num_threads, 64));
 }
 
 int mtg_boss_ctor_add_sequences(mtg_boss_ctor *c, const char *const *seqs, const uint64_t *lens,
@@ -1725,9 +1718,14 @@ int mtg_boss_ctor_add_sequences(mtg_boss_ctor *c, const char *const *seqs, const
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
     }
-    std::lock_guard<std::mutex> lock(c->mu);
-    for (size_t i = 0; i < n; ++i) stage_one(c, seqs[i], lens[i], counts ? counts[i] : 1);
-    return MTG_OK;
+    try {
+        StageTimer t{c->stage_ns};
+        c->stage.add(seqs, lens, counts, n, stage_threads(c));
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_ARGUMENT;
+    }
 }
 
 int mtg_boss_ctor_add_sequence(mtg_boss_ctor *c, const char *seq, uint64_t len, uint64_t count) {
@@ -1735,9 +1733,8 @@ int mtg_boss_ctor_add_sequence(mtg_boss_ctor *c, const char *seq, uint64_t len, 
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
     }
-    std::lock_guard<std::mutex> lock(c->mu);
-    stage_one(c, seq, len, count);
-    return MTG_OK;
+    const char *p = seq ? seq : "";
+    return mtg_boss_ctor_add_sequences(c, &p, &len, &count, 1);
 }
 
 int mtg_boss_ctor_add_packed(mtg_boss_ctor *c, const char *data, const uint64_t *offsets,
@@ -1746,10 +1743,17 @@ int mtg_boss_ctor_add_packed(mtg_boss_ctor *c, const char *data, const uint64_t 
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
     }
-    std::lock_guard<std::mutex> lock(c->mu);
-    for (size_t i = 0; i < n; ++i)
-        stage_one(c, data + offsets[i], offsets[i + 1] - offsets[i], counts ? counts[i] : 1);
-    return MTG_OK;
+    std::vector<const char *> ptrs(n);
+    std::vector<uint64_t> lens(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) {
+            set_error("offsets must be nondecreasing");
+            return MTG_ERR_ARGUMENT;
+        }
+        ptrs[i] = data + offsets[i];
+        lens[i] = offsets[i + 1] - offsets[i];
+    }
+    return mtg_boss_ctor_add_sequences(c, ptrs.data(), lens.data(), counts, n);
 }
 
 int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_count, uint64_t max_count,
@@ -1760,7 +1764,7 @@ int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_c
     }
     try {
         KmcInput in = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0);
-        std::lock_guard<std::mutex> lock(c->mu);
+        std::lock_guard<std::mutex> lock(c->kmc_mu);
         if (in.total) c->kmc.push_back(std::move(in));
         return MTG_OK;
     } catch (const std::exception &e) {
@@ -1807,18 +1811,28 @@ static int build_device_impl(mtg_boss_ctor *c, mtg::Comm *comm, const uint8_t *d
     return MTG_OK;
 }
 
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// build_chunk on the staged reads: one H2D copy of the pinned read buffer (+ KMC records), the
+// device path, then W / packed last / weights D2H into pinned blocks the chunk owns
 static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *out) {
     if (!c || !out) {
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
     }
+    const auto t_start = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lock(c->mu);
+    std::unique_lock<std::shared_mutex> stage_lock(c->stage.lock());  // no add runs during the build
+    std::lock_guard<std::mutex> kmc_lock(c->kmc_mu);
     std::memset(out, 0, sizeof(*out));
     try {
         HIP_CHECK(hipSetDevice(c->device));
         hipStream_t s = c->ctx.stream;
-        const uint64_t len = c->data.size();
-        const uint64_t nr = c->starts.size();
+        const HostStage &st = c->stage;
+        const uint64_t len = st.size();
+        const uint64_t nr = st.n_reads();
         uint64_t kmc_bytes = 0, kmc_reads = 0;
         for (const auto &m : c->kmc) {
             kmc_bytes += m.total * (m.k + 1) * (m.both ? 2 : 1);
@@ -1826,18 +1840,21 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         }
         const uint64_t total_len = len + kmc_bytes, total_reads = nr + kmc_reads;
         uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
-        if (len) HIP_CHECK(hipMemcpyAsync(dseq, c->data.data(), len, hipMemcpyHostToDevice, s));
+        const auto t_h2d = std::chrono::steady_clock::now();
+        if (len) HIP_CHECK(hipMemcpyAsync(dseq, st.data(), len, hipMemcpyHostToDevice, s));
         uint64_t *dstarts = nullptr;
         uint32_t *dcounts = nullptr;
-        const bool per_read = c->params.bits_per_count && (c->any_count_not_one || kmc_reads) && total_reads;
+        const bool per_read = c->params.bits_per_count && (st.any_count_not_one() || kmc_reads) && total_reads;
         if (per_read) {
             dstarts = (uint64_t *)c->ctx.ws.get(Workspace::STARTS, total_reads * 8);
             dcounts = (uint32_t *)c->ctx.ws.get(Workspace::RCOUNTS, total_reads * 4);
             if (nr) {
-                HIP_CHECK(hipMemcpyAsync(dstarts, c->starts.data(), nr * 8, hipMemcpyHostToDevice, s));
-                HIP_CHECK(hipMemcpyAsync(dcounts, c->counts.data(), nr * 4, hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(dstarts, st.starts().data(), nr * 8, hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(dcounts, st.counts().data(), nr * 4, hipMemcpyHostToDevice, s));
             }
         }
+        HIP_CHECK(hipStreamSynchronize(s));
+        const double h2d_ms = ms_since(t_h2d);
         // KMC records -> reads, on the device (kmc.hpp)
         uint64_t seq_base = len, read_base = nr;
         for (const auto &m : c->kmc) {
@@ -1858,6 +1875,13 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         BuildOutput o{};
         run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
                      c->params.bits_per_count, in, &o);
+        const auto t_d2h = std::chrono::steady_clock::now();
+        const uint64_t nwords = ceil_div(o.n, 64);
+        uint64_t *dbits = (uint64_t *)c->ctx.ws.get(Workspace::LAST_BITS, std::max<uint64_t>(nwords, 1) * 8);
+        if (nwords) {
+            pack_bits_kernel<<<dim3((unsigned)ceil_div(nwords, 256)), dim3(256), 0, s>>>(o.last, o.n, dbits);
+            HIP_CHECK(hipGetLastError());
+        }
         out->k = c->params.k;
         out->alph_size = 5;
         out->n = o.n;
@@ -1865,22 +1889,24 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         out->n_real = o.n_real;
         out->n_dummy = o.n_dummy;
         std::memcpy(out->F, o.F, sizeof(o.F));
-        out->W = (uint8_t *)std::malloc(o.n);
-        out->last = (uint8_t *)std::malloc(o.n);
-        if (!out->W || !out->last) throw std::runtime_error("host out of memory");
+        PinnedPool &pool = PinnedPool::get();
+        out->W = (uint8_t *)pool.take(o.n);
+        out->last = (uint64_t *)pool.take(std::max<uint64_t>(nwords, 1) * 8);
         HIP_CHECK(hipMemcpyAsync(out->W, o.W, o.n, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipMemcpyAsync(out->last, o.last, o.n, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(out->last, dbits, nwords * 8, hipMemcpyDeviceToHost, s));
         if (o.weights) {
-            out->weights = (uint32_t *)std::malloc(o.n * 4);
-            if (!out->weights) throw std::runtime_error("host out of memory");
+            out->weights = (uint32_t *)pool.take(o.n * 4);
             HIP_CHECK(hipMemcpyAsync(out->weights, o.weights, o.n * 4, hipMemcpyDeviceToHost, s));
         }
         HIP_CHECK(hipStreamSynchronize(s));
-        c->data.clear();
-        c->starts.clear();
-        c->counts.clear();
-        c->any_count_not_one = false;
+        mtg_boss_timings &T = c->ctx.timings;
+        T.d2h_ms = ms_since(t_d2h);
+        T.h2d_ms = h2d_ms;
+        T.stage_ms = (double)c->stage_ns.exchange(0) * 1e-6;
+        stage_lock.unlock();
+        c->stage.clear();
         c->kmc.clear();
+        T.host_total_ms = ms_since(t_start);
         return MTG_OK;
     } catch (const std::exception &e) {
         set_error(e.what());
@@ -1980,12 +2006,17 @@ int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64
 
 void mtg_boss_chunk_free(mtg_boss_chunk *chunk) {
     if (!chunk) return;
-    std::free(chunk->W);
-    std::free(chunk->last);
-    std::free(chunk->weights);
-    chunk->W = chunk->last = nullptr;
+    PinnedPool &pool = PinnedPool::get();
+    for (void *p : {(void *)chunk->W, (void *)chunk->last, (void *)chunk->weights})
+        if (!pool.give(p)) std::free(p);
+    chunk->W = nullptr;
+    chunk->last = nullptr;
     chunk->weights = nullptr;
     chunk->n = 0;
+}
+
+void mtg_dna_encode_table(uint8_t *out) {
+    for (uint32_t c = 0; c < 256; ++c) out[c] = (uint8_t)encode_dna(c);
 }
 
 int mtg_boss_last_timings(const mtg_boss_ctor *c, mtg_boss_timings *out) {

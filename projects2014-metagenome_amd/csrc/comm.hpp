@@ -167,18 +167,30 @@ struct LocalGroup {
     std::vector<Slot> slots;
     std::vector<std::vector<uint64_t>> host;
 
-    // a rank that failed never arrives: the others give up after a minute instead of hanging
+    std::string failure;  // first error any rank reported: every barrier then throws it
+
+    // a rank that failed says so (fail), and peers waiting in a barrier throw its message at once;
+    // a rank that dies without failing never arrives, and the others give up after a minute
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (!failure.empty()) throw std::runtime_error(failure);
         const uint64_t gen = generation;
         if (++arrived == size) {
             arrived = 0;
             ++generation;
             cv.notify_all();
-        } else if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return generation != gen; })) {
-            --arrived;
-            throw std::runtime_error("local exchange group: a peer rank did not arrive");
+            return;
         }
+        const bool ok = cv.wait_for(lk, std::chrono::seconds(60),
+                                    [&] { return generation != gen || !failure.empty(); });
+        if (generation != gen) return;
+        --arrived;
+        throw std::runtime_error(ok ? failure : std::string("local exchange group: a peer rank did not arrive"));
+    }
+    void fail(const std::string &msg) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (failure.empty()) failure = msg;
+        cv.notify_all();
     }
 };
 
@@ -218,10 +230,16 @@ class LocalComm : public Comm {
         slot.soff.assign(soff, soff + size_);
         slot.scnt.assign(scnt, scnt + size_);
         g_->barrier();
+        for (int i = 0; i < size_; ++i)
+            if (g_->slots[i].scnt[rank_] != rcnt[i]) {
+                const std::string msg = "local all-to-all: rank " + std::to_string(rank_) + " expects " +
+                                        std::to_string(rcnt[i]) + " elements from rank " + std::to_string(i) +
+                                        ", which sends " + std::to_string(g_->slots[i].scnt[rank_]);
+                g_->fail(msg);  // peers in the next barrier throw this too, without waiting
+                throw std::runtime_error(msg);
+            }
         for (int i = 0; i < size_; ++i) {
             const auto &src = g_->slots[i];
-            if (src.scnt[rank_] != rcnt[i])
-                throw std::runtime_error("local all-to-all: count mismatch");
             if (rcnt[i])
                 COMM_HIP(hipMemcpyAsync((char *)d_recv + roff[i] * esz,
                                         (const char *)src.ptr + src.soff[rank_] * esz, rcnt[i] * esz,

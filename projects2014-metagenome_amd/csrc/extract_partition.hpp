@@ -138,8 +138,9 @@ template <bool COUNTED, int BLOCK_>
 __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
-    uint32_t cmax, unsigned b, unsigned long long *__restrict__ cursor, Key<1> *__restrict__ kout,
-    uint32_t *__restrict__ vout) {
+    uint32_t cmax, unsigned b, unsigned long long *__restrict__ cursor,
+    const unsigned long long *__restrict__ bend, Key<1> *__restrict__ kout, uint32_t *__restrict__ vout,
+    uint32_t *__restrict__ error) {
     using F = FusedTraits<COUNTED, BLOCK_>;
     constexpr int BLOCK = F::BLOCK, PPT = F::PPT, TILE = F::TILE;
     constexpr int NBMAX = 512;
@@ -184,7 +185,12 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
         const uint32_t i = tid * PER + q;
         if (i < nb) {
             s_cnt[i] = off;
-            s_gbase[i] = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
+            unsigned long long g = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
+            if (c[q] && g + c[q] > bend[i]) {  // pass A counted this bucket differently: never
+                atomicOr(error, 2u);            // write past its range (the host raises)
+                g = ~0ull;
+            }
+            s_gbase[i] = g;
         }
         off += c[q];
     }
@@ -201,10 +207,20 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     for (uint32_t p = tid; p < total; p += BLOCK) {
         const Key<1> key = s_keys[p];
         const uint32_t lb = key_prefix(key, 2 * K, b);
+        if (s_gbase[lb] == ~0ull) continue;
         const uint64_t o = s_gbase[lb] + (p - s_cnt[lb]);
         kout[o] = key;
         if (COUNTED) vout[o] = s_vals[p];
     }
+}
+
+// after pass B every cursor must sit exactly at its bucket's end (fewer keys than pass A counted
+// would leave holes); sets error bit 2 otherwise
+__global__ void cursor_check_kernel(const unsigned long long *__restrict__ cursor,
+                                    const unsigned long long *__restrict__ bend, uint32_t nb,
+                                    uint32_t *__restrict__ error) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb && cursor[i] != bend[i]) atomicOr(error, 2u);
 }
 
 // duplication estimate straight from the read bytes (the keys do not exist yet): the k-mer at

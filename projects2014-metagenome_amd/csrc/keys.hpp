@@ -166,7 +166,7 @@ MTG_HD uint32_t char_at(const Key<L> &a, unsigned i, unsigned bits_per_char) {
 }
 
 // reverse the order of the 32 2-bit groups of a word
-MTG_HD inline uint64_t reverse_pairs64(uint64_t v) {
+MTG_HD uint64_t reverse_pairs64(uint64_t v) {
     v = __builtin_bswap64(v);
     v = ((v >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((v & 0x0F0F0F0F0F0F0F0Full) << 4);
     v = ((v >> 2) & 0x3333333333333333ull) | ((v & 0x3333333333333333ull) << 2);

@@ -82,7 +82,7 @@ static KmcInput kmc_open(const std::string &path, uint64_t min_count, uint64_t m
         throw bad("no KMCS markers");
     uint32_t hsize;
     memcpy(&hsize, pre.data() + pre.size() - 8, 4);
-    if (hsize < 36 || hsize + 12 > pre.size()) throw bad("header size");
+    if (hsize < 36 || (uint64_t)hsize + 12 > (uint64_t)pre.size()) throw bad("header size");
     const uint8_t *h = pre.data() + pre.size() - 8 - hsize;
     uint32_t f[6];
     memcpy(f, h, 24);

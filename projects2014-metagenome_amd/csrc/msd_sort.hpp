@@ -166,7 +166,7 @@ __global__ __launch_bounds__(512) void scan_counts_kernel(const uint32_t *__rest
  * and each run is written contiguously.  Keys outside the tile's LDS window (tiles spanning
  * more than MSD_WIN tiny segments) take one atomic each.
  */
-template <int L, bool HAS_VAL, bool VEC = false, int BLOCK = MSD_BLOCK>
+template <int L, bool HAS_VAL, int BLOCK = MSD_BLOCK>
 __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
@@ -192,39 +192,14 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     Key<L> k[ITEMS];
     uint32_t v[ITEMS];
     uint32_t r[ITEMS];
-    // L == 1: lane tid loads keys (2 tid, 2 tid + 1) of each 2 * BLOCK span as one 16-byte
-    // load (order inside a tile is irrelevant to the partition)
-    constexpr bool PAIR = L == 1 && VEC;
     bool have[ITEMS];
-    if constexpr (PAIR) {
 #pragma unroll
-        for (int j = 0; j < ITEMS; j += 2) {
-            const uint64_t i = base + 2 * ((uint64_t)(j / 2) * BLOCK + tid);
-            have[j] = i < n;
-            have[j + 1] = i + 1 < n;
-            if (i + 1 < n) {
-                const ulonglong2 kv = *(const ulonglong2 *)(kin + i);
-                k[j] = Key<L>::from(kv.x);
-                k[j + 1] = Key<L>::from(kv.y);
-                if (HAS_VAL) {
-                    const uint2 vv = *(const uint2 *)(vin + i);
-                    v[j] = vv.x;
-                    v[j + 1] = vv.y;
-                }
-            } else if (i < n) {
-                k[j] = kin[i];
-                if (HAS_VAL) v[j] = vin[i];
-            }
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const uint64_t i = base + (uint64_t)j * BLOCK + tid;
-            have[j] = i < n;
-            if (i < n) {
-                k[j] = kin[i];
-                if (HAS_VAL) v[j] = vin[i];
-            }
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * BLOCK + tid;
+        have[j] = i < n;
+        if (i < n) {
+            k[j] = kin[i];
+            if (HAS_VAL) v[j] = vin[i];
         }
     }
 #pragma unroll
@@ -278,25 +253,8 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
         const Key<L> key = s_keys[p];
         const uint32_t lb = key_prefix(key, nbits, b) - wbase;
         const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
-        if constexpr (PAIR) {
-            // 16-byte stores at even output slots: the lane at an even slot writes its key and
-            // the next one of the run; an odd slot is written alone only at the run's start
-            if (o & 1) {
-                if (p == s_loff[lb]) {
-                    kout[o] = key;
-                    if (HAS_VAL) vout[o] = s_vals[p];
-                }
-            } else if (p + 1 < s_loff[lb] + s_cnt[lb]) {
-                *(ulonglong2 *)(kout + o) = make_ulonglong2(key.w[0], s_keys[p + 1].w[0]);
-                if (HAS_VAL) *(uint2 *)(vout + o) = make_uint2(s_vals[p], s_vals[p + 1]);
-            } else {
-                kout[o] = key;
-                if (HAS_VAL) vout[o] = s_vals[p];
-            }
-        } else {
-            kout[o] = key;
-            if (HAS_VAL) vout[o] = s_vals[p];
-        }
+        kout[o] = key;
+        if (HAS_VAL) vout[o] = s_vals[p];
     }
 }
 

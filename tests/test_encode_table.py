@@ -1,23 +1,26 @@
-"""The device's branchless DNA encode (csrc/boss_kernels.hpp encode_dna) against the alphabet of
-kmer/alphabets.hpp:127-143: A/a 0, C/c 1, G/g 2, T/t/U/u 3, every other byte invalid (4).
-The table constant is read from the header and evaluated for all 256 byte values."""
-import os
-import re
+"""The extractor's DNA encode (csrc/boss_kernels.hpp encode_dna, the same __host__ __device__
+function the kernels call) against the alphabet of kmer/alphabets.hpp:127-143: A/a 0, C/c 1,
+G/g 2, T/t/U/u 3, every other byte invalid (4), for all 256 byte values.  The library evaluates
+the function itself (mtg_dna_encode_table), so no copy of its formula lives in the test."""
+import importlib
 
-HDR = os.path.join(os.path.dirname(__file__), "..", "projects2014-metagenome_amd", "csrc", "boss_kernels.hpp")
-
-
-def _table():
-    src = open(HDR).read()
-    m = re.search(r"TAB\s*=\s*(0x[0-9a-fA-F]+)ull", src)
-    assert m, "encode_dna table constant not found"
-    return int(m.group(1), 16)
+boss = importlib.import_module("projects2014-metagenome_amd.boss")
 
 
 def test_encode_table_matches_alphabet():
-    tab = _table()
+    got = boss.dna_encode_table()
     want = {ord(c): v for c, v in zip("AaCcGgTtUu", [0, 0, 1, 1, 2, 2, 3, 3, 3, 3])}
     for c in range(256):
-        idx = ((c | 0x20) - 0x61) & 0xFFFFFFFF
-        got = 4 if idx > 20 else (tab >> (3 * idx)) & 7
-        assert got == want.get(c, 4), (c, got)
+        assert got[c] == want.get(c, 4), (c, got[c])
+
+
+def test_last_bit_packing_roundtrip():
+    import numpy as np
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 63, 64, 65, 1000):
+        last = rng.integers(0, 2, size=n).astype(np.uint8)
+        words = boss.pack_last(last)
+        assert len(words) == (n + 63) // 64
+        assert np.array_equal(boss.unpack_last(words, n), last)
+        if n:
+            assert int(words[0]) & 1 == last[0]

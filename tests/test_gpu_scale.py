@@ -1,0 +1,126 @@
+"""Parity at the bench's scale: the code paths that only switch on for big inputs, compared bit
+for bit with the oracle (oracle/, the C restatement of boss_chunk_construct.cpp:54-356 and
+boss_chunk.cpp:32-133).
+
+* 2 M genome-sampled 150 bp reads at k = 31 (BASELINE configs[1]'s generator, a fifth of its
+  reads): the fused K1 (>= 4 M windows), the sampled duplication estimate and the multi-level
+  MSD plan it drives -- the same plan the 10 M-read bench step runs, without MTG_* overrides;
+* configs[0]: `build -k 12` on the whole transcripts_1000.fa (k_b = 11), basic and canonical;
+* k = 63 (2-bit u128 keys, lifted u256) on more than 4 M windows;
+* the full bench size (10 M reads, 1.2e9 windows), where the oracle would take minutes: the build
+  is invariant under the order of the reads and its size identities hold.
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+import bench
+
+boss = importlib.import_module("projects2014-metagenome_amd.boss")
+
+pytestmark = pytest.mark.gpu
+
+
+def _packed(asc):
+    n, L = asc.shape
+    return asc.reshape(-1), np.arange(n + 1, dtype=np.uint64) * L
+
+
+def _gpu_build(kb, asc, canonical, bits, threads=8):
+    ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=canonical, bits_per_count=bits,
+                                                 num_threads=threads)
+    data, off = _packed(asc)
+    ctor.add_packed(data, off)
+    chunk = ctor.build_chunk()
+    return chunk, ctor.timings()
+
+
+def _assert_same(got, want, ctx):
+    assert len(got.W) == len(want.W), ctx
+    assert np.array_equal(got.W, want.W), ctx
+    assert np.array_equal(got.last, want.last), ctx
+    assert np.array_equal(got.F, want.F), ctx
+    if want.weights is None:
+        assert got.weights is None, ctx
+    else:
+        assert np.array_equal(got.weights, want.weights), ctx
+    assert got.n_real == want.n_real, ctx
+
+
+@pytest.mark.parametrize("canonical,bits", [(True, 0), (False, 8)])
+def test_bench_generator_2m_reads_k31(canonical, bits):
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    got, t = _gpu_build(30, asc, canonical, bits)
+    assert t.n_extracted == 2_000_000 * 120
+    assert t.radix_launches >= 1, "the multi-level MSD plan did not run"
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=bits)
+    _assert_same(got, want, "2M reads k=31 canonical=%s bits=%d" % (canonical, bits))
+
+
+@pytest.mark.parametrize("canonical", [False, True])
+def test_config0_k12_full_transcripts(transcripts_1000, canonical):
+    for bits in (0, 8):
+        ctor = boss.IBOSSChunkConstructor.initialize(11, both_strands=canonical, bits_per_count=bits)
+        ctor.add_sequences(transcripts_1000)
+        got = ctor.build_chunk()
+        want = O.build_chunk(11, transcripts_1000, canonical=canonical, bits_per_count=bits)
+        _assert_same(got, want, "k=12 canonical=%s bits=%d" % (canonical, bits))
+
+
+def test_k63_u128_over_4m_windows():
+    asc = bench.make_reads_host_codes(50_000, 150, 777, "genome", 10.0)
+    assert len(asc) * (150 - 63 + 1) > 4_000_000
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    for canonical, bits in ((True, 0), (False, 16)):
+        got, _ = _gpu_build(62, asc, canonical, bits)
+        want = O.build_chunk(62, reads, canonical=canonical, bits_per_count=bits)
+        _assert_same(got, want, "k=63 canonical=%s bits=%d" % (canonical, bits))
+
+
+def test_fused_histogram_grid_stride(monkeypatch):
+    # the histogram pass's grid-stride loop with its next-tile prefetch, on a small input: a
+    # 3-workgroup grid strides over every tile (pass A and pass B must agree)
+    monkeypatch.setenv("MTG_FUSED_MIN", "0")
+    monkeypatch.setenv("MTG_HIST_ROWS", "3")
+    asc = bench.make_reads_host_codes(20_000, 150, 4242, "genome", 4.0)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    for kb, canonical, bits in ((30, True, 0), (20, False, 8), (9, True, 8)):
+        got, _ = _gpu_build(kb, asc, canonical, bits)
+        want = O.build_chunk(kb, reads, canonical=canonical, bits_per_count=bits)
+        _assert_same(got, want, "k=%d" % (kb + 1))
+
+
+def test_full_bench_size_order_invariant():
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n_reads, L = 10_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    # the same reads in reverse order (each read keeps its '$' separator)
+    rev = seq.view(n_reads, L + 1).flip(0).reshape(-1).contiguous()
+    torch.cuda.synchronize()
+    L_ = boss.lib()
+    out = []
+    for buf in (seq, rev):
+        ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True)
+        dc = ctor.build_device(buf.data_ptr(), buf.numel())
+        t = ctor.timings()
+        assert t.n_extracted == n_reads * (L - 31 + 1)
+        assert dc.n == t.n_rows == 1 + dc.n_real + dc.n_dummy
+        W = np.empty(dc.n, dtype=np.uint8)
+        last = np.empty(dc.n, dtype=np.uint8)
+        assert L_.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n) == 0
+        assert L_.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n) == 0
+        F = [int(f) for f in dc.F]
+        assert W.max() <= 9 and last.max() <= 1 and W[0] == 0 and last[0] == 0
+        assert F == sorted(F) and F[4] <= dc.n - 1
+        # real edges: W in 1..4 or 6..9 with a non-$ source node; every node closes with last = 1
+        assert last[-1] == 1
+        out.append((dc.n, dc.n_real, F, W, last))
+        del ctor
+    a, b = out
+    assert a[:3] == b[:3]
+    assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
