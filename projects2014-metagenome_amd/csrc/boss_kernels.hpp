@@ -757,143 +757,216 @@ __global__ __launch_bounds__(256) void merge_kernel(const Key<LA> *__restrict__ 
 }
 
 /*
- * K7 + K8 fused: the merge-path tile of merge(lift(A), B) is built in LDS exactly as merge_kernel
- * does, and the rows are emitted from there (emit_fast_kernel's rules, initialize_chunk,
- * boss_chunk.cpp:32-133) instead of writing the lifted stream and reading it back.  Stream row
- * r = off + d for merge position d (off = 1 behind the main dummy row, which emit_root_kernel
- * writes); output row r + 1.  The row after the tile is the merge's next element; the W "minus"
- * look-back continues past the tile start by merging A and B backwards (groups hold <= 25 rows).
- * A redundant dummy sink sets *skip and the caller redoes K7 + K8 unfused (compacting emit).
+ * K7 + K8 without materialising the merge ("split emit").  The stream rows are the lifted real
+ * edges A (2-bit keys, sorted) and the sorted distinct dummies B, interleaved in key order behind
+ * the main dummy row.  Two facts of the reference's construction make each row's W and last
+ * depend on its own array only:
+ *  - no dummy shares a node with a real edge: a sink exists only for a node that no real edge
+ *    leaves (boss_chunk_construct.cpp:63-97), and a source's node starts with $ (:123-168).  So
+ *    `last` of a real row compares it with the next real edge, and a dummy's with the next dummy;
+ *  - no dummy shares (chars 2..k, label) with a real edge: a level-1 source exists only when no
+ *    real edge has its chars 2..k and label (:148-166), higher levels have $ at char 2, and sinks
+ *    carry the label $.  So the W "minus" flag (boss_chunk.cpp:91-103) of a real row looks at
+ *    real rows only, and a dummy's at dummies only.
+ * dummy_rank_kernel checks both facts for every dummy against its group-mates in A, and also
+ * flags a redundant dummy sink (a row initialize_chunk skips).  Any hit raises *skip, and the
+ * caller then runs the exact unfused path (merge_kernel + the compacting emit_kernel).
+ *
+ * unlift_floor: the 2-bit X with #{A : lift(A) < b} = #{A : A < X}.  Walking b's chars from the
+ * top, lift(A) and b compare as A's char + 1 against b's char until b's first $, where every A
+ * that matched so far is bigger (lifted chars are >= 1).  So X = b's chars - 1 above that $,
+ * zeros from it down.
  */
-template <int LO, int LA>
-__device__ __forceinline__ bool merged_at(const Key<LA> *__restrict__ a, uint64_t na, const Key<LO> *__restrict__ b,
-                                          uint64_t nb, uint64_t ia, uint64_t ib, unsigned K, Key<LO> *out) {
-    // smallest of A[ia..] (lifted) and B[ib..]; false past both ends
-    const bool ha = ia < na, hb = ib < nb;
-    if (!ha && !hb) return false;
-    if (ha) {
-        const Key<LO> x = lift_fast<LO>(a[ia], K);
-        *out = (!hb || x < b[ib]) ? x : b[ib];
-    } else {
-        *out = b[ib];
+template <int L2, int L3>
+__device__ __forceinline__ Key<L2> unlift_floor(const Key<L3> &b, unsigned K) {
+    Key<L2> x = Key<L2>::zero();
+    for (int i = (int)K - 1; i >= 0; --i) {
+        const uint32_t ch = char_at(b, (unsigned)i, 3);
+        if (ch == 0) break;
+        x = x | shl(Key<L2>::from(ch - 1), 2 * i);
     }
-    return true;
+    return x;
 }
 
-template <int LO, int LA, bool COUNTED>
-__global__ __launch_bounds__(256) void merge_emit_kernel(const Key<LA> *__restrict__ a,
-                                                         const uint32_t *__restrict__ ac, uint64_t na,
-                                                         const Key<LO> *__restrict__ b, uint64_t nb, unsigned K,
-                                                         const uint64_t *__restrict__ splits, uint64_t off,
-                                                         uint32_t wmax, uint8_t *__restrict__ W,
-                                                         uint8_t *__restrict__ last, uint32_t *__restrict__ weights,
-                                                         uint32_t *__restrict__ skip) {
-    constexpr int TILE = MergeTraits<LO>::TILE, ITEMS = TILE / 256;
-    __shared__ Key<LO> s_in[TILE];
-    __shared__ Key<LO> s_out[TILE + 1];  // + the row after the tile
-    __shared__ uint32_t s_cin[COUNTED ? TILE : 1];
-    __shared__ uint32_t s_cout[COUNTED ? TILE : 1];
-    __shared__ uint8_t s_w[TILE], s_l[TILE];
-    __shared__ uint64_t s_split[2];
-    __shared__ int s_hasnext;
+// per dummy j: its output row pos[j] (row0 = output row of the first merged row) and its
+// W | last << 4 byte; *root_same = the main dummy row and B[0] share the all-$ node
+template <int L2, int L3>
+__global__ __launch_bounds__(256) void dummy_rank_kernel(
+    const Key<L2> *__restrict__ a, uint64_t na, const Key<L3> *__restrict__ b, uint64_t nb, unsigned K,
+    const uint64_t *__restrict__ bstart, unsigned bshift, uint64_t row0, uint64_t *__restrict__ pos,
+    uint8_t *__restrict__ wl, uint32_t *__restrict__ skip, uint32_t *__restrict__ root_same) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nb) return;
     const unsigned k = K - 1;
-    const uint64_t total = na + nb;
-    const uint64_t d0 = (uint64_t)blockIdx.x * TILE;
-    const uint64_t d1 = min(total, d0 + TILE);
-    if (threadIdx.x < 2) s_split[threadIdx.x] = splits[blockIdx.x + threadIdx.x];
-    __syncthreads();
-    const uint64_t a0 = s_split[0], a1 = s_split[1];
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-    const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0), n = la + lb;
-    for (uint32_t i = threadIdx.x; i < la; i += 256) {
-        s_in[i] = lift_fast<LO>(a[a0 + i], K);
-        if (COUNTED) s_cin[i] = ac[a0 + i];
-    }
-    for (uint32_t i = threadIdx.x; i < lb; i += 256) {
-        s_in[la + i] = b[b0 + i];
-        if (COUNTED) s_cin[la + i] = 0;
-    }
-    if (threadIdx.x == 0) {
-        Key<LO> nx;
-        s_hasnext = merged_at<LO, LA>(a, na, b, nb, a1, b1, K, &nx) ? 1 : 0;
-        if (s_hasnext) s_out[n] = nx;
-    }
-    __syncthreads();
-    const uint32_t t0 = min((uint32_t)threadIdx.x * ITEMS, n);
-    const uint32_t t1 = min(t0 + ITEMS, n);
-    uint32_t lo = t0 > lb ? t0 - lb : 0, hi = min(t0, la);
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_in[mid] < s_in[la + t0 - mid - 1]) lo = mid + 1; else hi = mid;
-    }
-    uint32_t i = lo, j = t0 - lo;
-    for (uint32_t o = t0; o < t1; ++o) {
-        const bool take_a = i < la && (j >= lb || s_in[i] < s_in[la + j]);
-        const uint32_t src = take_a ? i : la + j;
-        s_out[o] = s_in[src];
-        if (COUNTED) s_cout[o] = s_cin[src];
-        if (take_a) ++i; else ++j;
-    }
-    __syncthreads();
-    bool skipped = false;
-    for (uint32_t t = threadIdx.x; t < n; t += 256) {
-        const Key<LO> key = s_out[t];
-        const uint32_t c = (uint32_t)(key.w[0] & 7);
-        const Key<LO> node = shr(key, 3);
-        const bool has_next = t + 1 < n || s_hasnext;
-        const bool same_next = has_next && shr(s_out[t + 1], 3) == node;
-        if (same_next && c == 0 && char_at(key, k, 3) > 0) skipped = true;
-        uint32_t ww = c;
-        if (c) {
-            const Key<LO> grp = shr(key, 6);
-            bool done = false;
-            for (int64_t p = (int64_t)t - 1; p >= 0; --p) {
-                const Key<LO> y = s_out[p];
-                if (shr(y, 6) != grp) { done = true; break; }
-                if ((uint32_t)(y.w[0] & 7) == c) { ww = c + 5; done = true; break; }
-            }
-            if (!done) {  // the group continues before the tile: merge A, B backwards
-                uint64_t ia = a0, ib = b0;
-                while (ia > 0 || ib > 0) {
-                    Key<LO> y;
-                    if (ia > 0 && ib > 0) {
-                        const Key<LO> x = lift_fast<LO>(a[ia - 1], K);
-                        if (b[ib - 1] < x) { y = x; --ia; } else { y = b[ib - 1]; --ib; }
-                    } else if (ia > 0) {
-                        y = lift_fast<LO>(a[--ia], K);
-                    } else {
-                        y = b[--ib];
-                    }
-                    if (shr(y, 6) != grp) break;
-                    if ((uint32_t)(y.w[0] & 7) == c) { ww = c + 5; break; }
-                }
-            }
+    const Key<L3> x = b[j];
+    const Key<L2> X = unlift_floor<L2, L3>(x, K);
+    uint64_t r;
+    if (bstart) {
+        r = lower_bound_bucketed(a, bstart, bshift, X);
+    } else {
+        uint64_t lo = 0, hi = na;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (a[mid] < X) lo = mid + 1; else hi = mid;
         }
-        s_w[t] = (uint8_t)ww;
-        s_l[t] = same_next ? 0 : 1;
-        if (COUNTED) {
-            const uint32_t cnt = s_cout[t];
-            weights[off + d0 + t + 1] = (cnt && ww && char_at(key, 1, 3)) ? (cnt < wmax ? cnt : wmax) : 0;
+        r = lo;
+    }
+    pos[j] = row0 + j + r;
+    const Key<L3> node = shr(x, 3), grp = shr(x, 6);
+    const uint32_t c = (uint32_t)(x.w[0] & 7);
+    bool bad = false;
+    // the real edges of x's chars-2..k group sit next to r (at most 16: 4 first chars x 4 labels)
+    for (uint64_t i = r; i < na && i < r + 16; ++i) {
+        const Key<L3> y = lift_fast<L3>(a[i], K);
+        if (shr(y, 6) != grp) break;
+        bad |= shr(y, 3) == node || (c && (uint32_t)(y.w[0] & 7) == c);
+    }
+    for (uint64_t i = r; i > 0 && i + 16 > r; --i) {
+        const Key<L3> y = lift_fast<L3>(a[i - 1], K);
+        if (shr(y, 6) != grp) break;
+        bad |= shr(y, 3) == node || (c && (uint32_t)(y.w[0] & 7) == c);
+    }
+    uint32_t w = c;
+    if (c) {  // "minus" among the dummies of the group (at most 25 rows)
+        for (uint64_t p = j; p > 0; --p) {
+            const Key<L3> y = b[p - 1];
+            if (shr(y, 6) != grp) break;
+            if ((uint32_t)(y.w[0] & 7) == c) { w = c + 5; break; }
         }
     }
-    if (skipped) atomicOr(skip, 1u);
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n; t += 256) {
-        W[off + d0 + t + 1] = s_w[t];
-        last[off + d0 + t + 1] = s_l[t];
-    }
+    const bool same_next = j + 1 < nb && shr(b[j + 1], 3) == node;
+    if (same_next && c == 0 && char_at(x, k, 3) > 0) bad = true;  // redundant sink (boss_chunk.cpp:78-86)
+    wl[j] = (uint8_t)(w | (same_next ? 0u : 1u) << 4);
+    if (j == 0 && node == Key<L3>::zero()) *root_same = 1;
+    if (bad) atomicOr(skip, 1u);
 }
 
-// the main dummy row (stream row 0, all $) when the fused K7 + K8 runs: output row 1
-template <int LO, int LA, bool COUNTED>
-__global__ void emit_root_kernel(const Key<LA> *__restrict__ a, uint64_t na, const Key<LO> *__restrict__ b,
-                                 uint64_t nb, unsigned K, uint8_t *__restrict__ W, uint8_t *__restrict__ last,
-                                 uint32_t *__restrict__ weights) {
-    Key<LO> nx;
-    const bool has = merged_at<LO, LA>(a, na, b, nb, 0, 0, K, &nx);
-    W[1] = 0;  // label $
-    last[1] = has && shr(nx, 3) == Key<LO>::zero() ? 0 : 1;
-    if (COUNTED) weights[1] = 0;
+template <int L2>
+struct SplitEmitTraits {
+    static constexpr int TILE = L2 <= 2 ? 2048 : 1024;  // output rows per workgroup
+    static constexpr int PER = 8;                        // consecutive rows per thread
+    static constexpr int BLOCK = TILE / PER;
+    static constexpr int HALO = 16;                      // real edges staged before the tile
+};
+
+// jsplit[t] = #dummies whose output row is < t * TILE (one binary search per tile boundary)
+template <int TILE>
+__global__ void split_points_kernel(const uint64_t *__restrict__ pos, uint64_t nb, uint64_t ntiles,
+                                    uint64_t *__restrict__ jsplit) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t o = t * (uint64_t)TILE;
+    uint64_t lo = 0, hi = nb;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (pos[mid] < o) lo = mid + 1; else hi = mid;
+    }
+    jsplit[t] = lo;
+}
+
+/*
+ * The output rows [o0, o0 + TILE): row 0 is the leading all-zero row, row 1 the main dummy (when
+ * `root`), then the merged stream.  The tile's dummies are the pos[] entries in range (bitmask
+ * in LDS); the real edges between them are a contiguous run of A, staged in LDS with HALO edges
+ * before it (a chars-2..k group holds at most 16 real edges, so the "minus" look-back never
+ * leaves LDS) and one after it (the `last` compare).  A thread owns PER consecutive rows, so W
+ * and last leave as one aligned 8-byte store each.
+ */
+template <int L2, bool COUNTED>
+__global__ __launch_bounds__(SplitEmitTraits<L2>::BLOCK) void split_emit_kernel(
+    const Key<L2> *__restrict__ a, const uint32_t *__restrict__ ac, uint64_t na,
+    const uint64_t *__restrict__ pos, const uint8_t *__restrict__ wl, const uint64_t *__restrict__ jsplit,
+    uint64_t nout, uint32_t root, const uint32_t *__restrict__ root_same, uint32_t wmax,
+    uint8_t *__restrict__ W, uint8_t *__restrict__ last, uint32_t *__restrict__ weights) {
+    using T = SplitEmitTraits<L2>;
+    constexpr int TILE = T::TILE, PER = T::PER, HALO = T::HALO, BLOCK = T::BLOCK;
+    __shared__ Key<L2> s_a[TILE + HALO + 1];
+    __shared__ uint8_t s_bwl[TILE];
+    __shared__ uint32_t s_bm[TILE / 32];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t o0 = (uint64_t)blockIdx.x * TILE;
+    const uint64_t o1 = min(nout, o0 + TILE);
+    const uint64_t j0 = jsplit[blockIdx.x], j1 = jsplit[blockIdx.x + 1];
+    const uint32_t nbt = (uint32_t)(j1 - j0);
+    const uint64_t lead = 1 + root;  // output rows before the merged stream
+    const uint64_t m0 = o0 > lead ? o0 - lead : 0, m1 = o1 > lead ? o1 - lead : 0;
+    const uint64_t i0 = m0 - j0;                  // first real edge of the tile
+    const uint64_t i1 = m1 - j1;                  // one past its last
+    // stage A[i0 - HALO, i1 + 1) (clipped to [0, na))
+    const int64_t g0 = (int64_t)i0 - HALO;
+    const uint32_t ns = (uint32_t)(i1 - i0) + HALO + 1;
+    for (uint32_t q = tid; q < ns; q += BLOCK) {
+        const int64_t g = g0 + q;
+        if (g >= 0 && g < (int64_t)na) s_a[q] = a[g];
+    }
+    for (uint32_t q = tid; q < TILE / 32; q += BLOCK) s_bm[q] = 0;
+    __syncthreads();
+    for (uint32_t q = tid; q < nbt; q += BLOCK) {
+        const uint32_t off = (uint32_t)(pos[j0 + q] - o0);
+        s_bwl[q] = wl[j0 + q];
+        atomicOr(&s_bm[off >> 5], 1u << (off & 31));
+    }
+    __syncthreads();
+    const uint32_t r0 = tid * PER;
+    const uint32_t bits = (s_bm[r0 >> 5] >> (r0 & 31)) & 0xFFu;
+    uint32_t tot;
+    const uint32_t bq0 = block_exclusive_sum<BLOCK>((uint32_t)__popc(bits), s_scan, &tot);
+    uint64_t wpack = 0, lpack = 0;
+    uint32_t wt[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        wt[q] = 0;
+        const uint64_t o = o0 + r0 + q;
+        if (o >= o1) continue;
+        uint32_t ww = 0, ll = 0;
+        const uint32_t bq = bq0 + (uint32_t)__popc(bits & ((1u << q) - 1));
+        if (o < lead) {
+            ll = o == 0 ? 0u : (*root_same ? 0u : 1u);  // leading row; main dummy row
+        } else if ((bits >> q) & 1u) {
+            const uint32_t v = s_bwl[bq];
+            ww = v & 15u;
+            ll = v >> 4;
+        } else {
+            const uint64_t ia = (o - lead) - (j0 + bq);
+            const uint32_t li = (uint32_t)(ia - i0) + HALO;
+            const Key<L2> x = s_a[li];
+            const uint32_t c = (uint32_t)(x.w[0] & 3);
+            const Key<L2> grp = shr(x, 4);
+            bool minus = false;
+            const uint32_t back = (uint32_t)min<uint64_t>(ia, HALO - 1);
+            for (uint32_t p = 1; p <= back; ++p) {
+                const Key<L2> y = s_a[li - p];
+                if (shr(y, 4) != grp) break;
+                if ((uint32_t)(y.w[0] & 3) == c) { minus = true; break; }
+            }
+            ww = c + 1 + (minus ? 5u : 0u);
+            ll = ia + 1 < na && shr(s_a[li + 1], 2) == shr(x, 2) ? 0u : 1u;
+            if (COUNTED) {
+                const uint32_t cnt = ac[ia];
+                wt[q] = cnt < wmax ? cnt : wmax;
+            }
+        }
+        wpack |= (uint64_t)ww << (8 * q);
+        lpack |= (uint64_t)ll << (8 * q);
+    }
+    const uint64_t ob = o0 + r0;
+    if (ob + PER <= o1) {
+        *(uint64_t *)(W + ob) = wpack;
+        *(uint64_t *)(last + ob) = lpack;
+        if (COUNTED) {
+            *(uint4 *)(weights + ob) = make_uint4(wt[0], wt[1], wt[2], wt[3]);
+            *(uint4 *)(weights + ob + 4) = make_uint4(wt[4], wt[5], wt[6], wt[7]);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            if (ob + q >= o1) break;
+            W[ob + q] = (uint8_t)(wpack >> (8 * q));
+            last[ob + q] = (uint8_t)(lpack >> (8 * q));
+            if (COUNTED) weights[ob + q] = wt[q];
+        }
+    }
 }
 
 // F[c] = #stream rows whose last node char < c: the root ($), lifted A (char + 1) and B, by

@@ -53,7 +53,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR,
-        LAST_BITS, NSLOTS
+        LAST_BITS, DPOS, DWL, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -97,6 +97,7 @@ struct Small {  // one device word block, zeroed per use
     unsigned long long fhist[8];
     uint32_t counter;
     uint32_t skip;
+    uint32_t root_same;
     uint32_t error;
 };
 
@@ -147,6 +148,11 @@ struct Ctx {
     double fused_ms = 0;           // device time of the last fused extract+partition launch
     bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it (the
                                    // redundant-sink path)
+    // bucket index over the real edges, built by the dummy stage and reused by the split emit
+    const void *bidx_keys = nullptr;
+    uint64_t bidx_n = 0;
+    const uint64_t *bidx = nullptr;
+    unsigned bidx_shift = 0;
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -910,6 +916,14 @@ static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db
     return D;
 }
 
+// remember the bucket index over the real edges for the split emit's dummy ranks
+static void note_bucket_index(Ctx &c, const void *keys, uint64_t n, const uint64_t *start, unsigned shift) {
+    c.bidx_keys = keys;
+    c.bidx_n = n;
+    c.bidx = start;
+    c.bidx_shift = shift;
+}
+
 // K5/K6 on one device: dummy sinks and sources (all levels) of the sorted real edges ka[0..R)
 template <int L2, int L3>
 static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint64_t R, Key<L3> **dk) {
@@ -922,6 +936,7 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
     const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
     bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
     HIP_CHECK(hipGetLastError());
+    note_bucket_index(c, ka, R, bstart, bshift);
     uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
     uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
     const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
@@ -966,28 +981,32 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
     const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
     const uint64_t M = (root ? 1 : 0) + R + D;
     if (c.fused_emit && !c.emit_slow && M) {
-        // K7 + K8 in one pass over A and B (merge_emit_kernel); a redundant sink falls through
-        uint8_t *W = (uint8_t *)c.ws.get(Workspace::OW, M + 1);
-        uint8_t *last = (uint8_t *)c.ws.get(Workspace::OLAST, M + 1);
-        uint32_t *weights = COUNTED ? (uint32_t *)c.ws.get(Workspace::OWEIGHTS, (M + 1) * 4) : nullptr;
-        HIP_CHECK(hipMemsetAsync(W, 0, 1, c.stream));
-        HIP_CHECK(hipMemsetAsync(last, 0, 1, c.stream));
-        if (COUNTED) HIP_CHECK(hipMemsetAsync(weights, 0, 4, c.stream));
+        // K7 + K8 without the merged stream (split_emit_kernel): the dummies' output rows from
+        // their ranks in A, then one pass over the output rows; a violated premise or a redundant
+        // sink falls through to the exact unfused path below
+        using SE = SplitEmitTraits<L2>;
+        const uint64_t nout = M + 1;
+        uint8_t *W = (uint8_t *)c.ws.get(Workspace::OW, nout);
+        uint8_t *last = (uint8_t *)c.ws.get(Workspace::OLAST, nout);
+        uint32_t *weights = COUNTED ? (uint32_t *)c.ws.get(Workspace::OWEIGHTS, nout * 4) : nullptr;
+        uint64_t *pos = (uint64_t *)c.ws.get(Workspace::DPOS, D * 8);
+        uint8_t *wl = (uint8_t *)c.ws.get(Workspace::DWL, D);
+        const uint64_t ntiles = ceil_div(nout, SE::TILE);
+        uint64_t *jsplit = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
         reset_small(c);
-        if (root) {
-            emit_root_kernel<L3, L2, COUNTED><<<1, 1, 0, c.stream>>>(real, R, dk, D, K, W, last, weights);
+        if (D) {
+            const bool idx = c.bidx_keys == (const void *)real && c.bidx_n == R;
+            dummy_rank_kernel<L2, L3><<<dim3((unsigned)ceil_div(D, 256)), dim3(256), 0, c.stream>>>(
+                real, R, dk, D, K, idx ? c.bidx : nullptr, c.bidx_shift, root ? 2 : 1, pos, wl,
+                &c.small->skip, &c.small->root_same);
             HIP_CHECK(hipGetLastError());
         }
-        const uint64_t ntiles = ceil_div(R + D, MergeTraits<L3>::TILE);
-        if (ntiles) {
-            uint64_t *splits = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
-            merge_partition_kernel<L3, L2, true><<<dim3((unsigned)ceil_div(ntiles + 1, 256)), dim3(256), 0, c.stream>>>(
-                real, R, dk, D, K, ntiles, splits);
-            HIP_CHECK(hipGetLastError());
-            merge_emit_kernel<L3, L2, COUNTED><<<dim3((unsigned)ntiles), dim3(256), 0, c.stream>>>(
-                real, realc, R, dk, D, K, splits, root ? 1 : 0, wmax, W, last, weights, &c.small->skip);
-            HIP_CHECK(hipGetLastError());
-        }
+        split_points_kernel<SE::TILE><<<dim3((unsigned)ceil_div(ntiles + 1, 256)), dim3(256), 0, c.stream>>>(
+            pos, D, ntiles, jsplit);
+        HIP_CHECK(hipGetLastError());
+        split_emit_kernel<L2, COUNTED><<<dim3((unsigned)ntiles), dim3(SE::BLOCK), 0, c.stream>>>(
+            real, realc, R, pos, wl, jsplit, nout, root ? 1 : 0, &c.small->root_same, wmax, W, last, weights);
+        HIP_CHECK(hipGetLastError());
         f_bounds_split_kernel<L3, L2><<<1, 64, 0, c.stream>>>(real, R, dk, D, K, root ? 1 : 0, c.small->fhist);
         HIP_CHECK(hipGetLastError());
         *ev_merge = tm.mark();
@@ -999,7 +1018,7 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
             out->W = W;
             out->last = last;
             out->weights = weights;
-            out->n = M + 1;
+            out->n = nout;
             out->n_real = R;
             out->n_dummy = M - R;
             return;
@@ -1074,6 +1093,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
     mtg_boss_timings &T = c.timings;
     T = mtg_boss_timings{};
+    note_bucket_index(c, nullptr, 0, nullptr, 0);
     T.world = 1;
     T.n_batches = 1;
     HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
@@ -1350,6 +1370,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
     mtg_boss_timings &T = c.timings;
     T = mtg_boss_timings{};
+    note_bucket_index(c, nullptr, 0, nullptr, 0);
     HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
     EventTimer tm(c.stream);
     const int ev_start = tm.mark();
@@ -1463,6 +1484,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
         bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(E, R, bshift, nbk, bstart);
         HIP_CHECK(hipGetLastError());
+        note_bucket_index(c, E, R, bstart, bshift);
         uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
         uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
         if (R) {

@@ -166,13 +166,11 @@ def test_device_build_matches_host_build():
         L.mtg_device_free(d)
 
 
-@pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_DUMMY_SORT": "msd"},
-                                 {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_FUSED": "0"},
-                                 {"MTG_MERGE": "insert"}, {"MTG_FUSED_EMIT": "0"},
-                                 {"MTG_FUSED_MIN": "0", "MTG_FUSED_BLOCK": "256"},
-                                 {"MTG_FUSED_MIN": "0", "MTG_FUSED_BLOCK": "1024"}])
+@pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"},
+                                 {"MTG_FUSED": "0"}, {"MTG_FUSED_EMIT": "0"}])
 def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
-    # the compacting emit kernel, the MSD dummy sort and the LSD sorts stay bit-exact too
+    # the unfused merge + emit, the compacting emit kernel, the unfused K1 and the LSD sorts
+    # stay bit-exact too
     for key, val in env.items():
         monkeypatch.setenv(key, val)
     for k, canonical, bits in [(19, True, 8), (30, False, 0), (40, True, 16), (3, False, 8)]:

@@ -1,9 +1,11 @@
 """Summarise a rocprofv3 kernel_stats.csv (and per-launch trace) of a bench run."""
 import csv
+import glob
 import sys
 
 d = sys.argv[1]
-rows = list(csv.DictReader(open(d + "/run_kernel_stats.csv")))
+path = sorted(glob.glob(d + "/**/*kernel_stats.csv", recursive=True))[0]
+rows = list(csv.DictReader(open(path)))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:int(sys.argv[2]) if len(sys.argv) > 2 else 25]:
     name = r["Name"]
