@@ -30,8 +30,19 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
+# BASELINE.json configs this bench runs (configs[1] is the default line; configs[2] is the
+# k=63 / 100 M-read u128 build that does not fit HBM in one pass and runs in key ranges)
+CONFIGS = {
+    "cfg2": {"k": 31, "reads": 10_000_000},
+    "cfg3": {"k": 63, "reads": 100_000_000, "host_steps": 0, "cpu_sample_reads": 500_000,
+             "steps": 2, "warmup": 1},
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="a BASELINE config preset (explicit flags still override)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -47,7 +58,13 @@ def parse():
     ap.add_argument("--host-steps", type=int, default=3,
                     help="steps of the host-buffer leg (0 = skip)")
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config:
+        given = {a.split("=")[0].lstrip("-").replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
+        for key, val in CONFIGS[args.config].items():
+            if key not in given:
+                setattr(args, key, val)
+    return args
 
 
 def make_reads_device(torch, n_reads, read_len, seed, data, coverage, device, world=1,
@@ -320,7 +337,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64",
+        "dtype": "u64" if 2 * args.k <= 64 else "u128" if 2 * args.k <= 128 else "u256",
         "data": "synthetic (%s-sampled %d bp reads, %gx coverage, seeded per rank)"
                 % (args.data, args.read_len, args.coverage),
         "config": {"workload": "metagraph build -k %d --mode %s%s, %d synthetic %d bp reads per GPU"
@@ -344,7 +361,8 @@ def main():
         "stages_ms": {k2: last[k2] for k2 in ("extract_ms", "sort_ms", "unique_ms", "rc_ms",
                                               "dummy_ms", "merge_ms", "emit_ms", "total_ms")},
         "counts": {k2: last[k2] for k2 in ("n_extracted", "n_unique", "n_real", "n_dummy",
-                                           "n_rows", "radix_launches", "n_sent")},
+                                           "n_rows", "radix_launches", "n_sent", "n_batches",
+                                           "peak_bytes")},
         "exchange_ms": last["exchange_ms"],
     }
     if rank == 0 and args.host_steps > 0 and world == 1:

@@ -51,7 +51,7 @@ extern "C" {
 #define MTG_OK 0
 #define MTG_ERR_INVALID_K -1        /* k not in [1, 84]      (reference: exit(1)) */
 #define MTG_ERR_COUNT_WIDTH -2      /* bits_per_count > 32   (reference: runtime_error) */
-#define MTG_ERR_UNSUPPORTED -3      /* suffix filter / disk container not on this path */
+#define MTG_ERR_UNSUPPORTED -3      /* suffix filter not on this path */
 #define MTG_ERR_DEVICE -4           /* HIP runtime / kernel failure */
 #define MTG_ERR_ARGUMENT -5
 #define MTG_ERR_NO_DEVICE -6        /* no MI355X visible: the product path never falls back */
@@ -64,9 +64,11 @@ typedef struct mtg_boss_params {
     uint64_t num_threads;        /* host threads for input staging */
     double memory_preallocated;  /* bytes of device memory the build may use (0 = all free HBM);
                                     larger inputs are built in key-range batches */
-    int container_type;          /* MTG_CONTAINER_VECTOR */
-    const char *swap_dir;        /* unused on the in-memory path */
-    uint64_t disk_cap_bytes;     /* unused on the in-memory path */
+    int container_type;          /* MTG_CONTAINER_VECTOR, or MTG_CONTAINER_VECTOR_DISK (--disk-swap):
+                                    the bounded-memory build, in key-range batches (nothing spills:
+                                    the real edges stay in HBM) */
+    const char *swap_dir;        /* unused: no spill files */
+    uint64_t disk_cap_bytes;     /* unused: no spill files */
     int device_id;               /* HIP device ordinal */
 } mtg_boss_params;
 

@@ -143,6 +143,9 @@ struct Ctx {
     bool trace = false;            // MTG_TRACE=1: per-step wall times and sizes of the dist build
     bool fused = true;             // MTG_FUSED=0: K1 writes in window order, K2 partitions after
     uint64_t fused_min = 1ull << 22;  // MTG_FUSED_MIN: fewest window starts for the fused K1
+    uint32_t force_ranges = 0;     // MTG_RANGES=P: collect in P key ranges (tests; else planned from memory)
+    double mem_budget = 0;         // memory_preallocated (bytes; 0 = free HBM)
+    bool disk = false;             // MTG_CONTAINER_VECTOR_DISK: the bounded-memory (range-batched) build
     uint32_t hist_rows = 2048;     // MTG_HIST_ROWS: workgroups of the fused K1 histogram pass (tests
                                    // lower it so the grid-stride + prefetch loop runs on small inputs)
     double fused_ms = 0;           // device time of the last fused extract+partition launch
@@ -172,6 +175,7 @@ static void load_knobs(Ctx &c) {
     c.debug = getenv("MTG_DEBUG") != nullptr;
     c.trace = getenv("MTG_TRACE") != nullptr;
     if (const char *e = getenv("MTG_FUSED_MIN")) c.fused_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("MTG_RANGES")) c.force_ranges = (uint32_t)std::max(0L, std::min(4096L, atol(e)));
     if (const char *e = getenv("MTG_HIST_ROWS")) c.hist_rows = (uint32_t)std::max(1L, std::min(2048L, atol(e)));
 }
 
@@ -849,6 +853,128 @@ static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, K
     return U;
 }
 
+// ------------------------------------------------------------------- range-batched collection
+//
+// Inputs whose k-mers do not fit HBM at once (BASELINE configs[2]: 8.8e9 u128 windows) are
+// collected one key range at a time, the bounded-memory role of the reference's disk container
+// (SortedSetDisk + construct_boss_chunk_disk, boss_chunk_construct.cpp:664-933): every range
+// re-scans the read buffer, extracts only the k-mers whose top chars fall in it, sorts and
+// dedupes them (saturating counts), and appends them to the real-edge array.  The ranges are
+// consecutive in BOSS order, so the appended array is sorted.  Canonical mode extracts BOTH
+// strands: the real edges of CANONICAL_ONLY are exactly the k-mers of both strands (the canonical
+// set plus add_reverse_complements, :179-222), and a palindrome window contributes its k-mer twice,
+// the reference's doubled palindrome count.  Everything after the real edges (dummies, emit) is
+// the single-pass pipeline's.
+
+static std::vector<uint64_t> balanced_bounds(const uint64_t *hist, uint64_t nb, int P);
+
+// number of key ranges for this input: 1 when the single-pass footprint fits the budget
+// (memory_preallocated, else the free HBM plus what the workspace already holds)
+template <int L2, bool COUNTED>
+static uint32_t plan_ranges(Ctx &c, unsigned K, bool canonical, const BuildInput &in) {
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    if (c.force_ranges) return c.force_ranges;
+    const double per_key = (double)sizeof(Key<L2>) + (COUNTED ? 4.0 : 0.0);
+    double budget = c.mem_budget;
+    if (budget <= 0) {
+        size_t fr = 0, tot = 0;
+        HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        budget = 0.9 * ((double)fr + (double)c.ws.held());
+    }
+    // single pass: KA + KB over every window, then the real edges, rc and dummy buffers
+    if ((double)npos * per_key * 2.5 <= budget && !c.disk) return 1;
+    const double keys = (double)npos * (canonical ? 2.0 : 1.0);
+    uint32_t P = (uint32_t)std::ceil(keys * per_key * 2.0 / (0.4 * budget));
+    P = std::max<uint32_t>(P, (uint32_t)std::ceil(keys / 2.0e9));  // <= 2e9 keys per range
+    return std::min<uint32_t>(std::max<uint32_t>(P, 2), 4096);
+}
+
+template <int L2, bool COUNTED>
+static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                               uint32_t P, Key<L2> **real, uint32_t **realc) {
+    using K2 = Key<L2>;
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    c.timings.n_positions = npos;
+    const int strands = canonical ? STRAND_BOTH : STRAND_FWD;
+    const uint32_t rows = canonical ? 2 : 1;
+    const unsigned hbits = 2 * std::min(6u, K);
+    const uint64_t nh = 1ull << hbits;
+    constexpr int TILE = ExtractTraits<L2>::TILE;
+    const uint64_t tiles = ceil_div(npos, TILE);
+    std::vector<uint64_t> hist(nh, 0);
+    if (tiles) {
+        auto *dh = (unsigned long long *)c.ws.get(Workspace::XHIST, nh * 8);
+        HIP_CHECK(hipMemsetAsync(dh, 0, nh * 8, c.stream));
+        prefix_hist_kernel<L2><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, strands,
+                                                                                 hbits, dh);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(hist.data(), dh, nh * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+    uint64_t total = 0;
+    for (uint64_t v : hist) total += v;
+    const std::vector<uint64_t> bounds = balanced_bounds(hist.data(), nh, (int)P);
+    c.timings.n_batches = P;
+    uint64_t off = 0, cap = 0, nx = 0;
+    *real = nullptr;
+    *realc = nullptr;
+    for (uint32_t j = 0; j < P; ++j) {
+        const uint64_t lo = bounds[j], hi = bounds[j + 1];
+        uint64_t nj = 0;
+        for (uint64_t b = lo; b < hi; ++b) nj += hist[b];
+        if (!nj) continue;
+        K2 *ka = (K2 *)c.ws.get(Workspace::KA, nj * sizeof(K2));
+        K2 *kb = (K2 *)c.ws.get(Workspace::KB, nj * sizeof(K2));
+        uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nj * 4) : nullptr;
+        uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nj * 4) : nullptr;
+        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (rows * tiles + 1) * 4);
+        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (rows * tiles + 1) * 8);
+        extract_kernel<L2, COUNTED, true, true><<<dim3((unsigned)tiles, rows), dim3(256), 0, c.stream>>>(
+            in.seq, in.seq_len, K, strands, in.read_starts, in.read_counts, in.n_reads, cmax, nullptr, nullptr,
+            tcnt, nullptr, nullptr, 0, hbits, (uint32_t)lo, (uint32_t)hi);
+        HIP_CHECK(hipGetLastError());
+        uint32_t ep;
+        const uint64_t st = ceil_div(rows * tiles, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, rows * tiles, toff, desc, ep,
+                                                                          &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        const uint64_t N = read_u64(c, (const unsigned long long *)(toff + rows * tiles));
+        if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
+        extract_kernel<L2, COUNTED, false, true><<<dim3((unsigned)tiles, rows), dim3(256), 0, c.stream>>>(
+            in.seq, in.seq_len, K, strands, in.read_starts, in.read_counts, in.n_reads, cmax, ka, ca, nullptr,
+            toff, nullptr, 0, hbits, (uint32_t)lo, (uint32_t)hi);
+        HIP_CHECK(hipGetLastError());
+        nx += N;
+        // the range fills (hi - lo) / nh of the top-prefix space: plan the MSD depth as if its keys
+        // were spread over all of it
+        const double spread = (double)nh / (double)(hi - lo);
+        const double dup = estimate_dup<L2>(c, ka, N, 8.0) / spread;
+        c.track_partition = j == 0;  // the roofline's partition pass: the first range's first level
+        const uint64_t U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, dup);
+        c.track_partition = false;
+        if (off + U > cap) {
+            // first range: size the real edges from its distinct ratio (+25 %); later growth keeps
+            // what is already appended
+            const uint64_t want = off == 0 ? (uint64_t)((double)U / (double)N * (double)total * 1.25) + U
+                                           : (off + U) + (off + U) / 4;
+            cap = std::max(want, off + U);
+            *real = (K2 *)c.ws.get(Workspace::REAL, cap * sizeof(K2), off * sizeof(K2), c.stream);
+            if (COUNTED) *realc = (uint32_t *)c.ws.get(Workspace::REALC, cap * 4, off * 4, c.stream);
+        }
+        HIP_CHECK(hipMemcpyAsync(*real + off, ka, U * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+        if (COUNTED) HIP_CHECK(hipMemcpyAsync(*realc + off, ca, U * 4, hipMemcpyDeviceToDevice, c.stream));
+        off += U;
+    }
+    if (!*real) {
+        *real = (K2 *)c.ws.get(Workspace::REAL, sizeof(K2));
+        if (COUNTED) *realc = (uint32_t *)c.ws.get(Workspace::REALC, 4);
+    }
+    c.timings.n_extracted = nx / rows;  // valid windows (each emits one k-mer per strand)
+    return off;
+}
+
 // K4: the reverse complements of a sorted canonical set ka[0..U) (add_reverse_complements,
 // boss_chunk_construct.cpp:179-222), sorted on their own.  rc(x) of odd K is never x, so it is a
 // 1:1 map; even K drops the palindromes and doubles their counts (rc_augment_kernel).  `buf`
@@ -1109,21 +1235,32 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
+    const uint32_t P = plan_ranges<L2, COUNTED>(c, K, canonical, in);
+    uint64_t U = 0, R = 0;
+    int ev_extract, ev_sort, ev_unique;
+    if (P > 1) {
+        // ---- K1-K4 one key range at a time (both strands in canonical mode): the real edges
+        ev_extract = tm.mark();
+        R = U = collect_ranges<L2, COUNTED>(c, K, canonical, cmax, in, P, &ka, &ca);
+        ev_sort = ev_unique = tm.mark();
+        T.n_unique = U;
+    } else {
     if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
         N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
-    const int ev_extract = tm.mark();
+    ev_extract = tm.mark();
 
     // ---- K2 sort + K3 unique / saturating count merge (ka)
-    const uint64_t U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
-    const int ev_sort = tm.mark();
+    U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
+    ev_sort = tm.mark();
     T.n_unique = U;
     debug_check_sorted(c, "collected k-mers", ka, U);
-    const int ev_unique = tm.mark();
+    ev_unique = tm.mark();
 
     // ---- K4 reverse complements (CANONICAL_ONLY): rc(x) of the sorted canonical set is sorted
     // on its own (no duplicates) and merged with it
-    uint64_t R = U;
-    if (canonical && U) {
+    R = U;
+    }
+    if (canonical && U && P == 1) {
         K2 *rk;
         uint32_t *rkc;
         const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc);
@@ -1685,8 +1822,9 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         set_error("Error: trying to allocate too many bits per k-mer count");
         return nullptr;
     }
-    if ((p->filter_suffix && p->filter_suffix[0]) || p->container_type != MTG_CONTAINER_VECTOR) {
-        set_error("only the in-memory container without a suffix filter runs on the GPU path");
+    if ((p->filter_suffix && p->filter_suffix[0]) ||
+        (p->container_type != MTG_CONTAINER_VECTOR && p->container_type != MTG_CONTAINER_VECTOR_DISK)) {
+        set_error("a suffix filter or an unknown container does not run on the GPU path");
         return nullptr;
     }
     int ndev = 0;
@@ -1702,6 +1840,9 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
         load_knobs(c->ctx);
+        c->ctx.mem_budget = p->memory_preallocated;
+        // the disk container bounds memory: always collect in key ranges (boss_chunk_construct.cpp:664-933)
+        if (p->container_type == MTG_CONTAINER_VECTOR_DISK && !c->ctx.force_ranges) c->ctx.disk = true;
     } catch (const std::exception &e) {
         set_error(e.what());
         delete c;

@@ -65,10 +65,9 @@ def test_no_cpu_fallback_without_device():
         boss.IBOSSChunkConstructor.initialize(10)
 
 
-def test_disk_container_and_suffix_are_not_silently_accepted():
-    if boss.device_count() == 0:
-        pytest.skip("needs a device to get past device selection")
-    with pytest.raises(RuntimeError):
+def test_suffix_and_unknown_container_are_not_silently_accepted():
+    # the checks come before device selection, so they run without a GPU too
+    with pytest.raises(RuntimeError, match="suffix filter"):
         boss.IBOSSChunkConstructor.initialize(10, filter_suffix="A")
-    with pytest.raises(RuntimeError):
-        boss.IBOSSChunkConstructor.initialize(10, container_type=boss.CONTAINER_VECTOR_DISK)
+    with pytest.raises(RuntimeError, match="unknown container"):
+        boss.IBOSSChunkConstructor.initialize(10, container_type=7)
