@@ -37,17 +37,11 @@ __device__ __forceinline__ Key<L> plain_to_boss(const Key<L> &P, unsigned K, con
     return shl(P & low, 2) | shr(P, 2 * (K - 1));
 }
 
-// which k-mer of a window the extractor emits: the forward strand (BASIC), min(fwd, rc)
-// (CANONICAL_ONLY), or the reverse complement (with the forward one, the both-strands
-// extraction of the range-batched build)
-enum : int { STRAND_FWD = 0, STRAND_CANONICAL = 1, STRAND_RC = 2, STRAND_BOTH = 3 };
-
 /*
  * One thread's PPT consecutive windows starting at p0 (tile-relative code offset r0 in s_code):
  * slides the forward and reverse-complement plain words, skips windows with an invalid char
  * (drag_and_mark_segments, common/algorithms.hpp:50-67), canonicalises (fwd <= rc in BOSS
  * integer order, kmer_extractor.cpp:165-196) and clamps per-read counts (kmer_collector.cpp:92).
- * `canonical` is a STRAND_* (FWD / CANONICAL / RC).
  * Returns the valid mask; with KEYS = false only the mask (the counting passes).
  */
 template <int L, bool COUNTED, int PPT, bool KEYS>
@@ -84,11 +78,9 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
             if (last_bad < (int64_t)j) {
                 if (KEYS) {
                     Key<L> f = plain_to_boss(P, K, low);
-                    if (canonical == STRAND_CANONICAL) {
+                    if (canonical) {
                         Key<L> r = plain_to_boss(R, K, low);
                         if (r < f) f = r;
-                    } else if (canonical == STRAND_RC) {
-                        f = plain_to_boss(R, K, low);
                     }
                     kk[j] = f;
                     if (COUNTED) {
@@ -130,20 +122,15 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
  * full launch writes its tile's k-mers at that offset (block scan, staged in LDS, written
  * coalesced).  No inter-workgroup hand-off, so tiles need no dequeue counter.
  */
-template <int L, bool COUNTED, bool COUNT_ONLY, bool FILTER = false>
+template <int L, bool COUNTED, bool COUNT_ONLY>
 __global__ __launch_bounds__(256) void extract_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts,
     uint64_t n_reads, uint32_t cmax, Key<L> *__restrict__ out_keys,
     uint32_t *__restrict__ out_counts, uint32_t *__restrict__ tcnt,
-    const uint64_t *__restrict__ toff, uint32_t *__restrict__ hist, unsigned hist_bits,
-    unsigned fbits = 0, uint32_t flo = 0, uint32_t fhi = 0) {
+    const uint64_t *__restrict__ toff, uint32_t *__restrict__ hist, unsigned hist_bits) {
     // hist: when hist_bits > 0, counts of the top hist_bits (<= 9) bits of the 2K-bit keys
-    // written (the first MSD level's histogram, so the sort skips its own histogram pass).
-    // STRAND_BOTH: gridDim.y = 2, row 0 emits the forward k-mers and row 1 the reverse
-    // complements; tile t of row y is tcnt / toff entry y * gridDim.x + t.
-    // FILTER: only k-mers whose top fbits bits lie in [flo, fhi) (one key range of the
-    // range-batched build).
+    // written (the first MSD level's histogram, so the sort skips its own histogram pass)
     using T = ExtractTraits<L>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
     __shared__ uint8_t s_code[TILE + T::MAXK];
@@ -153,12 +140,11 @@ __global__ __launch_bounds__(256) void extract_kernel(
     __shared__ uint32_t s_hist[COUNT_ONLY ? 1 : 512];
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const int strand = canonical == STRAND_BOTH ? (blockIdx.y ? STRAND_RC : STRAND_FWD) : canonical;
+    const uint32_t tile = blockIdx.x;
     if (!COUNT_ONLY && hist_bits)
         for (uint32_t i = tid; i < (1u << hist_bits); i += BLOCK) s_hist[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t base = (uint64_t)tile * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
     for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
     __syncthreads();
@@ -166,15 +152,8 @@ __global__ __launch_bounds__(256) void extract_kernel(
     const uint64_t p0 = base + (uint64_t)tid * PPT;
     Key<L> kk[PPT];
     uint32_t cc[PPT];
-    uint32_t valid_mask = slide_windows<L, COUNTED, PPT, !COUNT_ONLY || FILTER>(
-        s_code, tid * PPT, p0, npos, K, strand, read_starts, read_counts, n_reads, cmax, kk, cc);
-    if (FILTER) {
-#pragma unroll
-        for (int j = 0; j < PPT; ++j) {
-            const uint32_t top = bits_at(kk[j], 2 * K - fbits, fbits);
-            if (top < flo || top >= fhi) valid_mask &= ~(1u << j);
-        }
-    }
+    const uint32_t valid_mask = slide_windows<L, COUNTED, PPT, !COUNT_ONLY>(
+        s_code, tid * PPT, p0, npos, K, canonical, read_starts, read_counts, n_reads, cmax, kk, cc);
     const uint32_t nvalid = __popc(valid_mask);
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nvalid, s_scan, &tile_total);
@@ -206,43 +185,6 @@ __global__ __launch_bounds__(256) void extract_kernel(
         for (uint32_t i = tid; i < (1u << hist_bits); i += BLOCK)
             if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
     }
-}
-
-/*
- * Histogram of the top `hbits` bits (<= 12) of every k-mer the extractor emits (both strands
- * with STRAND_BOTH), over the whole read buffer: the key ranges of the range-batched build are
- * balanced on it.  Counts flush from LDS into 64-bit global counters.
- */
-template <int L>
-__global__ __launch_bounds__(256) void prefix_hist_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
-                                                          unsigned K, int strands, unsigned hbits,
-                                                          unsigned long long *__restrict__ hist) {
-    using T = ExtractTraits<L>;
-    constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
-    __shared__ uint8_t s_code[TILE + T::MAXK];
-    __shared__ uint32_t s_hist[4096];
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < (1u << hbits); i += BLOCK) s_hist[i] = 0;
-    const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
-    const uint64_t span_end = min(seq_len, base + TILE + K - 1);
-    for (uint64_t i = base + tid; i < span_end; i += BLOCK) s_code[i - base] = encode_dna(seq[i]);
-    __syncthreads();
-    const uint64_t p0 = base + (uint64_t)tid * PPT;
-    Key<L> kk[PPT];
-    uint32_t cc[PPT];
-    const int nst = strands == STRAND_BOTH ? 2 : 1;
-    for (int y = 0; y < nst; ++y) {
-        const int strand = strands == STRAND_BOTH ? (y ? STRAND_RC : STRAND_FWD) : strands;
-        const uint32_t m = slide_windows<L, false, PPT, true>(s_code, tid * PPT, p0, npos, K, strand, nullptr,
-                                                               nullptr, 0, 0, kk, cc);
-#pragma unroll
-        for (int j = 0; j < PPT; ++j)
-            if ((m >> j) & 1u) atomicAdd(&s_hist[bits_at(kk[j], 2 * K - hbits, hbits)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < (1u << hbits); i += BLOCK)
-        if (s_hist[i]) atomicAdd(&hist[i], (unsigned long long)s_hist[i]);
 }
 
 /*

@@ -24,6 +24,7 @@
 #include "comm.hpp"
 #include "dist_kernels.hpp"
 #include "extract_partition.hpp"
+#include "range_extract.hpp"
 #include "host_stage.hpp"
 #include "kmc.hpp"
 #include "msd_sort.hpp"
@@ -53,7 +54,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR,
-        LAST_BITS, DPOS, DWL, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -873,6 +874,7 @@ static std::vector<uint64_t> balanced_bounds(const uint64_t *hist, uint64_t nb, 
 template <int L2, bool COUNTED>
 static uint32_t plan_ranges(Ctx &c, unsigned K, bool canonical, const BuildInput &in) {
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    if (K < RB_CHARS + 1) return 1;  // at most 4^4 distinct k-mers: never worth a range
     if (c.force_ranges) return c.force_ranges;
     const double per_key = (double)sizeof(Key<L2>) + (COUNTED ? 4.0 : 0.0);
     double budget = c.mem_budget;
@@ -886,7 +888,7 @@ static uint32_t plan_ranges(Ctx &c, unsigned K, bool canonical, const BuildInput
     const double keys = (double)npos * (canonical ? 2.0 : 1.0);
     uint32_t P = (uint32_t)std::ceil(keys * per_key * 2.0 / (0.4 * budget));
     P = std::max<uint32_t>(P, (uint32_t)std::ceil(keys / 2.0e9));  // <= 2e9 keys per range
-    return std::min<uint32_t>(std::max<uint32_t>(P, 2), 4096);
+    return std::min<uint32_t>(std::max<uint32_t>(P, 2), RB_BINS);
 }
 
 template <int L2, bool COUNTED>
@@ -895,61 +897,60 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
     using K2 = Key<L2>;
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     c.timings.n_positions = npos;
-    const int strands = canonical ? STRAND_BOTH : STRAND_FWD;
-    const uint32_t rows = canonical ? 2 : 1;
-    const unsigned hbits = 2 * std::min(6u, K);
-    const uint64_t nh = 1ull << hbits;
-    constexpr int TILE = ExtractTraits<L2>::TILE;
+    const int both = canonical ? 1 : 0;
+    constexpr int TILE = RangeTraits<L2>::TILE;
     const uint64_t tiles = ceil_div(npos, TILE);
-    std::vector<uint64_t> hist(nh, 0);
+    // count pass: per-tile counts of the 4^RB_CHARS top-char bins, and their column sums
+    std::vector<uint64_t> hist(RB_BINS, 0);
+    uint16_t *tbins = (uint16_t *)c.ws.get(Workspace::RANGE_BINS, std::max<uint64_t>(tiles, 1) * RB_BINS * 2);
     if (tiles) {
-        auto *dh = (unsigned long long *)c.ws.get(Workspace::XHIST, nh * 8);
-        HIP_CHECK(hipMemsetAsync(dh, 0, nh * 8, c.stream));
-        prefix_hist_kernel<L2><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, strands,
-                                                                                 hbits, dh);
+        auto *dh = (unsigned long long *)c.ws.get(Workspace::XHIST, RB_BINS * 8);
+        HIP_CHECK(hipMemsetAsync(dh, 0, RB_BINS * 8, c.stream));
+        range_count_kernel<L2><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, both, tbins);
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipMemcpyAsync(hist.data(), dh, nh * 8, hipMemcpyDeviceToHost, c.stream));
+        range_bins_reduce_kernel<<<dim3((unsigned)std::min<uint64_t>(tiles, 2048)), dim3(RB_BINS), 0, c.stream>>>(
+            tbins, tiles, dh);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(hist.data(), dh, RB_BINS * 8, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
     }
     uint64_t total = 0;
     for (uint64_t v : hist) total += v;
-    const std::vector<uint64_t> bounds = balanced_bounds(hist.data(), nh, (int)P);
+    P = std::min<uint32_t>(P, RB_BINS);
+    const std::vector<uint64_t> bounds = balanced_bounds(hist.data(), RB_BINS, (int)P);
     c.timings.n_batches = P;
-    uint64_t off = 0, cap = 0, nx = 0;
+    uint64_t off = 0, cap = 0;
     *real = nullptr;
     *realc = nullptr;
+    uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
+    uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
     for (uint32_t j = 0; j < P; ++j) {
-        const uint64_t lo = bounds[j], hi = bounds[j + 1];
+        const uint32_t lo = (uint32_t)bounds[j], hi = (uint32_t)bounds[j + 1];
         uint64_t nj = 0;
-        for (uint64_t b = lo; b < hi; ++b) nj += hist[b];
+        for (uint32_t b = lo; b < hi; ++b) nj += hist[b];
         if (!nj) continue;
         K2 *ka = (K2 *)c.ws.get(Workspace::KA, nj * sizeof(K2));
         K2 *kb = (K2 *)c.ws.get(Workspace::KB, nj * sizeof(K2));
         uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nj * 4) : nullptr;
         uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nj * 4) : nullptr;
-        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (rows * tiles + 1) * 4);
-        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (rows * tiles + 1) * 8);
-        extract_kernel<L2, COUNTED, true, true><<<dim3((unsigned)tiles, rows), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, strands, in.read_starts, in.read_counts, in.n_reads, cmax, nullptr, nullptr,
-            tcnt, nullptr, nullptr, 0, hbits, (uint32_t)lo, (uint32_t)hi);
+        range_tile_counts_kernel<<<dim3((unsigned)ceil_div(tiles, 256)), dim3(256), 0, c.stream>>>(tbins, tiles, lo,
+                                                                                                   hi, tcnt);
         HIP_CHECK(hipGetLastError());
         uint32_t ep;
-        const uint64_t st = ceil_div(rows * tiles, 4096);
+        const uint64_t st = ceil_div(tiles, 4096);
         uint64_t *desc = acquire_desc(c, st, &ep);
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, rows * tiles, toff, desc, ep,
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, tiles, toff, desc, ep,
                                                                           &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
-        const uint64_t N = read_u64(c, (const unsigned long long *)(toff + rows * tiles));
-        if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
-        extract_kernel<L2, COUNTED, false, true><<<dim3((unsigned)tiles, rows), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, strands, in.read_starts, in.read_counts, in.n_reads, cmax, ka, ca, nullptr,
-            toff, nullptr, 0, hbits, (uint32_t)lo, (uint32_t)hi);
+        range_write_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+            in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, cmax, lo, hi, toff, ka, ca);
         HIP_CHECK(hipGetLastError());
-        nx += N;
-        // the range fills (hi - lo) / nh of the top-prefix space: plan the MSD depth as if its keys
-        // were spread over all of it
-        const double spread = (double)nh / (double)(hi - lo);
+        const uint64_t N = read_u64(c, (const unsigned long long *)(toff + tiles));
+        if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
+        // the range fills (hi - lo) / RB_BINS of the top-char space: plan the MSD depth as if its
+        // keys were spread over all of it
+        const double spread = (double)RB_BINS / (double)(hi - lo);
         const double dup = estimate_dup<L2>(c, ka, N, 8.0) / spread;
         c.track_partition = j == 0;  // the roofline's partition pass: the first range's first level
         const uint64_t U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, dup);
@@ -971,7 +972,7 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
         *real = (K2 *)c.ws.get(Workspace::REAL, sizeof(K2));
         if (COUNTED) *realc = (uint32_t *)c.ws.get(Workspace::REALC, 4);
     }
-    c.timings.n_extracted = nx / rows;  // valid windows (each emits one k-mer per strand)
+    c.timings.n_extracted = total / (canonical ? 2 : 1);  // valid windows (one k-mer per strand each)
     return off;
 }
 
