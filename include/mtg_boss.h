@@ -200,6 +200,36 @@ int mtg_boss_build_device_dist(mtg_boss_ctor *ctor, mtg_comm *comm, const uint8_
 /* the range split: bounds[0..world] over n_prefixes buckets, balanced on hist (host) */
 int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64_t *bounds);
 
+/*
+ * The graph files `metagraph build` writes from a chunk (cli/build.cpp:323-352; DBGSuccinct::serialize,
+ * dbg_succinct.cpp:754-790): <outbase>.dbg (BOSS F / k / state, W, last, the graph mode, the
+ * suffix-range index), <outbase>.edgemask with mask_dummy (--mask-dummy: the valid edges of
+ * mark_all_dummy_edges, dbg_succinct.cpp:839-870), <outbase>.dbg.weights when the chunk has
+ * weights (node_weights.cpp:62-68).  graph_mode: 0 basic, 1 canonical.  suffix_length < 0 = the
+ * build's default min(10, k).  *n_valid (may be NULL) = edges left valid by the mask (`nodes (k)` of
+ * `metagraph stats`), else n - 1.  Host code: needs no device.  The sdsl-lite containers inside are
+ * restated (their bytes are unpinned); mtg_boss_read_dbg reads exactly this layout.
+ */
+int mtg_boss_write_dbg(const mtg_boss_chunk *chunk, const char *outbase, int graph_mode, int mask_dummy,
+                       int64_t suffix_length, uint64_t *n_valid);
+
+typedef struct mtg_dbg_file {
+    uint64_t k;
+    uint64_t n;                  /* rows incl. row 0 */
+    uint64_t F[5];
+    uint64_t state;              /* 3 = STAT */
+    uint64_t mode;               /* 0 basic, 1 canonical */
+    uint64_t suffix_length;
+    uint64_t n_ranges;           /* 4^suffix_length */
+    uint8_t *W;                  /* n labels */
+    uint64_t *last;              /* n bits, packed */
+    uint64_t *ranges;            /* 2 * n_ranges: first and last edge of each indexed suffix */
+    uint64_t *valid;             /* packed .edgemask bits, NULL when there is none */
+    uint64_t n_valid;
+} mtg_dbg_file;
+int mtg_boss_read_dbg(const char *outbase, mtg_dbg_file *out);
+void mtg_dbg_file_free(mtg_dbg_file *file);
+
 /* encode table of the extractor (kmer/alphabets.hpp:127-143) evaluated by the device function on
    the host: out[c] in {0, 1, 2, 3, 4 = invalid} for every byte c (256 entries) */
 void mtg_dna_encode_table(uint8_t *out);

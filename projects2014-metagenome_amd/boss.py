@@ -46,6 +46,15 @@ class _DeviceChunk(ctypes.Structure):
                 ("n_dummy", ctypes.c_uint64)]
 
 
+class _DbgFile(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_uint64) for name in ("k", "n")] + \
+               [("F", ctypes.c_uint64 * 5)] + \
+               [(name, ctypes.c_uint64) for name in ("state", "mode", "suffix_length", "n_ranges")] + \
+               [("W", ctypes.POINTER(ctypes.c_uint8)), ("last", ctypes.POINTER(ctypes.c_uint64)),
+                ("ranges", ctypes.POINTER(ctypes.c_uint64)), ("valid", ctypes.POINTER(ctypes.c_uint64)),
+                ("n_valid", ctypes.c_uint64)]
+
+
 class Timings(ctypes.Structure):
     _fields_ = [(name, ctypes.c_double) for name in
                 ("total_ms", "extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms",
@@ -72,7 +81,8 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_device_count", "mtg_device_synchronize", "mtg_comm_get_unique_id",
            "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
-           "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table")
+           "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
+           "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free")
 
 COMM_ID_BYTES = 128
 
@@ -134,6 +144,10 @@ def lib():
         L.mtg_dist_bounds.argtypes = [P(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_int,
                                       P(ctypes.c_uint64)]
         L.mtg_dna_encode_table.argtypes = [ctypes.c_char_p]
+        L.mtg_boss_write_dbg.argtypes = [P(_Chunk), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int64, P(ctypes.c_uint64)]
+        L.mtg_boss_read_dbg.argtypes = [ctypes.c_char_p, P(_DbgFile)]
+        L.mtg_dbg_file_free.argtypes = [P(_DbgFile)]
         for name in EXPORTS:
             getattr(L, name)
         _lib = L
@@ -175,6 +189,25 @@ class Chunk:
         if alph != 5:
             raise ValueError("ERROR: only the DNA alphabet of size 5 is supported")
         return cls(k, W, last, F, weights, bits_per_count=bits)
+
+    def write_dbg(self, outbase, canonical=False, mask_dummy=False, suffix_length=-1):
+        """The files `metagraph build` writes from this chunk (cli/build.cpp:323-352):
+        <outbase>.dbg, <outbase>.edgemask (mask_dummy) and <outbase>.dbg.weights (weighted).
+        Returns the valid edges after masking (`nodes (k)` of `metagraph stats`), else rows - 1."""
+        W = np.ascontiguousarray(self.W, dtype=np.uint8)
+        last = pack_last(self.last)
+        F = (ctypes.c_uint64 * 5)(*[int(f) for f in self.F])
+        c = _Chunk(k=self.k, alph_size=5, n=len(W), F=F, bits_per_count=self.bits_per_count or 0)
+        c.W = W.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        c.last = last.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        wts = None
+        if self.weights is not None and self.bits_per_count:
+            wts = np.ascontiguousarray(self.weights, dtype=np.uint32)
+            c.weights = wts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        nv = ctypes.c_uint64(0)
+        _check(lib().mtg_boss_write_dbg(ctypes.byref(c), os.fsencode(outbase), int(bool(canonical)),
+                                        int(bool(mask_dummy)), int(suffix_length), ctypes.byref(nv)))
+        return nv.value
 
     def extend(self, other):
         """BOSS::Chunk::extend (boss_chunk.cpp:230-270): append rows after index 0, sum F."""
@@ -397,6 +430,28 @@ def concatenate_files(chunk_filenames):
         else:
             full.extend(ch)
     return full
+
+
+class DbgFile:
+    """A `.dbg` (+ `.edgemask`) as mtg_boss_read_dbg parses it: k, F, state, mode, W, last,
+    the suffix-range index (n_ranges x 2: first and last edge) and the valid-edge mask."""
+
+    def __init__(self, outbase):
+        f = _DbgFile()
+        _check(lib().mtg_boss_read_dbg(os.fsencode(outbase), ctypes.byref(f)))
+        try:
+            self.k, self.n, self.state, self.mode = f.k, f.n, f.state, f.mode
+            self.F = np.array(list(f.F), dtype=np.uint64)
+            self.suffix_length = f.suffix_length
+            self.W = np.ctypeslib.as_array(f.W, shape=(f.n,)).copy()
+            self.last = unpack_last(np.ctypeslib.as_array(f.last, shape=((f.n + 63) // 64,)), f.n)
+            self.ranges = (np.ctypeslib.as_array(f.ranges, shape=(2 * f.n_ranges,)).reshape(-1, 2).copy()
+                           if f.n_ranges else np.zeros((0, 2), dtype=np.uint64))
+            self.valid = (unpack_last(np.ctypeslib.as_array(f.valid, shape=((f.n + 63) // 64,)), f.n)
+                          if f.valid else None)
+            self.n_valid = f.n_valid
+        finally:
+            lib().mtg_dbg_file_free(ctypes.byref(f))
 
 
 def unpack_last(words, n):

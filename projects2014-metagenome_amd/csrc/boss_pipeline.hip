@@ -22,6 +22,7 @@
 #include "../../include/mtg_boss.h"
 #include "boss_kernels.hpp"
 #include "comm.hpp"
+#include "dbg_io.hpp"
 #include "dist_kernels.hpp"
 #include "extract_partition.hpp"
 #include "range_extract.hpp"
@@ -2177,6 +2178,70 @@ void mtg_boss_chunk_free(mtg_boss_chunk *chunk) {
     chunk->last = nullptr;
     chunk->weights = nullptr;
     chunk->n = 0;
+}
+
+int mtg_boss_write_dbg(const mtg_boss_chunk *chunk, const char *outbase, int graph_mode, int mask_dummy,
+                       int64_t suffix_length, uint64_t *n_valid) {
+    if (!chunk || !outbase || !chunk->W || !chunk->last || chunk->n < 1 || graph_mode < 0 || graph_mode > 1) {
+        set_error("write_dbg: bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    try {
+        const uint64_t v = dbgio::write_dbg(outbase, chunk->W, chunk->last, chunk->n, chunk->F, chunk->k,
+                                            (uint64_t)graph_mode, mask_dummy != 0, suffix_length, chunk->weights,
+                                            chunk->bits_per_count);
+        if (n_valid) *n_valid = v;
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_ARGUMENT;
+    }
+}
+
+int mtg_boss_read_dbg(const char *outbase, mtg_dbg_file *out) {
+    if (!outbase || !out) return MTG_ERR_ARGUMENT;
+    std::memset(out, 0, sizeof(*out));
+    try {
+        dbgio::DbgFile f = dbgio::read_dbg(outbase);
+        out->k = f.k;
+        out->n = f.n;
+        for (int c = 0; c < 5; ++c) out->F[c] = f.F[c];
+        out->state = f.state;
+        out->mode = f.mode;
+        out->suffix_length = f.suffix_length;
+        out->n_ranges = f.ranges.size();
+        out->W = (uint8_t *)std::malloc(std::max<size_t>(f.W.size(), 1));
+        std::memcpy(out->W, f.W.data(), f.W.size());
+        out->last = (uint64_t *)std::malloc(std::max<size_t>(f.last.size() * 8, 8));
+        std::memcpy(out->last, f.last.data(), f.last.size() * 8);
+        out->ranges = (uint64_t *)std::malloc(std::max<size_t>(f.ranges.size() * 16, 16));
+        for (size_t i = 0; i < f.ranges.size(); ++i) {
+            out->ranges[2 * i] = f.ranges[i].first;
+            out->ranges[2 * i + 1] = f.ranges[i].second;
+        }
+        if (f.has_mask) {
+            out->valid = (uint64_t *)std::malloc(std::max<size_t>(f.valid.size() * 8, 8));
+            std::memcpy(out->valid, f.valid.data(), f.valid.size() * 8);
+            for (uint64_t x : f.valid) out->n_valid += __builtin_popcountll(x);
+        }
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        mtg_dbg_file_free(out);
+        return MTG_ERR_ARGUMENT;
+    }
+}
+
+void mtg_dbg_file_free(mtg_dbg_file *f) {
+    if (!f) return;
+    std::free(f->W);
+    std::free(f->last);
+    std::free(f->ranges);
+    std::free(f->valid);
+    f->W = nullptr;
+    f->last = nullptr;
+    f->ranges = nullptr;
+    f->valid = nullptr;
 }
 
 void mtg_dna_encode_table(uint8_t *out) {

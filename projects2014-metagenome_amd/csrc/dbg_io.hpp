@@ -1,0 +1,567 @@
+// dbg_io.hpp -- the graph files `metagraph build` writes after construction (host code):
+//   <base>.dbg          DBGSuccinct::serialize (dbg_succinct.cpp:754-770): BOSS::serialize
+//                       (boss.cpp:245-262: F, k, state, W, last), the graph mode, the suffix-range
+//                       index (boss.cpp:330-337, built as index_suffix_ranges, :3091-3161);
+//   <base>.edgemask     the valid-edge mask of --mask-dummy (dbg_succinct.cpp:839-870:
+//                       mark_all_dummy_edges flipped, boss.cpp:1681-1691);
+//   <base>.dbg.weights  the chunk's weight vector (node_weights.cpp:55-68 renames the chunk's
+//                       weights buffer), written by chunk_io.py in the int_vector layout.
+// The BOSS navigation the index and the mask need (rank_W, rank_last, select_last, fwd,
+// tighten_range: boss.hpp:655-666, boss.cpp:381-385, 521-536, 586-597) runs on the chunk arrays.
+//
+// Byte layout.  The reference's own framing is exact: numbers are serialize_number (8-byte
+// big-endian, common/serialization.cpp:38-46), F is serialize_number_vector_raw (count + values,
+// :84-90), the suffix index is a raw native-endian pair<u64,u64> array.  The sdsl-lite containers
+// (wt_huff<> for W, bit_vector_stat = bit_vector + rank_support_v5 + select_support_mcl +
+// select_support_scan for last, bit_vector_small for the mask) are RESTATED, not reproduced:
+// sdsl-lite is an empty submodule in the reference snapshot and no .dbg file exists in its tests,
+// so their bytes are unpinned.  The restatement keeps sdsl's int_vector framing (u64 size in bits,
+// u8 width for width-0 vectors, u64 words) for every bit/int vector and writes each auxiliary
+// structure as documented below; read_dbg parses exactly this layout back.
+#pragma once
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <queue>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace mtg {
+namespace dbgio {
+
+// ---------------------------------------------------------------------------------- framing
+
+inline void put_be(std::ostream &o, uint64_t v) {  // serialize_number
+    uint8_t b[8];
+    for (int i = 0; i < 8; ++i) b[i] = (uint8_t)(v >> (56 - 8 * i));
+    o.write((const char *)b, 8);
+}
+inline uint64_t get_be(std::istream &in) {
+    uint8_t b[8];
+    if (!in.read((char *)b, 8)) throw std::runtime_error("truncated .dbg file");
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = v << 8 | b[i];
+    return v;
+}
+template <typename T>
+inline void put_raw(std::ostream &o, const T &v) { o.write((const char *)&v, sizeof(T)); }
+template <typename T>
+inline T get_raw(std::istream &in) {
+    T v;
+    if (!in.read((char *)&v, sizeof(T))) throw std::runtime_error("truncated .dbg file");
+    return v;
+}
+
+// sdsl int_vector framing: u64 size in bits, [u8 width when the width is a run-time value], then
+// ceil(bits / 64) u64 words
+inline void put_bits(std::ostream &o, const std::vector<uint64_t> &words, uint64_t nbits, int width = -1) {
+    put_raw<uint64_t>(o, nbits);
+    if (width >= 0) put_raw<uint8_t>(o, (uint8_t)width);
+    o.write((const char *)words.data(), (std::streamsize)(((nbits + 63) / 64) * 8));
+}
+inline std::vector<uint64_t> get_bits(std::istream &in, uint64_t *nbits, bool has_width = false, int *width = nullptr) {
+    *nbits = get_raw<uint64_t>(in);
+    if (has_width) {
+        const uint8_t w = get_raw<uint8_t>(in);
+        if (width) *width = w;
+    }
+    std::vector<uint64_t> words((*nbits + 63) / 64);
+    if (!words.empty() && !in.read((char *)words.data(), (std::streamsize)(words.size() * 8)))
+        throw std::runtime_error("truncated .dbg file");
+    return words;
+}
+inline void put_u64s(std::ostream &o, const std::vector<uint64_t> &v) {  // int_vector<64>
+    put_bits(o, v, 64 * (uint64_t)v.size());
+}
+inline std::vector<uint64_t> get_u64s(std::istream &in) {
+    uint64_t nb;
+    return get_bits(in, &nb);
+}
+
+inline bool bit(const uint64_t *w, uint64_t i) { return (w[i >> 6] >> (i & 63)) & 1; }
+
+// ---------------------------------------------------------------- rank / select supports
+
+// cumulative ones before every 2048-bit superblock (rank_support_v5's block size), plus the end
+struct RankSupport {
+    std::vector<uint64_t> super;
+    void build(const uint64_t *w, uint64_t nbits) {
+        const uint64_t nw = (nbits + 63) / 64;
+        super.assign(nw / 32 + 2, 0);
+        uint64_t c = 0;
+        for (uint64_t i = 0; i < nw; ++i) {
+            if (i % 32 == 0) super[i / 32] = c;
+            c += __builtin_popcountll(w[i]);
+        }
+        super[nw / 32 + 1] = c;
+        if (nw % 32 == 0) super[nw / 32] = c;
+    }
+};
+
+// position of every 4096-th one (select_support_mcl's superblock sampling), as int_vector<64>
+inline std::vector<uint64_t> select_samples(const uint64_t *w, uint64_t nbits, bool ones) {
+    std::vector<uint64_t> s;
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < nbits; ++i) {
+        if (bit(w, i) == ones) {
+            if (c % 4096 == 0) s.push_back(i);
+            ++c;
+        }
+    }
+    return s;
+}
+
+// bit_vector_stat (bit_vector_sdsl.hpp:270-277): bit_vector, num_set_bits (BE), then the
+// restated supports: rank (int_vector<64> superblock counts), select-1 (u64 count + int_vector<64>
+// samples); select_support_scan<0> stores nothing
+inline void put_bit_vector_stat(std::ostream &o, const std::vector<uint64_t> &w, uint64_t nbits) {
+    put_bits(o, w, nbits);
+    uint64_t ones = 0;
+    for (uint64_t x : w) ones += __builtin_popcountll(x);
+    put_be(o, ones);
+    RankSupport r;
+    r.build(w.data(), nbits);
+    put_u64s(o, r.super);
+    put_raw<uint64_t>(o, ones);
+    put_u64s(o, select_samples(w.data(), nbits, true));
+}
+inline std::vector<uint64_t> get_bit_vector_stat(std::istream &in, uint64_t *nbits) {
+    std::vector<uint64_t> w = get_bits(in, nbits);
+    const uint64_t ones = get_be(in);
+    uint64_t c = 0;
+    for (uint64_t x : w) c += __builtin_popcountll(x);
+    if (c != ones) throw std::runtime_error("bit_vector_stat: set-bit count mismatch");
+    get_u64s(in);
+    if (get_raw<uint64_t>(in) != ones) throw std::runtime_error("bit_vector_stat: select support mismatch");
+    get_u64s(in);
+    return w;
+}
+
+// --------------------------------------------------------------------------- W: wt_huff<>
+
+// Huffman-shaped wavelet tree over the W symbols (sdsl wt_pc<huff_shape>): node 0 the root, nodes
+// numbered breadth first; the concatenated bit vector holds each inner node's bits (0 = left
+// child) in node order, each in text order.  Layout: u64 size, u64 sigma, bit_vector, rank
+// support (as above), select-1 and select-0 supports (u64 count + int_vector<64> samples each),
+// then the tree: u64 node count, per node (u64 bv_pos, u64 bv_pos_rank, u16 parent, u16 child[2],
+// 0xFFFF = none), u16 symbol -> leaf[256], u64 symbol -> path[256] (code length << 56 | code bits,
+// root bit first).  Followed by the BE logsigma of wavelet_tree_sdsl (wavelet_tree.cpp:365-368).
+struct HuffTree {
+    struct Node {
+        uint64_t bv_pos = 0, bv_pos_rank = 0, count = 0;
+        uint16_t parent = 0xFFFF, child[2] = {0xFFFF, 0xFFFF};
+        int symbol = -1;
+    };
+    std::vector<Node> nodes;
+    uint16_t leaf[256];
+    uint64_t path[256];
+};
+
+inline HuffTree huff_build(const uint64_t freq[256]) {
+    // deterministic Huffman: repeatedly join the two lightest trees (ties: smaller id first)
+    struct T {
+        uint64_t f;
+        int id;
+    };
+    auto cmp = [](const T &a, const T &b) { return a.f != b.f ? a.f > b.f : a.id > b.id; };
+    std::priority_queue<T, std::vector<T>, decltype(cmp)> pq(cmp);
+    std::vector<std::pair<int, int>> kids;  // tree id >= 256: (left, right)
+    std::vector<uint64_t> tf;
+    for (int s = 0; s < 256; ++s)
+        if (freq[s]) pq.push({freq[s], s});
+    int next = 256;
+    while (pq.size() > 1) {
+        T a = pq.top();
+        pq.pop();
+        T b = pq.top();
+        pq.pop();
+        kids.push_back({a.id, b.id});
+        pq.push({a.f + b.f, next++});
+    }
+    HuffTree h;
+    std::fill(h.leaf, h.leaf + 256, (uint16_t)0xFFFF);
+    std::fill(h.path, h.path + 256, 0ull);
+    if (pq.empty()) return h;
+    // breadth-first numbering from the root
+    std::vector<std::pair<int, uint64_t>> q{{pq.top().id, 0}};  // (tree id, code << 8 | len)
+    std::vector<int> parent_of{-1};
+    for (size_t i = 0; i < q.size(); ++i) {
+        const int id = q[i].first;
+        HuffTree::Node n;
+        if (parent_of[i] >= 0) n.parent = (uint16_t)parent_of[i];
+        if (id < 256) {
+            n.symbol = id;
+            const uint64_t code = q[i].second >> 8, len = q[i].second & 0xFF;
+            h.leaf[id] = (uint16_t)i;
+            h.path[id] = len << 56 | code;
+        } else {
+            const auto &kv = kids[id - 256];
+            const uint64_t code = q[i].second >> 8, len = q[i].second & 0xFF;
+            for (int c = 0; c < 2; ++c) {
+                n.child[c] = (uint16_t)q.size();
+                q.push_back({c ? kv.second : kv.first, ((code | (uint64_t)c << len) << 8) | (len + 1)});
+                parent_of.push_back((int)i);
+            }
+        }
+        h.nodes.push_back(n);
+    }
+    if (h.nodes.size() == 1) {  // one symbol: a leaf root, no bits
+        h.path[h.nodes[0].symbol] = 0;
+    }
+    return h;
+}
+
+inline void put_wt_huff(std::ostream &o, const uint8_t *W, uint64_t n) {
+    uint64_t freq[256] = {0};
+    for (uint64_t i = 0; i < n; ++i) ++freq[W[i]];
+    HuffTree h = huff_build(freq);
+    uint64_t sigma = 0;
+    for (int s = 0; s < 256; ++s) sigma += freq[s] != 0;
+    // bits per inner node = symbols passing through it; positions in node order
+    for (int s = 0; s < 256; ++s) {
+        if (!freq[s]) continue;
+        for (int v = h.nodes[h.leaf[s]].parent; v != 0xFFFF; v = h.nodes[v].parent) h.nodes[v].count += freq[s];
+    }
+    uint64_t total = 0;
+    for (auto &v : h.nodes) {
+        v.bv_pos = total;
+        total += v.symbol < 0 ? v.count : 0;
+    }
+    std::vector<uint64_t> bv((total + 63) / 64, 0);
+    std::vector<uint64_t> cur(h.nodes.size(), 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t p = h.path[W[i]], len = p >> 56;
+        uint16_t v = 0;
+        for (uint64_t d = 0; d < len; ++d) {
+            const uint64_t b = (p >> d) & 1, pos = h.nodes[v].bv_pos + cur[v]++;
+            if (b) bv[pos >> 6] |= 1ull << (pos & 63);
+            v = h.nodes[v].child[b];
+        }
+    }
+    RankSupport r;
+    r.build(bv.data(), total);
+    uint64_t ones = 0;
+    for (uint64_t x : bv) ones += __builtin_popcountll(x);
+    for (auto &v : h.nodes) {  // ones before each node's bits
+        const uint64_t w = v.bv_pos >> 6, b = v.bv_pos & 63;
+        uint64_t c = r.super[w / 32];
+        for (uint64_t q = w / 32 * 32; q < w; ++q) c += __builtin_popcountll(bv[q]);
+        if (b) c += __builtin_popcountll(bv[w] & ((1ull << b) - 1));
+        v.bv_pos_rank = c;
+    }
+    put_raw<uint64_t>(o, n);
+    put_raw<uint64_t>(o, sigma);
+    put_bits(o, bv, total);
+    put_u64s(o, r.super);
+    put_raw<uint64_t>(o, ones);
+    put_u64s(o, select_samples(bv.data(), total, true));
+    put_raw<uint64_t>(o, total - ones);
+    put_u64s(o, select_samples(bv.data(), total, false));
+    put_raw<uint64_t>(o, (uint64_t)h.nodes.size());
+    for (const auto &v : h.nodes) {
+        put_raw<uint64_t>(o, v.bv_pos);
+        put_raw<uint64_t>(o, v.bv_pos_rank);
+        put_raw<uint16_t>(o, v.parent);
+        put_raw<uint16_t>(o, v.child[0]);
+        put_raw<uint16_t>(o, v.child[1]);
+    }
+    o.write((const char *)h.leaf, sizeof(h.leaf));
+    o.write((const char *)h.path, sizeof(h.path));
+}
+
+inline std::vector<uint8_t> get_wt_huff(std::istream &in) {
+    const uint64_t n = get_raw<uint64_t>(in);
+    get_raw<uint64_t>(in);  // sigma
+    uint64_t total;
+    const std::vector<uint64_t> bv = get_bits(in, &total);
+    get_u64s(in);
+    get_raw<uint64_t>(in);
+    get_u64s(in);
+    get_raw<uint64_t>(in);
+    get_u64s(in);
+    const uint64_t nn = get_raw<uint64_t>(in);
+    if (nn > 511) throw std::runtime_error("wt_huff: bad tree");
+    std::vector<HuffTree::Node> nodes(nn);
+    for (auto &v : nodes) {
+        v.bv_pos = get_raw<uint64_t>(in);
+        v.bv_pos_rank = get_raw<uint64_t>(in);
+        v.parent = get_raw<uint16_t>(in);
+        v.child[0] = get_raw<uint16_t>(in);
+        v.child[1] = get_raw<uint16_t>(in);
+    }
+    uint16_t leaf[256];
+    uint64_t path[256];
+    if (!in.read((char *)leaf, sizeof(leaf)) || !in.read((char *)path, sizeof(path)))
+        throw std::runtime_error("truncated .dbg file");
+    std::vector<int> sym(nn, -1);
+    for (int s = 0; s < 256; ++s)
+        if (leaf[s] != 0xFFFF && leaf[s] < nn) sym[leaf[s]] = s;
+    std::vector<uint8_t> W(n);
+    std::vector<uint64_t> cur(nn, 0);
+    for (uint64_t i = 0; i < n; ++i) {  // walk root -> leaf with one cursor per inner node
+        uint16_t v = 0;
+        while (nn && nodes[v].child[0] != 0xFFFF) {
+            const uint64_t pos = nodes[v].bv_pos + cur[v]++;
+            if (pos >= total) throw std::runtime_error("wt_huff: bits out of range");
+            v = nodes[v].child[bit(bv.data(), pos)];
+        }
+        if (!nn || sym[v] < 0) throw std::runtime_error("wt_huff: leaf without symbol");
+        W[i] = (uint8_t)sym[v];
+    }
+    return W;
+}
+
+// ----------------------------------------------------------------------- BOSS navigation
+
+struct BossNav {
+    const uint8_t *W;
+    const uint64_t *last;
+    uint64_t n;  // rows incl. row 0
+    uint64_t F[5];
+    uint64_t k;
+    uint64_t NF[5];
+    std::vector<uint64_t> last_rank;     // ones in last before word w
+    std::vector<uint64_t> wrank[5];      // W == c (exact, no minus) before each 64-row block
+
+    BossNav(const uint8_t *W_, const uint64_t *last_, uint64_t n_, const uint64_t *F_, uint64_t k_)
+        : W(W_), last(last_), n(n_), k(k_) {
+        for (int c = 0; c < 5; ++c) F[c] = F_[c];
+        const uint64_t nw = (n + 63) / 64;
+        last_rank.assign(nw + 1, 0);
+        for (uint64_t i = 0; i < nw; ++i) last_rank[i + 1] = last_rank[i] + __builtin_popcountll(last[i]);
+        for (int c = 0; c < 5; ++c) wrank[c].assign(nw + 1, 0);
+        for (uint64_t b = 0; b < nw; ++b) {
+            uint64_t cnt[5] = {0, 0, 0, 0, 0};
+            for (uint64_t i = 64 * b; i < std::min(n, 64 * b + 64); ++i)
+                if (W[i] < 5) ++cnt[W[i]];
+            for (int c = 0; c < 5; ++c) wrank[c][b + 1] = wrank[c][b] + cnt[c];
+        }
+        for (int c = 0; c < 5; ++c) NF[c] = rank_last(F[c]);  // recompute_NF
+    }
+    // #{p in [1, i] : last[p]} (boss.cpp:521-525; last[0] = 0)
+    uint64_t rank_last(uint64_t i) const {
+        if (i == 0) return 0;
+        const uint64_t e = i + 1, w = e >> 6, b = e & 63;
+        return last_rank[w] + (b ? __builtin_popcountll(last[w] & ((1ull << b) - 1)) : 0);
+    }
+    // position of the j-th set bit of last (boss.cpp:532-536)
+    uint64_t select_last(uint64_t j) const {
+        if (j == 0) return 0;
+        uint64_t lo = 0, hi = last_rank.size() - 1;  // last word with last_rank[w] < j
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (last_rank[mid] < j) lo = mid; else hi = mid;
+        }
+        uint64_t x = last[lo], r = j - last_rank[lo];
+        for (uint64_t q = 1; q < r; ++q) x &= x - 1;
+        return 64 * lo + __builtin_ctzll(x);
+    }
+    // #{p in [1, i] : W[p] == c} (boss.cpp:381-385)
+    uint64_t rank_W(uint64_t i, uint8_t c) const {
+        if (i == 0) return 0;
+        const uint64_t e = i + 1, b = e >> 6;
+        uint64_t r = wrank[c][b];
+        for (uint64_t p = 64 * b; p < e; ++p) r += W[p] == c;
+        return r - (c == 0 ? 1 : 0);
+    }
+    // boss.hpp:655-666
+    bool tighten_range(uint64_t *rl, uint64_t *ru, uint8_t s) const {
+        const uint64_t rk_rl = rank_W(*rl - 1, s) + 1;
+        const uint64_t rk_ru = rank_W(*ru, s);
+        if (rk_rl > rk_ru) return false;
+        *rl = select_last(NF[s] + rk_rl - 1) + 1;
+        *ru = select_last(NF[s] + rk_ru);
+        return true;
+    }
+    // boss.cpp:586-597
+    uint64_t fwd(uint64_t i, uint8_t c) const { return select_last(NF[c] + rank_W(i, c)); }
+};
+
+// BOSS::index_suffix_ranges (boss.cpp:3091-3161)
+inline std::vector<std::pair<uint64_t, uint64_t>> index_suffix_ranges(const BossNav &b, uint64_t L) {
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    if (L == 0) return out;
+    struct R {
+        uint64_t idx, rl, ru;
+    };
+    std::vector<R> ranges{{0, 1, b.n - 1}};
+    uint64_t num = 1;
+    for (uint64_t len = 1; len < L; ++len) {
+        std::vector<R> nx;
+        nx.reserve(ranges.size() * 4);
+        for (const R &r : ranges)
+            for (uint8_t c = 1; c < 5; ++c) {
+                uint64_t rl = r.rl, ru = r.ru;
+                if (!b.tighten_range(&rl, &ru, c)) continue;
+                nx.push_back({num * (c - 1) + r.idx, rl, ru});
+            }
+        ranges.swap(nx);
+        num *= 4;
+    }
+    out.assign(num * 4, {b.n, 0});
+    for (const R &r : ranges)
+        for (uint8_t c = 1; c < 5; ++c) {
+            uint64_t rl = r.rl, ru = r.ru;
+            if (!b.tighten_range(&rl, &ru, c)) continue;
+            out[num * (c - 1) + r.idx] = {rl, ru};
+        }
+    for (size_t i = 1; i < out.size(); ++i)
+        if (!out[i].second) {
+            out[i].second = out[i - 1].second;
+            out[i].first = out[i - 1].second + 1;
+        }
+    return out;
+}
+
+// mark_all_dummy_edges (boss.cpp:1681-1691): the source-dummy tree from the main dummy node down to
+// depth k - 1 (every node there starts with $), the sink dummies (W == $, from row 2), row 0.
+// Returns the mask of VALID edges (the flipped mask DBGSuccinct keeps, dbg_succinct.cpp:839-870).
+inline std::vector<uint64_t> valid_edges(const BossNav &b) {
+    const uint64_t nw = (b.n + 63) / 64;
+    std::vector<uint64_t> dummy(nw, 0);
+    auto set = [&](uint64_t i) { dummy[i >> 6] |= 1ull << (i & 63); };
+    set(0);
+    if (b.n > 1) {
+        std::vector<uint64_t> level{b.select_last(1)};  // last edge of the main dummy node
+        for (uint64_t depth = 0; depth < b.k && !level.empty(); ++depth) {
+            std::vector<uint64_t> next;
+            for (uint64_t last_edge : level) {
+                const uint64_t node = b.rank_last(last_edge);
+                const uint64_t first = b.select_last(node - 1) + 1;
+                for (uint64_t i = first; i <= last_edge; ++i) {
+                    set(i);
+                    const uint8_t c = b.W[i];
+                    if (c >= 1 && c <= 4 && depth + 1 < b.k) next.push_back(b.fwd(i, c));
+                }
+            }
+            level.swap(next);
+        }
+    }
+    for (uint64_t i = 2; i < b.n; ++i)  // mark_sink_dummy_edges (boss.cpp:1659-1679)
+        if (b.W[i] == 0) set(i);
+    for (uint64_t w = 0; w < nw; ++w) dummy[w] = ~dummy[w];
+    if (b.n % 64) dummy[nw - 1] &= (1ull << (b.n % 64)) - 1;
+    return dummy;
+}
+
+// bit_vector_small (bit_vector_adaptive.hpp:319) restated as a type tag (BE 0 = the stat
+// representation) followed by bit_vector_stat
+inline void put_bit_vector_small(std::ostream &o, const std::vector<uint64_t> &w, uint64_t nbits) {
+    put_be(o, 0);
+    put_bit_vector_stat(o, w, nbits);
+}
+inline std::vector<uint64_t> get_bit_vector_small(std::istream &in, uint64_t *nbits) {
+    if (get_be(in) != 0) throw std::runtime_error("bit_vector_small: unknown representation");
+    return get_bit_vector_stat(in, nbits);
+}
+
+// ------------------------------------------------------------------------ the graph files
+
+constexpr uint64_t kStateStat = 3;  // BOSS::State::STAT (boss.hpp:325), the build's default state
+
+struct DbgFile {
+    uint64_t k = 0, n = 0, F[5] = {0, 0, 0, 0, 0}, state = 0, mode = 0, suffix_length = 0;
+    std::vector<uint8_t> W;
+    std::vector<uint64_t> last, valid;
+    std::vector<std::pair<uint64_t, uint64_t>> ranges;
+    bool has_mask = false;
+};
+
+// `metagraph build` after construction (cli/build.cpp:323-352): optional --mask-dummy, the suffix
+// index of length min(node_suffix_length, k) (default 20 / log2(4) = 10, config.cpp:22-23), then
+// DBGSuccinct::serialize.  suffix_length < 0 selects that default.  Returns the valid edges
+// (`nodes (k)` of `metagraph stats`, stats.cpp:72-76) when masking, else n - 1.
+inline uint64_t write_dbg(const std::string &base, const uint8_t *W, const uint64_t *last, uint64_t n,
+                          const uint64_t *F, uint64_t k, uint64_t mode, bool mask_dummy, int64_t suffix_length,
+                          const uint32_t *weights, unsigned bits_per_count) {
+    BossNav nav(W, last, n, F, k);
+    uint64_t L = suffix_length < 0 ? std::min<uint64_t>(10, k) : std::min<uint64_t>((uint64_t)suffix_length, k);
+    if (L * 2 > 63) L = 0;  // "Node ranges for k-mer suffixes longer than ... cannot be indexed"
+    uint64_t n_valid = n ? n - 1 : 0;
+    {
+        std::ofstream o(base + ".dbg", std::ios::binary);
+        if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".dbg");
+        put_be(o, 5);
+        for (int c = 0; c < 5; ++c) put_be(o, F[c]);
+        put_be(o, k);
+        put_be(o, kStateStat);
+        put_wt_huff(o, W, n);
+        put_be(o, 4);  // logsigma of W: bits_per_char_W_
+        const uint64_t nw = (n + 63) / 64;
+        put_bit_vector_stat(o, std::vector<uint64_t>(last, last + nw), n);
+        put_be(o, mode);
+        const auto ranges = index_suffix_ranges(nav, L);
+        put_be(o, L);
+        for (const auto &r : ranges) {
+            put_raw<uint64_t>(o, r.first);
+            put_raw<uint64_t>(o, r.second);
+        }
+        if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".dbg");
+    }
+    if (mask_dummy) {
+        const std::vector<uint64_t> valid = valid_edges(nav);
+        n_valid = 0;
+        for (uint64_t x : valid) n_valid += __builtin_popcountll(x);
+        std::ofstream o(base + ".edgemask", std::ios::binary);
+        put_bit_vector_small(o, valid, n);
+        if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".edgemask");
+    }
+    if (weights && bits_per_count) {  // the chunk's weights buffer renamed (node_weights.cpp:62-68)
+        const unsigned w = bits_per_count;
+        std::vector<uint64_t> words((n * w + 63) / 64, 0);
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t v = (uint64_t)weights[i] & ((w >= 64) ? ~0ull : ((1ull << w) - 1));
+            const uint64_t pos = i * w, q = pos >> 6, b = pos & 63;
+            words[q] |= v << b;
+            if (b + w > 64) words[q + 1] |= v >> (64 - b);
+        }
+        std::ofstream o(base + ".dbg.weights", std::ios::binary);
+        put_bits(o, words, n * w, (int)w);
+        if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".dbg.weights");
+    }
+    return n_valid;
+}
+
+inline DbgFile read_dbg(const std::string &base) {
+    DbgFile f;
+    std::ifstream in(base + ".dbg", std::ios::binary);
+    if (!in.good()) throw std::runtime_error("Can't read file " + base + ".dbg");
+    if (get_be(in) != 5) throw std::runtime_error("ERROR: failed to load F vector, incompatible size");
+    for (int c = 0; c < 5; ++c) f.F[c] = get_be(in);
+    f.k = get_be(in);
+    f.state = get_be(in);
+    if (f.state != kStateStat) throw std::runtime_error("only the STAT representation is written here");
+    f.W = get_wt_huff(in);
+    if (get_be(in) != 4) throw std::runtime_error("ERROR: failed to load W vector");
+    uint64_t nb;
+    f.last = get_bit_vector_stat(in, &nb);
+    if (nb != f.W.size()) throw std::runtime_error("ERROR: failed to load L vector");
+    f.n = nb;
+    f.mode = get_be(in);
+    f.suffix_length = get_be(in);
+    if (f.suffix_length) {
+        uint64_t cnt = 1;
+        for (uint64_t i = 0; i < f.suffix_length; ++i) cnt *= 4;
+        f.ranges.resize(cnt);
+        for (auto &r : f.ranges) {
+            r.first = get_raw<uint64_t>(in);
+            r.second = get_raw<uint64_t>(in);
+        }
+    }
+    std::ifstream m(base + ".edgemask", std::ios::binary);
+    if (m.good()) {
+        uint64_t mb;
+        f.valid = get_bit_vector_small(m, &mb);
+        if (mb != f.n) throw std::runtime_error("edgemask size differs from the graph");
+        f.has_mask = true;
+    }
+    return f;
+}
+
+}  // namespace dbgio
+}  // namespace mtg
