@@ -149,6 +149,17 @@ int mtg_boss_ctor_add_packed(mtg_boss_ctor *ctor, const char *data, const uint64
                              const uint64_t *counts, size_t n);
 
 /*
+ * A FASTA or FASTQ file (plain or gzip) as input, the reference's parse_sequences ->
+ * read_fasta_file_critical path (cli/parse_sequences.hpp:103-151, seq_io/sequence_io.cpp:364-405)
+ * and push_sequences' one-thread-per-file loop (cli/build.cpp:31-56): the calling thread reads and
+ * inflates the file into pinned memory; at build time its bytes go to HBM in one copy and are split
+ * into records on the device (kseq rules: FASTA header lines start with '>', sequence lines are
+ * joined, line ends dropped; FASTQ four-line records).  Each record is one sequence of count 1.
+ * Thread-safe; call it concurrently for different files.
+ */
+int mtg_boss_ctor_add_fasta(mtg_boss_ctor *ctor, const char *path);
+
+/*
  * A KMC1 k-mer counter database (`<base>.kmc_pre` + `<base>.kmc_suf`; either name or the base) as
  * input: seq_io::read_kmers (seq_io/kmc_parser.cpp:27-62) + the build's KMC branch
  * (cli/parse_sequences.hpp:50-101).  Every k-mer with min_count <= count < max_count becomes a

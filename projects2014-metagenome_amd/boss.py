@@ -82,7 +82,8 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
            "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
-           "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free")
+           "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free",
+           "mtg_boss_ctor_add_fasta")
 
 COMM_ID_BYTES = 128
 
@@ -144,6 +145,7 @@ def lib():
         L.mtg_dist_bounds.argtypes = [P(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_int,
                                       P(ctypes.c_uint64)]
         L.mtg_dna_encode_table.argtypes = [ctypes.c_char_p]
+        L.mtg_boss_ctor_add_fasta.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.mtg_boss_write_dbg.argtypes = [P(_Chunk), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int64, P(ctypes.c_uint64)]
         L.mtg_boss_read_dbg.argtypes = [ctypes.c_char_p, P(_DbgFile)]
@@ -272,6 +274,19 @@ class BOSSChunkConstructor:
             self._h, buf.ctypes.data_as(ctypes.c_char_p),
             off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
             cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None, n))
+
+    def add_fasta(self, path):
+        """A FASTA / FASTQ file (plain or .gz): parse_sequences' FASTA branch
+        (cli/parse_sequences.hpp:103-151), split into records on the device at build time."""
+        _check(lib().mtg_boss_ctor_add_fasta(self._h, os.fsencode(path)))
+
+    def add_fasta_files(self, paths, threads=None):
+        """push_sequences (cli/build.cpp:31-56): one host thread per file."""
+        from concurrent.futures import ThreadPoolExecutor
+        paths = list(paths)
+        with ThreadPoolExecutor(max_workers=threads or max(1, min(len(paths), os.cpu_count() or 1))) as ex:
+            for f in [ex.submit(self.add_fasta, p) for p in paths]:
+                f.result()
 
     def add_kmc(self, kmc_path, min_count=1, max_count=2**32 - 1,
                 call_both_from_canonical=None):

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -25,6 +26,7 @@
 #include "dbg_io.hpp"
 #include "dist_kernels.hpp"
 #include "extract_partition.hpp"
+#include "fasta.hpp"
 #include "range_extract.hpp"
 #include "host_stage.hpp"
 #include "kmc.hpp"
@@ -55,7 +57,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -1022,7 +1024,10 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
 }
 
 // LSD sort + unique of the raw dummy k-mers da[0..Draw) (db is the ping-pong buffer); returns
-// D and leaves the distinct dummies in *dk
+// D and leaves the distinct dummies in *dk.  (An MSD sort of the dummies, planned for the 5-of-8
+// value density of lifted chars and with a read-before-CAS hash for their repeated keys, measured
+// 24.5 vs 7.5 ms per cfg2 step and 24.9 vs 0.51 s per cfg3 step: groups of the $-padded source
+// levels overflow the LDS tables and fall back.)
 template <int L3>
 static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db, uint64_t Draw,
                                     Key<L3> **dk) {
@@ -1782,6 +1787,11 @@ struct mtg_boss_ctor {
     std::mutex kmc_mu;
     std::vector<mtg::KmcInput> kmc;  // KMC databases, decoded on the device at build time
     std::atomic<uint64_t> stage_ns{0};  // host time spent staging since the last build
+    std::mutex fa_mu;
+    std::vector<mtg::FastaInput> fasta;  // FASTA / FASTQ files, split into reads on the device
+    ~mtg_boss_ctor() {
+        for (auto &f : fasta) mtg::free_fasta(f);
+    }
 };
 
 // one packed `last` word per thread: bit j of word w = last[64 w + j] (sdsl bit_vector layout)
@@ -1938,6 +1948,80 @@ int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_c
     }
 }
 
+int mtg_boss_ctor_add_fasta(mtg_boss_ctor *c, const char *path) {
+    if (!c || !path) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    try {
+        StageTimer t{c->stage_ns};
+        FastaInput in = load_fasta_file(path);  // read + inflate in the caller's thread
+        std::lock_guard<std::mutex> lock(c->fa_mu);
+        if (in.size) c->fasta.push_back(in);
+        else free_fasta(in);
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_ARGUMENT;
+    }
+}
+
+// the staged FASTA / FASTQ files -> reads appended to dseq at *seq_base (fasta.hpp); with
+// per-read counts (rstarts != nullptr) also their starts (count 1) from read index *read_base.
+// count_only: only sizes (*seq_base / *read_base advance by what the files will write).
+static void split_fasta_files(mtg_boss_ctor *c, uint8_t *dseq, uint64_t *seq_base, uint64_t *rstarts,
+                              uint32_t *rcounts, uint64_t *read_base, bool count_only) {
+    Ctx &x = c->ctx;
+    hipStream_t s = x.stream;
+    for (const FastaInput &f : c->fasta) {
+        const uint64_t n = f.size;
+        const uint64_t nt = ceil_div(n, FA_TILE);
+        uint8_t *raw = (uint8_t *)x.ws.get(Workspace::FA_RAW, n + 64);
+        int64_t *tlast = (int64_t *)x.ws.get(Workspace::FA_TLAST, (nt + 1) * 8);
+        int64_t *prev = (int64_t *)x.ws.get(Workspace::FA_PREV, (nt + 1) * 8);
+        uint32_t *ta = (uint32_t *)x.ws.get(Workspace::FA_TA, (nt + 1) * 4);
+        uint32_t *tb = (uint32_t *)x.ws.get(Workspace::FA_TB, (nt + 1) * 4);
+        uint64_t *oa = (uint64_t *)x.ws.get(Workspace::FA_OA, (nt + 1) * 8);
+        uint64_t *ob = (uint64_t *)x.ws.get(Workspace::FA_OB, (nt + 1) * 8);
+        HIP_CHECK(hipMemcpyAsync(raw, f.data, n, hipMemcpyHostToDevice, s));
+        unsigned long long first = ~0ull;
+        if (!f.fastq) {
+            HIP_CHECK(hipMemcpyAsync(&x.small->total, &first, 8, hipMemcpyHostToDevice, s));
+            fasta_first_header_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(n, 256), 8192)), dim3(256), 0, s>>>(
+                raw, n, &x.small->total);
+            HIP_CHECK(hipGetLastError());
+        }
+        fasta_stats_kernel<<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(raw, n, tlast, ta);
+        HIP_CHECK(hipGetLastError());
+        fasta_prefix_kernel<<<1, 1024, 0, s>>>(tlast, ta, nullptr, nt, prev, oa, nullptr);  // prev nl, lines
+        HIP_CHECK(hipGetLastError());
+        if (!f.fastq) first = read_u64(x, &x.small->total);
+        const uint64_t fh = f.fastq ? 0 : first;
+        fasta_split_kernel<false><<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(
+            raw, n, f.fastq ? 1 : 0, fh, prev, oa, ta, tb, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0);
+        HIP_CHECK(hipGetLastError());
+        uint64_t *koff = (uint64_t *)x.ws.get(Workspace::FA_KOFF, (nt + 1) * 8);
+        fasta_prefix_kernel<<<1, 1024, 0, s>>>(nullptr, ta, tb, nt, nullptr, koff, ob);
+        HIP_CHECK(hipGetLastError());
+        uint64_t tot[2];
+        HIP_CHECK(hipMemcpyAsync(&tot[0], koff + nt, 8, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(&tot[1], ob + nt, 8, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (!count_only) {
+            // the line-number prefix `oa` is still valid: the second prefix wrote koff / ob
+            fasta_split_kernel<true><<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(
+                raw, n, f.fastq ? 1 : 0, fh, prev, oa, nullptr, nullptr, koff, ob, dseq, *seq_base, rstarts,
+                rcounts, *read_base);
+            HIP_CHECK(hipGetLastError());
+            const uint8_t sep = '$';  // the last record's separator
+            HIP_CHECK(hipMemcpyAsync(dseq + *seq_base + tot[0], &sep, 1, hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipStreamSynchronize(s));  // the slots are reused by the next file
+        }
+        *seq_base += tot[0] + 1;
+        *read_base += tot[1];
+    }
+}
+
 static int run_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {
     try {
         HIP_CHECK(hipSetDevice(c->device));
@@ -1991,6 +2075,7 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
     std::lock_guard<std::mutex> lock(c->mu);
     std::unique_lock<std::shared_mutex> stage_lock(c->stage.lock());  // no add runs during the build
     std::lock_guard<std::mutex> kmc_lock(c->kmc_mu);
+    std::lock_guard<std::mutex> fa_lock(c->fa_mu);
     std::memset(out, 0, sizeof(*out));
     try {
         HIP_CHECK(hipSetDevice(c->device));
@@ -2003,13 +2088,20 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
             kmc_bytes += m.total * (m.k + 1) * (m.both ? 2 : 1);
             kmc_reads += m.total * (m.both ? 2 : 1);
         }
-        const uint64_t total_len = len + kmc_bytes, total_reads = nr + kmc_reads;
+        uint64_t fa_bytes = 0, fa_reads = 0;
+        for (const auto &f : c->fasta) fa_bytes += f.size + 1;  // split output <= raw bytes + a separator
+        const bool per_read_inputs = st.any_count_not_one() || kmc_reads;
+        if (c->params.bits_per_count && per_read_inputs && !c->fasta.empty()) {
+            uint64_t sb = 0;  // record counts first: the read-start arrays are sized by them
+            split_fasta_files(c, nullptr, &sb, nullptr, nullptr, &fa_reads, true);
+        }
+        const uint64_t total_len = len + kmc_bytes + fa_bytes, total_reads = nr + kmc_reads + fa_reads;
         uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
         const auto t_h2d = std::chrono::steady_clock::now();
         if (len) HIP_CHECK(hipMemcpyAsync(dseq, st.data(), len, hipMemcpyHostToDevice, s));
         uint64_t *dstarts = nullptr;
         uint32_t *dcounts = nullptr;
-        const bool per_read = c->params.bits_per_count && (st.any_count_not_one() || kmc_reads) && total_reads;
+        const bool per_read = c->params.bits_per_count && per_read_inputs && total_reads;
         if (per_read) {
             dstarts = (uint64_t *)c->ctx.ws.get(Workspace::STARTS, total_reads * 8);
             dcounts = (uint32_t *)c->ctx.ws.get(Workspace::RCOUNTS, total_reads * 4);
@@ -2036,7 +2128,9 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
             seq_base += m.total * (m.k + 1) * (m.both ? 2 : 1);
             read_base += m.total * (m.both ? 2 : 1);
         }
-        BuildInput in{dseq, total_len, dstarts, dcounts, per_read ? total_reads : 0};
+        split_fasta_files(c, dseq, &seq_base, per_read ? dstarts : nullptr, per_read ? dcounts : nullptr, &read_base,
+                          false);
+        BuildInput in{dseq, seq_base, dstarts, dcounts, per_read ? total_reads : 0};
         BuildOutput o{};
         run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
                      c->params.bits_per_count, in, &o);
@@ -2071,6 +2165,8 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         stage_lock.unlock();
         c->stage.clear();
         c->kmc.clear();
+        for (auto &f : c->fasta) free_fasta(f);
+        c->fasta.clear();
         T.host_total_ms = ms_since(t_start);
         return MTG_OK;
     } catch (const std::exception &e) {

@@ -83,6 +83,15 @@ def test_disk_container_is_the_batched_build(transcripts_1000):
     assert t.n_batches >= 2
 
 
+def test_ranges_k63_u256_dummies(monkeypatch):
+    # k = 63 / 64: u128 2-bit keys, u256 lifted dummies
+    monkeypatch.setenv("MTG_RANGES", "3")
+    reads = _random_reads(63, 3000, 150, 60000, n_rate=0.001)
+    for canonical in (False, True):
+        _check(62, reads, canonical, 8)
+        _check(63, reads, canonical, 0)
+
+
 def test_ranges_empty_and_tiny(monkeypatch):
     monkeypatch.setenv("MTG_RANGES", "9")
     for k in (1, 5, 31, 40):
