@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-steps", type=int, default=3,
                     help="steps of the host-buffer leg (0 = skip)")
+    ap.add_argument("--fasta-reads", type=int, default=2_000_000,
+                    help="reads of the FASTA-file leg (0 = skip)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
     if args.config:
@@ -202,6 +204,54 @@ def host_path(args, kb, boss, seq, steps):
                           "d2h_W_last_weights": m[4], "build_chunk_call": m[5]},
             "steps": steps, "staging_threads": cpu_threads(),
             "what": "add_packed + build_chunk through the C ABI on the same reads, host arrays out"}
+
+
+def fasta_path(args, kb, boss, steps, n_reads, files=8):
+    """SURVEY.md section 8(d)(ii), end to end from FASTA files: a sample of the same generator
+    written as `files` FASTA shards (60-column lines) to a temp dir (untimed), then per step
+    add_fasta on one host thread per shard (read into pinned memory) + build_chunk (one H2D of
+    the raw bytes, records split on the device, the device path, host arrays out)."""
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    asc = make_reads_host_codes(n_reads, args.read_len, 4321, args.data, args.coverage)
+    tmp = tempfile.mkdtemp(prefix="mtg_fa_")
+    paths, nbytes = [], 0
+    try:
+        for f in range(files):
+            p = os.path.join(tmp, "reads_%03d.fa" % f)
+            with open(p, "wb") as out:
+                for i in range(f, n_reads, files):
+                    r = asc[i].tobytes()
+                    out.write(b">r%d\n" % i)
+                    for j in range(0, len(r), 60):
+                        out.write(r[j:j + 60] + b"\n")
+            nbytes += os.path.getsize(p)
+            paths.append(p)
+        ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=args.mode == "canonical",
+                                                     bits_per_count=args.count_width)
+        rows = []
+        with ThreadPoolExecutor(max_workers=files) as ex:
+            for it in range(steps + 1):  # the first build sizes the buffers (untimed)
+                t0 = time.perf_counter()
+                list(ex.map(ctor.add_fasta, paths))
+                t1 = time.perf_counter()
+                ch = ctor.build_chunk()
+                dt = time.perf_counter() - t0
+                t = ctor.timings()
+                if it:
+                    rows.append((dt, t1 - t0, t.input_ms, t.total_ms, t.d2h_ms, t.host_total_ms))
+                del ch
+        m = [sum(r[i] for r in rows) / len(rows) for i in range(6)]
+        kmers = n_reads * (args.read_len - args.k + 1)
+        return {"value": kmers / m[0], "unit": "k-mers/s", "ms_per_step": m[0] * 1e3,
+                "fasta_gb_per_s": nbytes / m[0] / 1e9,
+                "stages_ms": {"read_files_into_pinned": m[1] * 1e3, "h2d_and_split_on_device": m[2],
+                              "device_path": m[3], "d2h_W_last_weights": m[4], "build_chunk_call": m[5]},
+                "sample": "%d reads in %d FASTA files, %.0f MB" % (n_reads, files, nbytes / 1e6),
+                "steps": steps}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def measured_copy_peak(torch, device, nbytes=4 << 30, reps=5):
@@ -367,6 +417,8 @@ def main():
     }
     if rank == 0 and args.host_steps > 0 and world == 1:
         result["host_path"] = host_path(args, kb, boss, seq, args.host_steps)
+        if args.fasta_reads > 0:
+            result["fasta_path"] = fasta_path(args, kb, boss, args.host_steps, args.fasta_reads)
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(args, kb, boss)
     if rank == 0:

@@ -130,6 +130,7 @@ typedef struct mtg_boss_timings {
     double host_total_ms;        /* the whole build_chunk call */
     uint64_t n_batches;          /* key-range batches of the build (1 = the input fit at once) */
     uint64_t peak_bytes;         /* device workspace held at the end of the build */
+    double input_ms;             /* host-buffer builds: KMC decode + FASTA split on the device (incl. their copies) */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);

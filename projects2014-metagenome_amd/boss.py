@@ -66,7 +66,8 @@ class Timings(ctypes.Structure):
                 ("world", ctypes.c_uint64)] + \
                [(name, ctypes.c_double) for name in
                 ("stage_ms", "h2d_ms", "d2h_ms", "host_total_ms")] + \
-               [("n_batches", ctypes.c_uint64), ("peak_bytes", ctypes.c_uint64)]
+               [("n_batches", ctypes.c_uint64), ("peak_bytes", ctypes.c_uint64),
+                ("input_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -161,19 +162,54 @@ def _check(rc):
         raise RuntimeError(lib().mtg_last_error().decode() or "error %d" % rc)
 
 
-class Chunk:
-    """BOSS::Chunk (boss_chunk.hpp:19-104): W (0..9), last (0/1), F[5], weights, k."""
+class _ChunkBlocks:
+    """Owner of one mtg_boss_chunk's pinned host arrays: numpy views keep it alive, and it
+    releases the arrays (mtg_boss_chunk_free) when the last view is gone."""
 
-    def __init__(self, k, W, last, F, weights=None, n_real=None, n_dummy=None, bits_per_count=0):
+    def __init__(self, c):
+        self._c = c
+
+    def view(self, ptr, n, dtype):
+        size = int(n) * np.dtype(dtype).itemsize
+        if size == 0:
+            return np.zeros(0, dtype=dtype)
+        buf = (ctypes.c_uint8 * size).from_address(ctypes.cast(ptr, ctypes.c_void_p).value)
+        buf._owner = self
+        return np.frombuffer(buf, dtype=dtype)
+
+    def __del__(self):
+        c, self._c = getattr(self, "_c", None), None
+        if c is not None and _lib is not None:
+            _lib.mtg_boss_chunk_free(ctypes.byref(c))
+
+
+class Chunk:
+    """BOSS::Chunk (boss_chunk.hpp:19-104): W (0..9), last (0/1), F[5], weights, k.  `last`
+    may be given as packed words (last_words, the ABI's layout) and is unpacked on first use."""
+
+    def __init__(self, k, W, last, F, weights=None, n_real=None, n_dummy=None, bits_per_count=0,
+                 last_words=None):
         self.k = k
         self.alph_size = 5
         self.bits_per_count = bits_per_count
         self.W = W
-        self.last = last
+        self._last = last
+        self._last_words = last_words
         self.F = F
         self.weights = weights
         self.n_real = n_real
         self.n_dummy = n_dummy
+
+    @property
+    def last(self):
+        if self._last is None:
+            self._last = unpack_last(self._last_words, len(self.W))
+        return self._last
+
+    @last.setter
+    def last(self, value):
+        self._last = value
+        self._last_words = None
 
     def size(self):
         return len(self.W)
@@ -197,7 +233,7 @@ class Chunk:
         <outbase>.dbg, <outbase>.edgemask (mask_dummy) and <outbase>.dbg.weights (weighted).
         Returns the valid edges after masking (`nodes (k)` of `metagraph stats`), else rows - 1."""
         W = np.ascontiguousarray(self.W, dtype=np.uint8)
-        last = pack_last(self.last)
+        last = self._last_words if self._last_words is not None else pack_last(self.last)
         F = (ctypes.c_uint64 * 5)(*[int(f) for f in self.F])
         c = _Chunk(k=self.k, alph_size=5, n=len(W), F=F, bits_per_count=self.bits_per_count or 0)
         c.W = W.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
@@ -306,13 +342,14 @@ class BOSSChunkConstructor:
         else:
             _check(lib().mtg_boss_ctor_build_chunk_dist(self._h, comm.handle, ctypes.byref(c)))
         n = c.n
-        W = np.ctypeslib.as_array(c.W, shape=(n,)).copy()
-        last = unpack_last(np.ctypeslib.as_array(c.last, shape=((n + 63) // 64,)), n)
-        weights = np.ctypeslib.as_array(c.weights, shape=(n,)).copy() if c.weights else None
+        # zero-copy views of the chunk's pinned host blocks; the blocks are released when the
+        # last view is gone (_ChunkBlocks)
+        owner = _ChunkBlocks(c)
+        W = owner.view(c.W, n, np.uint8)
+        words = owner.view(c.last, (n + 63) // 64, np.uint64)
+        weights = owner.view(c.weights, n, np.uint32) if c.weights else None
         F = np.array(list(c.F), dtype=np.uint64)
-        out = Chunk(c.k, W, last, F, weights, c.n_real, c.n_dummy, self._bits)
-        lib().mtg_boss_chunk_free(ctypes.byref(c))
-        return out
+        return Chunk(c.k, W, None, F, weights, c.n_real, c.n_dummy, self._bits, last_words=words)
 
     def build_device(self, d_seq, seq_len, d_read_starts=None, d_counts=None, n_reads=0,
                      stream=None, comm=None):

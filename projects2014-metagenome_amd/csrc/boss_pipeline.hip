@@ -57,7 +57,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -360,11 +360,23 @@ static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
     return p;
 }
 
+// the rc sort's local pass fused with the merge into the real edges (local_merge_kernel)
+template <int L>
+struct RcMerge {
+    const Key<L> *ck;   // the sorted canonical set
+    const uint32_t *cv;
+    uint64_t nc;
+    Key<L> *out;        // the real edges: merge(canonical, sorted rc)
+    uint32_t *outc;
+    bool done = false;  // set when the fused pass ran (else the caller merges)
+};
+
 template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
                                 double dup, const uint32_t *hist1 = nullptr, bool distinct = false,
-                                const std::vector<uint64_t> *runs = nullptr, bool level1_done = false) {
+                                const std::vector<uint64_t> *runs = nullptr, bool level1_done = false,
+                                RcMerge<L> *rm = nullptr) {
     // level1_done: the producer already scattered the keys by the plan's level-1 digit
     // (extract_partition_kernel); hist1 holds that level's counts
     // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them;
@@ -484,8 +496,25 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             HIP_CHECK(hipGetLastError());
         } else {
             uint32_t *gf = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nbuckets + 1) * 4);
+            const bool fuse = rm && distinct && b <= 32;
+            uint64_t *cstart = nullptr;
+            const uint64_t *gsize = bstart;
+            if (fuse) {
+                // fused rc merge: the canonical keys of every bucket (bucket index of the sorted
+                // set), and groups sized by rc + canonical keys together
+                cstart = (uint64_t *)c.ws.get(Workspace::RC_CSTART, (nbuckets + 2) * 8);
+                const uint64_t gi = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(rm->nc + 1, 256), 8192));
+                bucket_index_kernel<L><<<dim3((unsigned)gi), dim3(256), 0, c.stream>>>(rm->ck, rm->nc, nbits - b,
+                                                                                       nbuckets, cstart);
+                HIP_CHECK(hipGetLastError());
+                uint64_t *comb = (uint64_t *)c.ws.get(Workspace::RC_COMB, (nbuckets + 1) * 8);
+                add_starts_kernel<<<dim3((unsigned)ceil_div(nbuckets + 1, 256)), dim3(256), 0, c.stream>>>(
+                    bstart, cstart, nbuckets + 1, comb);
+                HIP_CHECK(hipGetLastError());
+                gsize = comb;
+            }
             group_flags_kernel<<<dim3((unsigned)ceil_div(nbuckets, 256)), dim3(256), 0, c.stream>>>(
-                bstart, nbuckets, G, gf);
+                gsize, nbuckets, G, gf);
             HIP_CHECK(hipGetLastError());
             uint64_t *gpos = (uint64_t *)c.ws.get(Workspace::MSD_USTART, (nbuckets + 1) * 8);
             uint32_t ep;
@@ -498,9 +527,45 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             HIP_CHECK(hipMemcpyAsync(&ngroups, gpos + nbuckets, 8, hipMemcpyDeviceToHost, c.stream));
             HIP_CHECK(hipStreamSynchronize(c.stream));
             gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, (ngroups + 1) * 8);
+            uint64_t *gbucket = fuse ? (uint64_t *)c.ws.get(Workspace::MSD_GBUCKET, (ngroups + 1) * 8) : nullptr;
             group_scatter_kernel<<<dim3((unsigned)ceil_div(nbuckets + 1, 256)), dim3(256), 0, c.stream>>>(
-                bstart, gf, gpos, nbuckets, n, gstart);
+                bstart, gf, gpos, nbuckets, n, gstart, gbucket);
             HIP_CHECK(hipGetLastError());
+            if (fuse && ngroups) {
+                // sort the rc groups and merge them with the canonical keys in one pass
+                constexpr int CAP = MergeLocalTraits<L>::CAP;
+                uint32_t *gflag = (uint32_t *)c.ws.get(Workspace::MSD_OVF, ngroups * 4);
+                HIP_CHECK(hipMemsetAsync(gflag, 0, ngroups * 4, c.stream));
+                HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+                local_merge_kernel<L, COUNTED, CAP><<<dim3((unsigned)ngroups), dim3(512), 0, c.stream>>>(
+                    *keys, COUNTED ? *vals : nullptr, gstart, gbucket, nullptr, rm->ck, rm->cv, cstart, rm->out,
+                    rm->outc, gflag, &c.small->counter);
+                HIP_CHECK(hipGetLastError());
+                uint32_t novf = 0;
+                HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));
+                if (novf) {  // the few big groups again with twice the LDS arrays
+                    std::vector<uint32_t> fl(ngroups), list;
+                    HIP_CHECK(hipMemcpyAsync(fl.data(), gflag, ngroups * 4, hipMemcpyDeviceToHost, c.stream));
+                    HIP_CHECK(hipStreamSynchronize(c.stream));
+                    for (uint64_t g = 0; g < ngroups; ++g)
+                        if (fl[g]) list.push_back((uint32_t)g);
+                    uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
+                    HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
+                    HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+                    local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
+                        *keys, COUNTED ? *vals : nullptr, gstart, gbucket, dlist, rm->ck, rm->cv, cstart, rm->out,
+                        rm->outc, gflag, &c.small->counter);
+                    HIP_CHECK(hipGetLastError());
+                    HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
+                    HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
+                    if (c.debug) fprintf(stderr, "[mtg debug] rc merge: %zu big groups -> %u left\n", list.size(), novf);
+                }
+                if (!novf) {
+                    rm->done = true;
+                    return n;  // the rc keys (distinct); rm->out holds U + n
+                }
+            }
         }
         uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (ngroups + 1) * 4);
         uint32_t *ovf = (uint32_t *)c.ws.get(Workspace::MSD_OVF, ngroups * 4);
@@ -986,7 +1051,8 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
 template <int L2, bool COUNTED>
 static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<L2> *ka,
                          uint32_t *ca, uint64_t U, Key<L2> *buf, uint32_t *bufc, Key<L2> **rk,
-                         uint32_t **rkc) {
+                         uint32_t **rkc, RcMerge<L2> *rm = nullptr) {
+    // rm: merge the sorted rc keys straight into rm->out (rm->done), when the MSD local pass can
     using K2 = Key<L2>;
     uint64_t Urc = U;
     uint32_t *rc_hist = nullptr;
@@ -1017,7 +1083,8 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
     K2 *ra = buf, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
     uint32_t *rca = bufc, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
     if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
-    else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true);
+    else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true, nullptr,
+                                            false, rm);
     *rk = ra;
     *rkc = rca;
     return Urc;
@@ -1270,11 +1337,13 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     if (canonical && U && P == 1) {
         K2 *rk;
         uint32_t *rkc;
-        const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc);
+        // the real edges hold at most 2U keys (the palindromes of even K drop out of the rc set)
+        K2 *real = (K2 *)c.ws.get(Workspace::REAL, 2 * U * sizeof(K2));
+        uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, 2 * U * 4) : nullptr;
+        RcMerge<L2> rm{ka, ca, U, real, realc};
+        const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc, &rm);
         R = U + Urc;
-        K2 *real = (K2 *)c.ws.get(Workspace::REAL, R * sizeof(K2));
-        uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, R * 4) : nullptr;
-        merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, rk, rkc, Urc, K, real, realc, 0);
+        if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, rk, rkc, Urc, K, real, realc, 0);
         ka = real;
         ca = realc;
     }
@@ -1918,17 +1987,20 @@ int mtg_boss_ctor_add_packed(mtg_boss_ctor *c, const char *data, const uint64_t 
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
     }
-    std::vector<const char *> ptrs(n);
-    std::vector<uint64_t> lens(n);
     for (size_t i = 0; i < n; ++i) {
         if (offsets[i + 1] < offsets[i]) {
             set_error("offsets must be nondecreasing");
             return MTG_ERR_ARGUMENT;
         }
-        ptrs[i] = data + offsets[i];
-        lens[i] = offsets[i + 1] - offsets[i];
     }
-    return mtg_boss_ctor_add_sequences(c, ptrs.data(), lens.data(), counts, n);
+    try {
+        StageTimer t{c->stage_ns};
+        c->stage.add_packed(data, offsets, counts, n, stage_threads(c));
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_ARGUMENT;
+    }
 }
 
 int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_count, uint64_t max_count,
@@ -2113,6 +2185,7 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         HIP_CHECK(hipStreamSynchronize(s));
         const double h2d_ms = ms_since(t_h2d);
         // KMC records -> reads, on the device (kmc.hpp)
+        const auto t_input = std::chrono::steady_clock::now();
         uint64_t seq_base = len, read_base = nr;
         for (const auto &m : c->kmc) {
             uint64_t *dlut = (uint64_t *)c->ctx.ws.get(Workspace::KMC_LUT, m.lut.size() * 8);
@@ -2130,6 +2203,8 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         }
         split_fasta_files(c, dseq, &seq_base, per_read ? dstarts : nullptr, per_read ? dcounts : nullptr, &read_base,
                           false);
+        HIP_CHECK(hipStreamSynchronize(s));
+        const double input_ms = ms_since(t_input);
         BuildInput in{dseq, seq_base, dstarts, dcounts, per_read ? total_reads : 0};
         BuildOutput o{};
         run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
@@ -2161,6 +2236,7 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         mtg_boss_timings &T = c->ctx.timings;
         T.d2h_ms = ms_since(t_d2h);
         T.h2d_ms = h2d_ms;
+        T.input_ms = input_ms;
         T.stage_ms = (double)c->stage_ns.exchange(0) * 1e-6;
         stage_lock.unlock();
         c->stage.clear();

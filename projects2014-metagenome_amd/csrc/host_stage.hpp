@@ -97,43 +97,75 @@ class HostStage {
         if (data_) (void)hipHostFree(data_);
     }
 
-    // n reads: read i is `lens[i]` bytes at ptrs[i]; counts may be null (all 1)
+    // n reads: read i is `lens[i]` bytes at ptrs[i]; counts may be null (all 1).
+    // Per-read counts are kept as (start, count) runs: consecutive reads of one count share a run
+    // (windows never span a separator, so a run maps each of its windows to the right count), and
+    // a batch without counts is one run -- no per-read bookkeeping on the common path.
     void add(const char *const *ptrs, const uint64_t *lens, const uint64_t *counts, size_t n, unsigned threads) {
+        add_reads(n, [&](size_t i) { return ptrs[i]; }, [&](size_t i) { return lens[i]; }, counts, threads);
+    }
+    // n reads back to back in `data`, read i = [offsets[i], offsets[i + 1])
+    void add_packed(const char *data, const uint64_t *offsets, const uint64_t *counts, size_t n, unsigned threads) {
+        add_reads(n, [&](size_t i) { return data + offsets[i]; },
+                  [&](size_t i) { return offsets[i + 1] - offsets[i]; }, counts, threads);
+    }
+
+    template <typename Ptr, typename Len>
+    void add_reads(size_t n, Ptr ptr, Len len, const uint64_t *counts, unsigned threads) {
         if (!n) return;
-        // offsets of the batch's reads inside it (prefix sums, separators included)
-        std::vector<uint64_t> rel(n + 1);
-        rel[0] = 0;
-        for (size_t i = 0; i < n; ++i) rel[i + 1] = rel[i] + lens[i] + 1;
-        const uint64_t total = rel[n];
+        // the batch's byte offsets: per-chunk sums in parallel, then each chunk copies from its base
+        const unsigned t = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(std::max(1u, threads), n / 4096));
+        std::vector<uint64_t> cbase(t + 1, 0);
+        parallel_ranges(t, t, 1, [&](uint64_t c0, uint64_t c1) {
+            for (uint64_t c = c0; c < c1; ++c) {
+                uint64_t sum = 0;
+                for (uint64_t i = n * c / t; i < n * (c + 1) / t; ++i) sum += len(i) + 1;
+                cbase[c + 1] = sum;
+            }
+        });
+        for (unsigned c = 0; c < t; ++c) cbase[c + 1] += cbase[c];
+        const uint64_t total = cbase[t];
         uint64_t off;
         {
             std::unique_lock<std::shared_mutex> ex(grow_);
             if (size_ + total > cap_) grow(std::max<uint64_t>(size_ + total, cap_ + cap_ / 2));
             off = size_;
             size_ += total;
-            starts_.reserve(starts_.size() + n);
-            counts_.reserve(counts_.size() + n);
+            uint64_t pos = off;
             for (size_t i = 0; i < n; ++i) {
-                starts_.push_back(off + rel[i]);
-                const uint64_t c = counts ? counts[i] : 1;
-                const uint32_t c32 = c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
-                counts_.push_back(c32);
+                const uint64_t cnt = counts ? counts[i] : 1;
+                const uint32_t c32 = cnt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cnt;
+                if (counts_.empty() || counts_.back() != c32 || run_end_ != pos) {
+                    starts_.push_back(pos);
+                    counts_.push_back(c32);
+                }
                 any_count_not_one_ |= c32 != 1;
+                if (!counts) {  // the whole batch is one run of count 1
+                    pos = off + total;
+                    break;
+                }
+                pos += len(i) + 1;
             }
+            run_end_ = pos;
         }
         std::shared_lock<std::shared_mutex> sh(grow_);  // a growth waits for the copy
         char *dst = data_ + off;
-        parallel_ranges(n, threads, 4096, [&](uint64_t i0, uint64_t i1) {
-            for (uint64_t i = i0; i < i1; ++i) {
-                std::memcpy(dst + rel[i], ptrs[i], lens[i]);
-                dst[rel[i] + lens[i]] = '$';
+        parallel_ranges(t, t, 1, [&](uint64_t c0, uint64_t c1) {
+            for (uint64_t c = c0; c < c1; ++c) {
+                uint64_t o = cbase[c];
+                for (uint64_t i = n * c / t; i < n * (c + 1) / t; ++i) {
+                    const uint64_t l = len(i);
+                    std::memcpy(dst + o, ptr(i), l);
+                    dst[o + l] = '$';
+                    o += l + 1;
+                }
             }
         });
     }
 
     const char *data() const { return data_; }
     uint64_t size() const { return size_; }
-    uint64_t n_reads() const { return starts_.size(); }
+    uint64_t n_reads() const { return starts_.size(); }  // count runs (see add)
     const std::vector<uint64_t> &starts() const { return starts_; }
     const std::vector<uint32_t> &counts() const { return counts_; }
     bool any_count_not_one() const { return any_count_not_one_; }
@@ -141,6 +173,7 @@ class HostStage {
     void clear() {
         std::unique_lock<std::shared_mutex> ex(grow_);
         size_ = 0;
+        run_end_ = ~0ull;
         starts_.clear();
         counts_.clear();
         any_count_not_one_ = false;
@@ -164,6 +197,7 @@ class HostStage {
     uint64_t size_ = 0, cap_ = 0;
     std::vector<uint64_t> starts_;
     std::vector<uint32_t> counts_;
+    uint64_t run_end_ = ~0ull;  // byte offset where the last run ends (a new batch may extend it)
     bool any_count_not_one_ = false;
 };
 

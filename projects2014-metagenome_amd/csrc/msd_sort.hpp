@@ -282,13 +282,28 @@ __global__ void group_flags_kernel(const uint64_t *__restrict__ bstart, uint64_t
     flags[b] = f;
 }
 
+// c[i] = a[i] + b[i] (bucket starts of two key sets -> starts of their union)
+__global__ void add_starts_kernel(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, uint64_t n,
+                                  uint64_t *__restrict__ c) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) c[i] = a[i] + b[i];
+}
+
 __global__ void group_scatter_kernel(const uint64_t *__restrict__ bstart,
                                      const uint32_t *__restrict__ flags,
                                      const uint64_t *__restrict__ pos, uint64_t nbuckets,
-                                     uint64_t n, uint64_t *__restrict__ gstart) {
+                                     uint64_t n, uint64_t *__restrict__ gstart,
+                                     uint64_t *__restrict__ gbucket = nullptr) {
+    // gbucket (optional): each group's first bucket; group 0 from bucket 0, the end = nbuckets
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nbuckets && flags[b]) gstart[pos[b]] = bstart[b];
-    if (b == nbuckets) gstart[pos[nbuckets]] = n;
+    if (b < nbuckets && flags[b]) {
+        gstart[pos[b]] = bstart[b];
+        if (gbucket) gbucket[pos[b]] = pos[b] == 0 ? 0 : b;
+    }
+    if (b == nbuckets) {
+        gstart[pos[nbuckets]] = n;
+        if (gbucket) gbucket[pos[nbuckets]] = nbuckets;
+    }
 }
 
 /*
@@ -644,6 +659,128 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
     if (tid == 0) {
         ucount[g] = (uint32_t)out_off;
         overflow[g] = 0;
+    }
+}
+
+/*
+ * The reverse-complement sort's local pass fused with the merge into the real edges
+ * (add_reverse_complements, boss_chunk_construct.cpp:179-222): one workgroup per group of the rc
+ * partition sorts the group's rc keys in LDS (distinct input: the counting sort + rank of
+ * local_unique_kernel<NODUP>), merges them with the canonical keys of the same bucket range
+ * (cstart: bucket index of the sorted canonical set over the same top b bits), and writes the
+ * merged run at its final place: the canonical keys before the range + the rc keys before the
+ * group.  A group or range over CAP keys sets *ovf and the caller takes the unfused path.
+ */
+template <int L>
+struct MergeLocalTraits {
+    static constexpr int CAP = L == 1 ? 2048 : L == 2 ? 1024 : 512;  // keys per array (3 arrays)
+};
+
+// CAP: keys per LDS array; glist (optional): the groups to run (the big-CAP rerun of the groups
+// the first launch flagged in gflag); *ovf counts groups left over
+template <int L, bool COUNTED, int CAP, int LB = 512>
+__global__ __launch_bounds__(LB) void local_merge_kernel(
+    const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals, const uint64_t *__restrict__ gstart,
+    const uint64_t *__restrict__ gbucket, const uint32_t *__restrict__ glist, const Key<L> *__restrict__ ck,
+    const uint32_t *__restrict__ cv, const uint64_t *__restrict__ cstart, Key<L> *__restrict__ out,
+    uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf) {
+    __shared__ Key<L> s_r[CAP];  // rc keys, then sorted
+    __shared__ Key<L> s_s[CAP];  // rc keys by sub-bucket
+    __shared__ Key<L> s_c[CAP];  // canonical keys of the range
+    __shared__ uint32_t s_rv[COUNTED ? CAP : 1], s_sv[COUNTED ? CAP : 1], s_cv[COUNTED ? CAP : 1];
+    __shared__ uint32_t s_hist[256], s_fill[256];
+    __shared__ int s_hb;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
+    const uint64_t g0 = gstart[g], g1 = gstart[g + 1];
+    const uint64_t c0 = cstart[gbucket[g]], c1 = cstart[gbucket[g + 1]];
+    if (g1 - g0 > (uint64_t)CAP || c1 - c0 > (uint64_t)CAP) {
+        if (tid == 0) {
+            gflag[g] = 1;
+            atomicAdd(ovf, 1u);
+        }
+        return;
+    }
+    const uint32_t nr = (uint32_t)(g1 - g0), nc = (uint32_t)(c1 - c0);
+    for (uint32_t i = tid; i < nr; i += LB) {
+        s_r[i] = keys[g0 + i];
+        if (COUNTED) s_rv[i] = vals[g0 + i];
+    }
+    for (uint32_t i = tid; i < nc; i += LB) {
+        s_c[i] = ck[c0 + i];
+        if (COUNTED) s_cv[i] = cv[c0 + i];
+    }
+    if (tid < 256) {
+        s_hist[tid] = 0;
+        s_fill[tid] = 0;
+    }
+    if (tid == 0) s_hb = -1;
+    __syncthreads();
+    if (nr) {
+        const Key<L> ref = s_r[0];
+        int hb_local = -1;
+        for (uint32_t i = tid; i < nr; i += LB) {
+            Key<L> dx;
+#pragma unroll
+            for (int w = 0; w < L; ++w) dx.w[w] = s_r[i].w[w] ^ ref.w[w];
+            hb_local = max(hb_local, key_msb(dx));
+        }
+        if (hb_local >= 0) atomicMax(&s_hb, hb_local);
+    }
+    __syncthreads();
+    const int hb = s_hb;
+    const unsigned dshift = hb >= 7 ? (unsigned)(hb - 7) : 0u;
+    for (uint32_t i = tid; i < nr; i += LB) atomicAdd(&s_hist[bits_at(s_r[i], dshift, 8)], 1u);
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t a0 = s_hist[4 * tid], a1 = s_hist[4 * tid + 1], a2 = s_hist[4 * tid + 2], a3 = s_hist[4 * tid + 3];
+        const uint32_t sum4 = a0 + a1 + a2 + a3;
+        const uint32_t bb = wave_inclusive_sum(sum4) - sum4;
+        s_hist[4 * tid] = bb;
+        s_hist[4 * tid + 1] = bb + a0;
+        s_hist[4 * tid + 2] = bb + a0 + a1;
+        s_hist[4 * tid + 3] = bb + a0 + a1 + a2;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nr; i += LB) {
+        const uint32_t d = bits_at(s_r[i], dshift, 8);
+        const uint32_t p = s_hist[d] + atomicAdd(&s_fill[d], 1u);
+        s_s[p] = s_r[i];
+        if (COUNTED) s_sv[p] = s_rv[i];
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < nr; p += LB) {
+        const Key<L> key = s_s[p];
+        const uint32_t d = bits_at(key, dshift, 8);
+        const uint32_t b0 = s_hist[d], b1 = b0 + s_fill[d];
+        uint32_t rank = 0;
+        for (uint32_t j = b0; j < b1; ++j) rank += s_s[j] < key;
+        s_r[b0 + rank] = key;
+        if (COUNTED) s_rv[b0 + rank] = s_sv[p];
+    }
+    __syncthreads();
+    // merge path over (s_r[0..nr), s_c[0..nc)): thread t writes outputs [t * IT, (t + 1) * IT)
+    const uint32_t n = nr + nc;
+    const uint32_t IT = (n + LB - 1) / LB;
+    const uint32_t o0 = min(tid * IT, n), o1 = min(o0 + IT, n);
+    uint32_t lo = o0 > nc ? o0 - nc : 0, hi = min(o0, nr);
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_r[mid] < s_c[o0 - mid - 1]) lo = mid + 1; else hi = mid;
+    }
+    uint32_t i = lo, j = o0 - lo;
+    const uint64_t base = c0 + g0;
+    for (uint32_t o = o0; o < o1; ++o) {
+        const bool take_r = i < nr && (j >= nc || s_r[i] < s_c[j]);
+        if (take_r) {
+            out[base + o] = s_r[i];
+            if (COUNTED) outc[base + o] = s_rv[i];
+            ++i;
+        } else {
+            out[base + o] = s_c[j];
+            if (COUNTED) outc[base + o] = s_cv[j];
+            ++j;
+        }
     }
 }
 
