@@ -360,6 +360,8 @@ static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
     return p;
 }
 
+static void note_bucket_index(Ctx &c, const void *keys, uint64_t n, const uint64_t *start, unsigned shift);
+
 // the rc sort's local pass fused with the merge into the real edges (local_merge_kernel)
 template <int L>
 struct RcMerge {
@@ -369,6 +371,8 @@ struct RcMerge {
     Key<L> *out;        // the real edges: merge(canonical, sorted rc)
     uint32_t *outc;
     bool done = false;  // set when the fused pass ran (else the caller merges)
+    uint64_t *istart = nullptr;  // also the dummy stage's bucket index over the top ib bits of out
+    unsigned ib = 0;
 };
 
 template <int L, bool COUNTED>
@@ -537,9 +541,10 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 uint32_t *gflag = (uint32_t *)c.ws.get(Workspace::MSD_OVF, ngroups * 4);
                 HIP_CHECK(hipMemsetAsync(gflag, 0, ngroups * 4, c.stream));
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+                uint64_t *istart = rm->istart && rm->ib >= b ? rm->istart : nullptr;
                 local_merge_kernel<L, COUNTED, CAP><<<dim3((unsigned)ngroups), dim3(512), 0, c.stream>>>(
                     *keys, COUNTED ? *vals : nullptr, gstart, gbucket, nullptr, rm->ck, rm->cv, cstart, rm->out,
-                    rm->outc, gflag, &c.small->counter);
+                    rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart);
                 HIP_CHECK(hipGetLastError());
                 uint32_t novf = 0;
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
@@ -555,7 +560,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                     HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
                     local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
                         *keys, COUNTED ? *vals : nullptr, gstart, gbucket, dlist, rm->ck, rm->cv, cstart, rm->out,
-                        rm->outc, gflag, &c.small->counter);
+                        rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart);
                     HIP_CHECK(hipGetLastError());
                     HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
                     HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
@@ -563,6 +568,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 }
                 if (!novf) {
                     rm->done = true;
+                    if (istart) {  // index end = the merged count
+                        const uint64_t R = n + rm->nc;
+                        HIP_CHECK(hipMemcpyAsync(istart + (1ull << rm->ib), &R, 8, hipMemcpyHostToDevice, c.stream));
+                        HIP_CHECK(hipStreamSynchronize(c.stream));  // R is a host local
+                        note_bucket_index(c, rm->out, R, istart, nbits - rm->ib);
+                    }
                     return n;  // the rc keys (distinct); rm->out holds U + n
                 }
             }
@@ -1133,10 +1144,12 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
     const unsigned bshift = 2 * K - B;
     const uint64_t nb = 1ull << B;
     uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nb + 2) * 8);
-    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
-    bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
-    HIP_CHECK(hipGetLastError());
-    note_bucket_index(c, ka, R, bstart, bshift);
+    if (!(c.bidx_keys == (const void *)ka && c.bidx_n == R && c.bidx_shift == bshift && c.bidx == bstart)) {
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
+        bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
+        HIP_CHECK(hipGetLastError());
+        note_bucket_index(c, ka, R, bstart, bshift);
+    }
     uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
     uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
     const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
@@ -1341,6 +1354,11 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         K2 *real = (K2 *)c.ws.get(Workspace::REAL, 2 * U * sizeof(K2));
         uint32_t *realc = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, 2 * U * 4) : nullptr;
         RcMerge<L2> rm{ka, ca, U, real, realc};
+        // the dummy stage's bucket index (stage_dummies_local) comes out of the fused merge, sized
+        // for R = 2U (odd K; even K loses its palindromes, and the dummy stage rebuilds the index
+        // when that changes its size)
+        rm.ib = bucket_bits<L2>(2 * U, 2 * K);
+        rm.istart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << rm.ib) + 2) * 8);
         const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc, &rm);
         R = U + Urc;
         if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, rk, rkc, Urc, K, real, realc, 0);

@@ -683,7 +683,10 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals, const uint64_t *__restrict__ gstart,
     const uint64_t *__restrict__ gbucket, const uint32_t *__restrict__ glist, const Key<L> *__restrict__ ck,
     const uint32_t *__restrict__ cv, const uint64_t *__restrict__ cstart, Key<L> *__restrict__ out,
-    uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf) {
+    uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf,
+    unsigned b, unsigned nbits, unsigned ib, uint64_t *__restrict__ istart) {
+    // istart (optional): the bucket index over the top ib >= b bits of the merged output that the
+    // dummy stage uses (bucket_index_kernel's layout); the group fills the entries of its range
     __shared__ Key<L> s_r[CAP];  // rc keys, then sorted
     __shared__ Key<L> s_s[CAP];  // rc keys by sub-bucket
     __shared__ Key<L> s_c[CAP];  // canonical keys of the range
@@ -770,17 +773,34 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     }
     uint32_t i = lo, j = o0 - lo;
     const uint64_t base = c0 + g0;
+    const unsigned ishift = nbits - ib;
+    // index bucket of the output before o0 (or the first bucket of the group's range - 1)
+    const uint64_t ifirst = gbucket[g] << (ib - b), iend = gbucket[g + 1] << (ib - b);
+    uint64_t prevb = ifirst - 1;
+    if (istart && o0 > 0 && o0 < o1) {
+        const uint32_t pi = lo, pj = o0 - lo;  // the merged element o0 - 1
+        const bool pr = pi > 0 && (pj == 0 || s_c[pj - 1] < s_r[pi - 1]);
+        prevb = bits_at(shr(pr ? s_r[pi - 1] : s_c[pj - 1], ishift), 0, 32);
+    }
     for (uint32_t o = o0; o < o1; ++o) {
         const bool take_r = i < nr && (j >= nc || s_r[i] < s_c[j]);
-        if (take_r) {
-            out[base + o] = s_r[i];
-            if (COUNTED) outc[base + o] = s_rv[i];
-            ++i;
-        } else {
-            out[base + o] = s_c[j];
-            if (COUNTED) outc[base + o] = s_cv[j];
-            ++j;
+        const Key<L> key = take_r ? s_r[i] : s_c[j];
+        out[base + o] = key;
+        if (COUNTED) outc[base + o] = take_r ? s_rv[i] : s_cv[j];
+        if (take_r) ++i; else ++j;
+        if (istart) {
+            const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
+            for (uint64_t x = prevb + 1; x <= kb; ++x) istart[x] = base + o;
+            prevb = kb;
         }
+    }
+    if (istart) {  // after the group's last key, up to the end of its range
+        uint64_t lastb = ifirst - 1;
+        if (n) {
+            const Key<L> lk = nr && (nc == 0 || s_c[nc - 1] < s_r[nr - 1]) ? s_r[nr - 1] : s_c[nc - 1];
+            lastb = bits_at(shr(lk, ishift), 0, 32);
+        }
+        for (uint64_t x = lastb + 1 + tid; x < iend; x += LB) istart[x] = base + n;
     }
 }
 
