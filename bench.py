@@ -36,6 +36,9 @@ CONFIGS = {
     "cfg2": {"k": 31, "reads": 10_000_000},
     "cfg3": {"k": 63, "reads": 100_000_000, "host_steps": 0, "cpu_sample_reads": 500_000,
              "steps": 2, "warmup": 1},
+    # configs[4]'s counting path (--count-kmers: SortedMultiset<uint8_t> saturating merge, 8-bit
+    # weights) on the cfg2 reads; the KMC1 input of that config is parity-tested (tests/test_kmc.py)
+    "cfg5": {"k": 31, "reads": 10_000_000, "count_width": 8, "fasta_reads": 0},
 }
 
 

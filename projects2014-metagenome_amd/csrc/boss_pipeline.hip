@@ -2074,19 +2074,11 @@ static void split_fasta_files(mtg_boss_ctor *c, uint8_t *dseq, uint64_t *seq_bas
         uint64_t *oa = (uint64_t *)x.ws.get(Workspace::FA_OA, (nt + 1) * 8);
         uint64_t *ob = (uint64_t *)x.ws.get(Workspace::FA_OB, (nt + 1) * 8);
         HIP_CHECK(hipMemcpyAsync(raw, f.data, n, hipMemcpyHostToDevice, s));
-        unsigned long long first = ~0ull;
-        if (!f.fastq) {
-            HIP_CHECK(hipMemcpyAsync(&x.small->total, &first, 8, hipMemcpyHostToDevice, s));
-            fasta_first_header_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(n, 256), 8192)), dim3(256), 0, s>>>(
-                raw, n, &x.small->total);
-            HIP_CHECK(hipGetLastError());
-        }
         fasta_stats_kernel<<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(raw, n, tlast, ta);
         HIP_CHECK(hipGetLastError());
         fasta_prefix_kernel<<<1, 1024, 0, s>>>(tlast, ta, nullptr, nt, prev, oa, nullptr);  // prev nl, lines
         HIP_CHECK(hipGetLastError());
-        if (!f.fastq) first = read_u64(x, &x.small->total);
-        const uint64_t fh = f.fastq ? 0 : first;
+        const uint64_t fh = f.fastq ? 0 : f.first_header;
         fasta_split_kernel<false><<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(
             raw, n, f.fastq ? 1 : 0, fh, prev, oa, ta, tb, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0);
         HIP_CHECK(hipGetLastError());

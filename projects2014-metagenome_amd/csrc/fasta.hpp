@@ -22,6 +22,7 @@
 #include <zlib.h>
 
 #include <cstdio>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -39,6 +40,7 @@ struct FastaInput {
     char *data = nullptr;
     uint64_t size = 0;
     bool fastq = false;
+    uint64_t first_header = 0;  // FASTA: the first '>' at a line start (bytes before it are skipped)
     std::string path;
 };
 
@@ -95,6 +97,14 @@ inline FastaInput load_fasta_file(const std::string &path) {
     uint64_t i = 0;
     while (i < size && (buf[i] == '\n' || buf[i] == '\r' || buf[i] == ' ')) ++i;
     in.fastq = i < size && buf[i] == '@';
+    if (!in.fastq) {  // the first header: almost always byte 0, else a host scan
+        uint64_t p = 0;
+        while (p < size && !(buf[p] == '>' && (p == 0 || buf[p - 1] == '\n'))) {
+            const void *nl = std::memchr(buf + p, '\n', size - p);
+            p = nl ? (uint64_t)((const char *)nl - buf) + 1 : size;
+        }
+        in.first_header = p;
+    }
     return in;
 }
 
@@ -316,18 +326,6 @@ __global__ __launch_bounds__(FA_BLOCK) void fasta_split_kernel(
         }
         __syncthreads();
         for (uint32_t q = tid; q < ktot; q += FA_BLOCK) out[ob + q] = s_out[q];
-    }
-}
-
-// first FASTA header: min i with raw[i] == '>' at a line start
-__global__ __launch_bounds__(256) void fasta_first_header_kernel(const uint8_t *__restrict__ raw, uint64_t n,
-                                                                 unsigned long long *__restrict__ first) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        if (raw[i] == '>' && (i == 0 || raw[i - 1] == '\n')) {
-            atomicMin(first, (unsigned long long)i);
-            return;
-        }
     }
 }
 

@@ -45,7 +45,7 @@ for r in rows:
                                                     (r["read_bytes"] + r["write_bytes"]) / 1e9))
 open(prefix + "_pmc_traffic.md", "w").write("\n".join(lines) + "\n")
 # the sort's first partition launch (K1 performs level 1 when fused, so this is level 2)
-part = [r for r in rows if r["kernel"].startswith("mtg::msd_partition_kernel<1, false, false")][0]
+part = [r for r in rows if r["kernel"].startswith("mtg::msd_partition_kernel<1, false")][0]
 json.dump({"kernel": part["kernel"], "hbm_bytes_per_launch": part["read_bytes"] + part["write_bytes"],
            "read_bytes": part["read_bytes"], "write_bytes": part["write_bytes"],
            "fetch_scale": fetch_scale, "write_scale": write_scale,
