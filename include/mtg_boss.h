@@ -252,6 +252,9 @@ int mtg_device_free(void *ptr);
 int mtg_memcpy_h2d(void *dst, const void *src, uint64_t bytes);
 int mtg_memcpy_d2h(void *dst, const void *src, uint64_t bytes);
 int mtg_device_count(void);
+/* device-to-device copy of `bytes` (multiple of 16, 16-byte aligned) by a streaming 16-byte-lane
+   kernel on `stream` (NULL = default): the bench's achievable-HBM-bandwidth probe */
+int mtg_device_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 int mtg_device_synchronize(int device_id);
 
 #ifdef __cplusplus

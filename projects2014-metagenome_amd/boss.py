@@ -84,7 +84,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
            "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
            "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free",
-           "mtg_boss_ctor_add_fasta")
+           "mtg_boss_ctor_add_fasta", "mtg_device_copy")
 
 COMM_ID_BYTES = 128
 
@@ -147,6 +147,7 @@ def lib():
                                       P(ctypes.c_uint64)]
         L.mtg_dna_encode_table.argtypes = [ctypes.c_char_p]
         L.mtg_boss_ctor_add_fasta.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.mtg_device_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         L.mtg_boss_write_dbg.argtypes = [P(_Chunk), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int64, P(ctypes.c_uint64)]
         L.mtg_boss_read_dbg.argtypes = [ctypes.c_char_p, P(_DbgFile)]

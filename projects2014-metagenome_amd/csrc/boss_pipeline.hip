@@ -2456,6 +2456,32 @@ int mtg_memcpy_d2h(void *dst, const void *src, uint64_t bytes) {
     return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
 }
 
+// streaming copy: 4 x 16 B in flight per thread per iteration, grid-stride
+__global__ __launch_bounds__(256) void copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+int mtg_device_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
+    if (!dst || !src || (bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15)) return MTG_ERR_ARGUMENT;
+    const uint64_t n = bytes / 16;
+    if (!n) return MTG_OK;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(n, 256), (uint64_t)cus * 16);
+    copy16_kernel<<<dim3(grid), dim3(256), 0, (hipStream_t)stream>>>((const uint4 *)src, (uint4 *)dst, n);
+    return hipGetLastError() == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
+}
+
 int mtg_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
