@@ -258,8 +258,8 @@ def fasta_path(args, kb, boss, steps, n_reads, files=8):
 
 
 def measured_copy_peak(torch, boss, device, nbytes=4 << 30, reps=10):
-    """Achievable HBM bandwidth on this GPU: the library's streaming 16-byte-lane copy kernel
-    (mtg_device_copy) over `nbytes` (read + write), timed with HIP events on torch's current
+    """Achievable HBM bandwidth on this GPU: the library's one-shot nontemporal 16-byte-lane copy
+    kernel (mtg_device_copy; tools/copy_bench.hip compares copy shapes) over `nbytes` (read + write), timed with HIP events on torch's current
     stream; the second roofline denominator BASELINE.md asks for (the best of torch's copy_ and
     that kernel)."""
     src = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -418,7 +418,7 @@ def main():
                      "traffic_source": traffic_src,
                      "peak_measured": copy_peak,
                      "frac_measured": achieved / copy_peak if copy_peak else None,
-                     "peak_measured_how": "best of a streaming 16-byte-lane copy kernel and torch copy_ "
+                     "peak_measured_how": "best of a one-shot nontemporal 16-byte-lane copy kernel and torch copy_ "
                                           "over 4 GiB (read + write), HIP events",
                      "kernel": "msd_partition_kernel (K2 level-2 MSD partition pass; level 1 runs "
                                "inside the fused K1 extract_partition_kernel)",

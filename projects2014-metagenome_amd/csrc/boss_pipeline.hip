@@ -437,9 +437,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         if (!COUNTED && bb - bp > 8) {  // wide digits: 1024-thread tiles keep the bucket runs long
             if constexpr (!COUNTED) {
                 constexpr int TILE2 = MsdTraits<L>::ITEMS * 1024;
-                msd_partition_kernel<L, false, 1024><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
-                                                       c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits, bb, bp,
-                                                                   cur);
+                msd_partition_kernel<L, false, 1024, true><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
+                                                             c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits, bb,
+                                                                         bp, cur);
             }
         } else {
             msd_partition_kernel<L, COUNTED><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
@@ -2457,27 +2457,35 @@ int mtg_memcpy_d2h(void *dst, const void *src, uint64_t bytes) {
 }
 
 // streaming copy: 4 x 16 B in flight per thread per iteration, grid-stride
+// One-shot streaming copy: each thread moves 4 x 16 B at block-strided offsets (every load and
+// store instruction is a fully coalesced 16 KiB per workgroup) with nontemporal loads and stores.
+// Measured on MI355X (tools/copy_bench.hip, 4 GiB): 6.0 TB/s, against 4.9 TB/s for a grid-stride
+// loop and for hipMemcpyAsync D2D -- the bench's achievable-bandwidth figure.
 __global__ __launch_bounds__(256) void copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
-    }
-    for (; i < n; i += stride) dst[i] = src[i];
+    const uint64_t b0 = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    uint64_t v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (b0 + 256 * q < n) {
+            const uint64_t *p = reinterpret_cast<const uint64_t *>(src + b0 + 256 * q);
+            v[2 * q] = __builtin_nontemporal_load(p);
+            v[2 * q + 1] = __builtin_nontemporal_load(p + 1);
+        }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (b0 + 256 * q < n) {
+            uint64_t *p = reinterpret_cast<uint64_t *>(dst + b0 + 256 * q);
+            __builtin_nontemporal_store(v[2 * q], p);
+            __builtin_nontemporal_store(v[2 * q + 1], p + 1);
+        }
 }
 
 int mtg_device_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!dst || !src || (bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15)) return MTG_ERR_ARGUMENT;
     const uint64_t n = bytes / 16;
     if (!n) return MTG_OK;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(n, 256), (uint64_t)cus * 16);
+    if (ceil_div(n, 1024) > 0x7fffffffull) return MTG_ERR_ARGUMENT;
+    const unsigned grid = (unsigned)ceil_div(n, 1024);
     copy16_kernel<<<dim3(grid), dim3(256), 0, (hipStream_t)stream>>>((const uint4 *)src, (uint4 *)dst, n);
     return hipGetLastError() == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
 }

@@ -166,11 +166,32 @@ __global__ __launch_bounds__(512) void scan_counts_kernel(const uint32_t *__rest
  * and each run is written contiguously.  Keys outside the tile's LDS window (tiles spanning
  * more than MSD_WIN tiny segments) take one atomic each.
  */
-template <int L, bool HAS_VAL, int BLOCK = MSD_BLOCK>
+template <int L>
+__device__ __forceinline__ Key<L> load_key(const Key<L> *p, bool nt) {
+    if (!nt) return *p;
+    Key<L> k;
+#pragma unroll
+    for (int i = 0; i < L; ++i) k.w[i] = __builtin_nontemporal_load(&p->w[i]);
+    return k;
+}
+
+template <int L>
+__device__ __forceinline__ void store_key(Key<L> *p, const Key<L> &k, bool nt) {
+    if (nt) {
+#pragma unroll
+        for (int i = 0; i < L; ++i) __builtin_nontemporal_store(k.w[i], &p->w[i]);
+    } else {
+        *p = k;
+    }
+}
+
+template <int L, bool HAS_VAL, int BLOCK = MSD_BLOCK, bool NT = false>
 __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
     unsigned long long *__restrict__ cursor, unsigned cstride = 1) {
+    // NT: nontemporal loads and stores (the streaming wide-digit pass: nothing it touches is
+    // re-read from L2; measured 4.65 vs 4.67 ms on the cfg2 pass)
     constexpr int ITEMS = MsdTraits<L>::ITEMS;
     constexpr int TILE = ITEMS * BLOCK;
     constexpr int WMAX = MSD_WIN << 8;
@@ -198,7 +219,7 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
         const uint64_t i = base + (uint64_t)j * BLOCK + tid;
         have[j] = i < n;
         if (i < n) {
-            k[j] = kin[i];
+            k[j] = load_key(kin + i, NT);
             if (HAS_VAL) v[j] = vin[i];
         }
     }
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
         const Key<L> key = s_keys[p];
         const uint32_t lb = key_prefix(key, nbits, b) - wbase;
         const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
-        kout[o] = key;
+        store_key(kout + o, key, NT);
         if (HAS_VAL) vout[o] = s_vals[p];
     }
 }
