@@ -136,6 +136,30 @@ static void radix_sort_records(void *keys, size_t esz, uint32_t *cnt, size_t n) 
     }
 }
 
+/* KmerExtractorBOSS codes -- kmer/alphabets.hpp:68-77: A C G T/U (either case) -> 1..4, else 5 */
+static uint8_t boss_code(char ch) {
+    switch (ch) {
+        case 'A': case 'a': return 1;
+        case 'C': case 'c': return 2;
+        case 'G': case 'g': return 3;
+        case 'T': case 't': case 'U': case 'u': return 4;
+        default: return 5;
+    }
+}
+
+/* COMPL_TAB of common/seq_tools/reverse_complement.hpp on the chars that encode as valid: the
+   table maps no other char onto A C G T U, so the rest stays invalid whatever it becomes */
+static char compl_char(char ch) {
+    switch (ch) {
+        case 'A': return 'T'; case 'a': return 't';
+        case 'C': return 'G'; case 'c': return 'g';
+        case 'G': return 'C'; case 'g': return 'c';
+        case 'T': case 'U': return 'A';
+        case 't': case 'u': return 'a';
+        default: return 'N';
+    }
+}
+
 #include "oracle_words.h"
 
 #define T2 u64
@@ -221,6 +245,27 @@ int oracle_build_chunk(uint64_t k, int canonical, int bits_per_count, const char
 int oracle_build_chunk_from_kmers(uint64_t k, int canonical, int bits_per_count,
                                   const oracle_keys *kmers, oracle_chunk *out) {
     return dispatch(3, k, canonical, bits_per_count, NULL, NULL, NULL, 0, kmers, NULL, out);
+}
+
+int oracle_build_suffix_chunk(uint64_t k, int both_strands, int bits_per_count, const char *suffix,
+                              const char *seq, const uint64_t *offsets, const uint64_t *counts,
+                              uint64_t n_seqs, oracle_chunk *out) {
+    if (k < 1 || k > 84) { set_error("k must be in [1, 84]"); return -1; }
+    if (bits_per_count < 0 || bits_per_count > 32) {
+        set_error("bits_per_count must be in [0, 32]");
+        return -1;
+    }
+    size_t ns = suffix ? strlen(suffix) : 0;
+    if (!ns || ns >= k + 1) { set_error("the suffix must be non-empty and shorter than k + 1"); return -1; }
+    uint8_t enc[96];
+    for (size_t i = 0; i < ns; ++i) enc[i] = suffix[i] == '$' ? 0 : boss_code(suffix[i]);
+    memset(out, 0, sizeof(*out));
+    const uint64_t K = k + 1;
+    if (3 * K <= 64)
+        return suffix_run_u64_u64(k, both_strands, bits_per_count, enc, ns, seq, offsets, counts, n_seqs, out);
+    if (3 * K <= 128)
+        return suffix_run_u128_u128(k, both_strands, bits_per_count, enc, ns, seq, offsets, counts, n_seqs, out);
+    return suffix_run_u256_u256(k, both_strands, bits_per_count, enc, ns, seq, offsets, counts, n_seqs, out);
 }
 
 void oracle_pack_kmer(const uint8_t *codes, uint64_t len, uint32_t bits_per_char,

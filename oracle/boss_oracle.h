@@ -78,6 +78,13 @@ int oracle_build_chunk(uint64_t k, int canonical, int bits_per_count,
 int oracle_build_chunk_from_kmers(uint64_t k, int canonical, int bits_per_count,
                                   const oracle_keys *kmers, oracle_chunk *out);
 
+/* the suffix-filtered route: IBOSSChunkConstructor::initialize(k, both_strands, bits_per_count,
+ * suffix) + build_chunk (boss_chunk_construct.cpp:946-1013): BOSS::Chunk of the `$`-padded
+ * (k+1)-mers whose node ends with `suffix` (chars of "$ACGT", shorter than k + 1) */
+int oracle_build_suffix_chunk(uint64_t k, int both_strands, int bits_per_count, const char *suffix,
+                              const char *seq, const uint64_t *offsets, const uint64_t *counts,
+                              uint64_t n_seqs, oracle_chunk *out);
+
 /* building blocks (unit-level KATs) */
 void oracle_pack_kmer(const uint8_t *codes, uint64_t len, uint32_t bits_per_char,
                       uint32_t limbs, uint64_t *out_words);

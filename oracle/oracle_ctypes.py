@@ -53,6 +53,9 @@ def lib():
             f.restype = ctypes.c_int
         L.oracle_build_chunk.argtypes = seq_args + [ctypes.POINTER(OracleChunk)]
         L.oracle_build_chunk.restype = ctypes.c_int
+        L.oracle_build_suffix_chunk.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_char_p] + seq_args[3:] + [ctypes.POINTER(OracleChunk)]
+        L.oracle_build_suffix_chunk.restype = ctypes.c_int
         L.oracle_build_chunk_from_kmers.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                                     ctypes.POINTER(OracleKeys),
                                                     ctypes.POINTER(OracleChunk)]
@@ -142,6 +145,21 @@ class Chunk:
 def build_chunk(k, seqs, canonical=False, bits_per_count=0, counts=None):
     out = OracleChunk()
     _seq_call(lib().oracle_build_chunk, k, canonical, bits_per_count, seqs, counts, out)
+    return Chunk(out)
+
+
+def build_suffix_chunk(k, seqs, suffix, both_strands=False, bits_per_count=0, counts=None):
+    """The suffix-filtered route (boss_chunk_construct.cpp:946-1013) for one filter suffix."""
+    data, offsets = pack_sequences(seqs)
+    cnt = None if counts is None else np.ascontiguousarray(counts, dtype=np.uint64)
+    out = OracleChunk()
+    rc = lib().oracle_build_suffix_chunk(
+        k, int(bool(both_strands)), bits_per_count, suffix.encode(), data,
+        offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+        cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None,
+        len(seqs), ctypes.byref(out))
+    if rc != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
     return Chunk(out)
 
 

@@ -229,9 +229,12 @@ class Chunk:
             raise ValueError("ERROR: only the DNA alphabet of size 5 is supported")
         return cls(k, W, last, F, weights, bits_per_count=bits)
 
-    def write_dbg(self, outbase, canonical=False, mask_dummy=False, suffix_length=-1):
+    def write_dbg(self, outbase, canonical=False, mask_dummy=False, suffix_length=-1, prune=False):
         """The files `metagraph build` writes from this chunk (cli/build.cpp:323-352):
         <outbase>.dbg, <outbase>.edgemask (mask_dummy) and <outbase>.dbg.weights (weighted).
+        prune=True is `metagraph concatenate --clear-dummy` (cli/build.cpp:400-405): the
+        redundant source dummies of suffix-built chunks are erased before writing, the mask is
+        written, and no weights file (build_boss_from_chunks takes none).
         Returns the valid edges after masking (`nodes (k)` of `metagraph stats`), else rows - 1."""
         W = np.ascontiguousarray(self.W, dtype=np.uint8)
         last = self._last_words if self._last_words is not None else pack_last(self.last)
@@ -245,7 +248,8 @@ class Chunk:
             c.weights = wts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
         nv = ctypes.c_uint64(0)
         _check(lib().mtg_boss_write_dbg(ctypes.byref(c), os.fsencode(outbase), int(bool(canonical)),
-                                        int(bool(mask_dummy)), int(suffix_length), ctypes.byref(nv)))
+                                        2 if prune else int(bool(mask_dummy)), int(suffix_length),
+                                        ctypes.byref(nv)))
         return nv.value
 
     def extend(self, other):
@@ -261,6 +265,23 @@ class Chunk:
         self.F = self.F + other.F
         if self.weights is not None:
             self.weights = np.concatenate([self.weights, other.weights[1:]])
+
+
+def generate_suffixes(length):
+    """KmerExtractorBOSS::generate_suffixes (kmer/kmer_extractor.cpp:402-416): the node suffixes
+    of `build --suffix-len` in BOSS order (last char slowest, common/utils/string_utils.cpp:82-95),
+    keeping those whose '$'s form a prefix.  Building one chunk per suffix (filter_suffix) and
+    concatenating them in this order gives the graph (cli/build.cpp:102-155)."""
+    out = [""]
+    while len(out[0]) < length:
+        head = out.pop(0)
+        out.extend(c + head for c in "$ACGT")
+    res = []
+    for s in out:
+        j = s.rfind("$")
+        if j < 0 or s[:j + 1] == "$" * (j + 1):
+            res.append(s)
+    return res
 
 
 class BOSSChunkConstructor:

@@ -28,6 +28,7 @@
 #include "extract_partition.hpp"
 #include "fasta.hpp"
 #include "range_extract.hpp"
+#include "suffix_extract.hpp"
 #include "host_stage.hpp"
 #include "kmc.hpp"
 #include "msd_sort.hpp"
@@ -1183,6 +1184,10 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
     return sort_unique_dummies<L3>(c, K, da, db, Draw, dk);
 }
 
+template <int L3, bool COUNTED>
+static void emit_stream(Ctx &c, unsigned k, uint32_t wmax, const Key<L3> *sk, const uint32_t *sc, uint64_t M,
+                        uint64_t R, BuildOutput *out);
+
 // K7 + K8: lift + merge the real edges with the sorted dummies (behind the main dummy row when
 // `root`), then W / last / F / weights.  Rows go to out[1..]; out row 0 is the leading row.
 template <int L2, int L3, bool COUNTED>
@@ -1246,7 +1251,14 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
     merge_sorted<L3, L2, true, COUNTED, false>(c, real, realc, R, dk, nullptr, D, K, sk, sc, root ? 1 : 0);
     debug_check_sorted(c, "merged stream", sk, M);
     *ev_merge = tm.mark();
+    emit_stream<L3, COUNTED>(c, k, wmax, sk, sc, M, R, out);
+}
 
+// K8 over a sorted lifted stream sk[0..M) (+ counts): initialize_chunk (boss_chunk.cpp:32-133),
+// rows to out[1..], compacted past redundant dummy sinks when there are any
+template <int L3, bool COUNTED>
+static void emit_stream(Ctx &c, unsigned k, uint32_t wmax, const Key<L3> *sk, const uint32_t *sc, uint64_t M,
+                        uint64_t R, BuildOutput *out) {
     uint8_t *W = (uint8_t *)c.ws.get(Workspace::OW, M + 1);
     uint8_t *last = (uint8_t *)c.ws.get(Workspace::OLAST, M + 1);
     uint32_t *weights = COUNTED ? (uint32_t *)c.ws.get(Workspace::OWEIGHTS, (M + 1) * 4) : nullptr;
@@ -1837,6 +1849,134 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     T.peak_bytes = c.ws.held();
 }
 
+// ------------------------------------------------------------------ suffix-filtered route
+//
+// IBOSSChunkConstructor with a non-empty filter suffix (boss_chunk_construct.cpp:946-1013): the
+// (k+1)-mers of the `$`-padded read segments whose node ends with the suffix, both strands in
+// BOTH mode (suffix_extract.hpp), sorted and deduplicated (counts added with saturation), then
+// initialize_chunk over that set as it is -- the padding supplies the dummy edges, so there is
+// no dummy reconstruction.  The chunk of the all-`$` suffix also holds the main dummy edge
+// (:977-980).  The chunks of all suffixes concatenate (in suffix order) into the graph
+// (cli/build.cpp:359-456; mtg_boss_concatenate prunes their redundant source dummies).
+template <int L3, bool COUNTED>
+static void run_suffix(Ctx &c, unsigned k, bool both, unsigned bits, const SuffixSpec &suf, bool all_sentinel,
+                       const BuildInput &in, BuildOutput *out) {
+    using K3 = Key<L3>;
+    using T = SuffixTraits;
+    const unsigned K = k + 1;
+    const unsigned cbits = bits <= 8 ? 8 : bits <= 16 ? 16 : 32;
+    const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+    const uint32_t wmax = bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << bits) - 1);
+    mtg_boss_timings &Tm = c.timings;
+    Tm = mtg_boss_timings{};
+    Tm.world = 1;
+    Tm.n_batches = 1;
+    HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
+    EventTimer tm(c.stream);
+    const int ev_start = tm.mark();
+
+    // ---- K1: count -> scan -> write over identical tiles of buffer positions
+    const uint64_t tiles = ceil_div(in.seq_len + 1, T::TILE);
+    uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
+    uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
+    suffix_extract_kernel<L3, COUNTED, true><<<dim3((unsigned)tiles), dim3(T::BLOCK), 0, c.stream>>>(
+        in.seq, in.seq_len, K, both ? 1 : 0, suf, in.read_starts, in.read_counts, in.n_reads, cmax, tcnt,
+        nullptr, nullptr, nullptr);
+    HIP_CHECK(hipGetLastError());
+    {
+        uint32_t ep;
+        const uint64_t st = ceil_div(tiles, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, tiles, toff, desc, ep,
+                                                                          &c.small->counter, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+    }
+    uint64_t N = read_u64(c, (const unsigned long long *)(toff + tiles));
+    Tm.n_positions = in.seq_len;
+    const uint64_t cap = N + (all_sentinel ? 1 : 0);
+    K3 *ka = (K3 *)c.ws.get(Workspace::KA, std::max<uint64_t>(cap, 1) * sizeof(K3));
+    K3 *kb = (K3 *)c.ws.get(Workspace::KB, std::max<uint64_t>(cap, 1) * sizeof(K3));
+    uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(cap, 1) * 4) : nullptr;
+    uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(cap, 1) * 4) : nullptr;
+    if (N) {
+        suffix_extract_kernel<L3, COUNTED, false><<<dim3((unsigned)tiles), dim3(T::BLOCK), 0, c.stream>>>(
+            in.seq, in.seq_len, K, both ? 1 : 0, suf, in.read_starts, in.read_counts, in.n_reads, cmax, nullptr,
+            toff, ka, ca);
+        HIP_CHECK(hipGetLastError());
+    }
+    if (all_sentinel) {  // add_kmer(k+1 sentinels): the main dummy edge, count 1
+        HIP_CHECK(hipMemsetAsync(ka + N, 0, sizeof(K3), c.stream));
+        if (COUNTED) {
+            const uint32_t one = 1;
+            HIP_CHECK(hipMemcpyAsync(ca + N, &one, 4, hipMemcpyHostToDevice, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+        }
+        ++N;
+    }
+    Tm.n_extracted = N;
+    const int ev_extract = tm.mark();
+
+    // ---- sort + unique / saturating count merge of the lifted keys (LSD over 3K bits)
+    radix_sort<L3, COUNTED>(c, &ka, &kb, &ca, &cb, N, 3 * K, false);
+    uint64_t U = 0;
+    reset_small(c);
+    if (N) {
+        const uint64_t utiles = ceil_div(N, 2048);
+        uint32_t desc_ep;
+        uint64_t *desc = acquire_desc(c, utiles, &desc_ep);
+        unsigned long long *sums = nullptr;
+        if (COUNTED) {
+            sums = (unsigned long long *)c.ws.get(Workspace::SUMS, N * 8);
+            HIP_CHECK(hipMemsetAsync(sums, 0, N * 8, c.stream));
+        }
+        unique_kernel<L3, COUNTED><<<dim3((unsigned)utiles), dim3(256), 0, c.stream>>>(
+            ka, ca, N, kb, sums, desc, desc_ep, &c.small->counter, &c.small->total, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        U = read_u64(c, &c.small->total);
+        if (COUNTED && U) {
+            count_clamp_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(U, 256), 4096))),
+                                 dim3(256), 0, c.stream>>>(sums, U, cmax, cb);
+            HIP_CHECK(hipGetLastError());
+        }
+        std::swap(ka, kb);
+        std::swap(ca, cb);
+    }
+    Tm.n_unique = U;
+    debug_check_sorted(c, "suffix k-mers", ka, U);
+    const int ev_sort = tm.mark();
+
+    // ---- K8 over the set as it is
+    emit_stream<L3, COUNTED>(c, k, wmax, ka, ca, U, U, out);
+    const int ev_emit = tm.mark();
+    check_error_word(c);
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    Tm.n_real = out->n ? out->n - 1 : 0;
+    Tm.n_dummy = 0;
+    Tm.n_rows = out->n;
+    Tm.extract_ms = tm.ms(ev_start, ev_extract);
+    Tm.sort_ms = tm.ms(ev_extract, ev_sort);
+    Tm.emit_ms = tm.ms(ev_sort, ev_emit);
+    Tm.total_ms = tm.ms(ev_start, ev_emit);
+    Tm.peak_bytes = c.ws.held();
+}
+
+// word choice of the suffix route: lifted keys by (k+1)*3 (boss_chunk_construct.cpp:1080-1091)
+static void run_suffix_dispatch(Ctx &c, unsigned k, bool both, unsigned bits, const SuffixSpec &suf,
+                                bool all_sentinel, const BuildInput &in, BuildOutput *out) {
+    const unsigned K = k + 1;
+    if (3 * K <= 64) {
+        if (bits) run_suffix<1, true>(c, k, both, bits, suf, all_sentinel, in, out);
+        else run_suffix<1, false>(c, k, both, bits, suf, all_sentinel, in, out);
+    } else if (3 * K <= 128) {
+        if (bits) run_suffix<2, true>(c, k, both, bits, suf, all_sentinel, in, out);
+        else run_suffix<2, false>(c, k, both, bits, suf, all_sentinel, in, out);
+    } else {
+        if (bits) run_suffix<4, true>(c, k, both, bits, suf, all_sentinel, in, out);
+        else run_suffix<4, false>(c, k, both, bits, suf, all_sentinel, in, out);
+    }
+}
+
 template <int L2, int L3>
 static void run_counted(Ctx &c, Comm *comm, unsigned k, bool canonical, unsigned bits, const BuildInput &in,
                         BuildOutput *out) {
@@ -1921,9 +2061,13 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         set_error("Error: trying to allocate too many bits per k-mer count");
         return nullptr;
     }
-    if ((p->filter_suffix && p->filter_suffix[0]) ||
-        (p->container_type != MTG_CONTAINER_VECTOR && p->container_type != MTG_CONTAINER_VECTOR_DISK)) {
-        set_error("a suffix filter or an unknown container does not run on the GPU path");
+    if (p->container_type != MTG_CONTAINER_VECTOR && p->container_type != MTG_CONTAINER_VECTOR_DISK) {
+        set_error("an unknown container does not run on the GPU path");
+        return nullptr;
+    }
+    const std::string suffix = p->filter_suffix ? p->filter_suffix : "";
+    if (suffix.size() >= p->k + 1) {  // kmer_extractor.cpp:325: the suffix excludes the last char
+        set_error("the filter suffix must be shorter than k + 1");
         return nullptr;
     }
     int ndev = 0;
@@ -1933,6 +2077,8 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
     }
     auto *c = new mtg_boss_ctor();
     c->params = *p;
+    c->params.filter_suffix = nullptr;  // the caller's string need not outlive the call
+    c->suffix = suffix;
     c->device = p->device_id;
     try {
         HIP_CHECK(hipSetDevice(c->device));
@@ -2104,11 +2250,50 @@ static void split_fasta_files(mtg_boss_ctor *c, uint8_t *dseq, uint64_t *seq_bas
     }
 }
 
+// encode_filter_suffix_boss (boss_chunk_construct.cpp:935-945): '$' -> 0, else the BOSS code
+// of the char (kmer/alphabets.hpp:68-77: A C G T/U -> 1..4, anything else 5, which never matches)
+static mtg::SuffixSpec encode_suffix(const std::string &suffix, bool *all_sentinel) {
+    mtg::SuffixSpec spec{};
+    spec.n = (uint32_t)suffix.size();
+    *all_sentinel = !suffix.empty();
+    for (size_t i = 0; i < suffix.size(); ++i) {
+        const char ch = suffix[i];
+        uint8_t code = 5;
+        if (ch == '$') code = 0;
+        else if (ch == 'A' || ch == 'a') code = 1;
+        else if (ch == 'C' || ch == 'c') code = 2;
+        else if (ch == 'G' || ch == 'g') code = 3;
+        else if (ch == 'T' || ch == 't' || ch == 'U' || ch == 'u') code = 4;
+        spec.c[i] = code;
+        if (ch != '$') *all_sentinel = false;
+    }
+    return spec;
+}
+
+static const char *kSuffixDist =
+    "the suffix-filtered route builds one chunk per suffix on one GPU; it has no multi-GPU form";
+
+// the build on the device buffers: the suffix route or the full construction
+static void dispatch_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {
+    if (!c->suffix.empty()) {
+        bool all_sentinel = false;
+        const mtg::SuffixSpec spec = encode_suffix(c->suffix, &all_sentinel);
+        mtg::run_suffix_dispatch(c->ctx, (unsigned)c->params.k, c->params.both_strands != 0,
+                                 c->params.bits_per_count, spec, all_sentinel, in, out);
+        return;
+    }
+    run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0, c->params.bits_per_count,
+                 in, out);
+}
+
 static int run_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {
+    if (comm && !c->suffix.empty()) {
+        set_error(kSuffixDist);
+        return MTG_ERR_UNSUPPORTED;
+    }
     try {
         HIP_CHECK(hipSetDevice(c->device));
-        run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
-                     c->params.bits_per_count, in, out);
+        dispatch_build(c, comm, in, out);
         return MTG_OK;
     } catch (const std::exception &e) {
         set_error(e.what());
@@ -2152,6 +2337,10 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
     if (!c || !out) {
         set_error("bad arguments");
         return MTG_ERR_ARGUMENT;
+    }
+    if (comm && !c->suffix.empty()) {
+        set_error(kSuffixDist);
+        return MTG_ERR_UNSUPPORTED;
     }
     const auto t_start = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lock(c->mu);
@@ -2217,8 +2406,7 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         const double input_ms = ms_since(t_input);
         BuildInput in{dseq, seq_base, dstarts, dcounts, per_read ? total_reads : 0};
         BuildOutput o{};
-        run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0,
-                     c->params.bits_per_count, in, &o);
+        dispatch_build(c, comm, in, &o);
         const auto t_d2h = std::chrono::steady_clock::now();
         const uint64_t nwords = ceil_div(o.n, 64);
         uint64_t *dbits = (uint64_t *)c->ctx.ws.get(Workspace::LAST_BITS, std::max<uint64_t>(nwords, 1) * 8);
@@ -2370,7 +2558,7 @@ int mtg_boss_write_dbg(const mtg_boss_chunk *chunk, const char *outbase, int gra
     }
     try {
         const uint64_t v = dbgio::write_dbg(outbase, chunk->W, chunk->last, chunk->n, chunk->F, chunk->k,
-                                            (uint64_t)graph_mode, mask_dummy != 0, suffix_length, chunk->weights,
+                                            (uint64_t)graph_mode, mask_dummy, suffix_length, chunk->weights,
                                             chunk->bits_per_count);
         if (n_valid) *n_valid = v;
         return MTG_OK;

@@ -449,6 +449,136 @@ inline std::vector<uint64_t> valid_edges(const BossNav &b) {
     return dummy;
 }
 
+// `concatenate --clear-dummy` (cli/build.cpp:400-405): DBGSuccinct::mask_dummy_kmers(with_pruning)
+// (dbg_succinct.cpp:839-870) = BOSS::prune_and_mark_all_dummy_edges (boss.cpp:1693-1703):
+//   erase_redundant_dummy_edges (:1609-1650) -- traverse the source-dummy tree (traverse_dummy_edges,
+//     :1443-1597; the parallel split at depth min(6, k/2) visits the same tree) and mark a dummy edge
+//     redundant when no path below it reaches a depth-k edge that is the single incoming edge of its
+//     (real) target node (is_single_incoming, :725-738); erase those edges (erase_edges, :1342-1403:
+//     `last` moves to the previous kept edge of the node, a "minus" W whose first occurrence was
+//     erased loses its minus, F counts the kept rows);
+//   then the mask of the remaining source dummies plus the sinks (W == $) and row 0, flipped.
+struct Pruned {
+    std::vector<uint8_t> W;
+    std::vector<uint64_t> last;   // packed
+    uint64_t n = 0;
+    uint64_t F[5] = {0, 0, 0, 0, 0};
+    std::vector<uint64_t> valid;  // packed, over the pruned rows
+    uint64_t n_erased = 0;
+};
+
+inline Pruned prune_dummy_edges(const BossNav &b) {
+    const uint64_t n = b.n, nw = (n + 63) / 64;
+    std::vector<uint64_t> redundant(nw, 0), source(nw, 0);
+    auto setb = [](std::vector<uint64_t> &v, uint64_t i) { v[i >> 6] |= 1ull << (i & 63); };
+    auto getb = [](const std::vector<uint64_t> &v, uint64_t i) { return (v[i >> 6] >> (i & 63)) & 1; };
+    if (n > 1) setb(source, 1);
+    if (n > 2 && !bit(b.last, 1)) {
+        // single[i]: edge i is the only edge into its target -- the next W in {c, c + 5} after i
+        // is not the minus c + 5 (is_single_incoming via succ_W, boss.cpp:725-738)
+        std::vector<uint64_t> single(nw, 0);
+        uint8_t next_kind[5] = {0, 0, 0, 0, 0};  // 0 none, 1 plain, 2 minus
+        for (uint64_t i = n; i-- > 1;) {
+            const uint8_t w = b.W[i];
+            const uint8_t c = w % 5;
+            if (w >= 1 && w <= 4 && next_kind[c] != 2) setb(single, i);
+            if (c) next_kind[c] = w > 5 ? 2 : 1;
+        }
+        const uint64_t K = b.k;  // check depth: the depth-k edges enter real nodes
+        // depth-first over the tree; returns whether the edge is needed (not redundant)
+        struct Frame {
+            uint64_t first, cur;  // children rows [first, last] of the current node, cur = next child
+            uint64_t last;
+            bool any;
+        };
+        auto visit = [&](uint64_t root) {
+            // iterative DFS so deep trees (k up to 84) and wide ones need no recursion limits
+            std::vector<std::pair<uint64_t, Frame>> st;  // (edge, its children frame)
+            auto open = [&](uint64_t e, uint64_t depth) -> int {
+                // returns 1 / 0 when e is an end edge (needed / redundant), -1 when it has children
+                setb(source, e);
+                const uint8_t c = b.W[e] % 5;
+                if (depth == K || c == 0) return (c == 0 || getb(single, e)) ? 1 : 0;
+                const uint64_t le = b.fwd(e, c);
+                const uint64_t node = b.rank_last(le);
+                const uint64_t fe = b.select_last(node - 1) + 1;
+                st.push_back({e, Frame{fe, fe, le, false}});
+                return -1;
+            };
+            int r = open(root, 1);
+            if (r >= 0) {
+                if (!r) setb(redundant, root);
+                return;
+            }
+            while (!st.empty()) {
+                const size_t top = st.size() - 1;  // st[0] holds the root, at depth 1
+                if (st[top].second.cur <= st[top].second.last) {
+                    const uint64_t child = st[top].second.cur++;
+                    const int rc = open(child, top + 2);  // may push the child's frame
+                    if (rc == 1) st[top].second.any = true;
+                    else if (rc == 0) setb(redundant, child);
+                    continue;
+                }
+                const uint64_t e = st[top].first;
+                const bool needed = st[top].second.any;
+                st.pop_back();
+                if (!needed) setb(redundant, e);
+                else if (!st.empty()) st.back().second.any = true;
+            }
+        };
+        for (uint64_t root = 2; root < n; ++root) {
+            visit(root);
+            if (bit(b.last, root)) break;
+        }
+    }
+    Pruned out;
+    uint64_t erased = 0;
+    for (uint64_t w = 0; w < nw; ++w) erased += __builtin_popcountll(redundant[w]);
+    out.n_erased = erased;
+    const uint64_t m = n - erased, mw = (m + 63) / 64;
+    out.n = m;
+    out.W.resize(m);
+    out.last.assign(std::max<uint64_t>(mw, 1), 0);
+    std::vector<uint64_t> src(std::max<uint64_t>(mw, 1), 0);
+    bool first_removed[5] = {false, false, false, false, false};
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t c = b.W[i];
+        const bool li = bit(b.last, i);
+        if (getb(redundant, i)) {
+            if (c < 5) first_removed[c] = true;
+            if (li && o > 1 && !((out.last[(o - 1) >> 6] >> ((o - 1) & 63)) & 1))
+                out.last[(o - 1) >> 6] |= 1ull << ((o - 1) & 63);
+            continue;
+        }
+        out.W[o] = (c > 5 && first_removed[c % 5]) ? (uint8_t)(c % 5) : c;
+        first_removed[c % 5] = false;
+        if (li) out.last[o >> 6] |= 1ull << (o & 63);
+        if (getb(source, i)) src[o >> 6] |= 1ull << (o & 63);
+        ++o;
+    }
+    // F: the kept rows up to each old boundary
+    uint64_t F[5];
+    for (int c = 0; c < 5; ++c) F[c] = b.F[c];
+    {
+        int c = 0;
+        uint64_t count = 0;
+        for (uint64_t i = 1; i <= F[4]; ++i) {
+            while (c < 5 && i > F[c]) F[c++] = count;
+            if (!getb(redundant, i)) ++count;
+        }
+        while (c < 5) F[c++] = count;
+    }
+    for (int c = 0; c < 5; ++c) out.F[c] = F[c];
+    // mark_sink_dummy_edges on the pruned graph, row 0, flip
+    out.valid.assign(std::max<uint64_t>(mw, 1), 0);
+    for (uint64_t i = 0; i < m; ++i) {
+        const bool dummy = i == 0 || ((src[i >> 6] >> (i & 63)) & 1) || (i >= 2 && out.W[i] == 0);
+        if (!dummy) out.valid[i >> 6] |= 1ull << (i & 63);
+    }
+    return out;
+}
+
 // bit_vector_small (bit_vector_adaptive.hpp:319) restated as a type tag (BE 0 = the stat
 // representation) followed by bit_vector_stat
 inline void put_bit_vector_small(std::ostream &o, const std::vector<uint64_t> &w, uint64_t nbits) {
@@ -472,13 +602,36 @@ struct DbgFile {
     bool has_mask = false;
 };
 
+inline uint64_t write_dbg_arrays(const std::string &base, const uint8_t *W, const uint64_t *last, uint64_t n,
+                                 const uint64_t *F, uint64_t k, uint64_t mode, const std::vector<uint64_t> *valid,
+                                 int64_t suffix_length, const uint32_t *weights, unsigned bits_per_count);
+
 // `metagraph build` after construction (cli/build.cpp:323-352): optional --mask-dummy, the suffix
 // index of length min(node_suffix_length, k) (default 20 / log2(4) = 10, config.cpp:22-23), then
 // DBGSuccinct::serialize.  suffix_length < 0 selects that default.  Returns the valid edges
 // (`nodes (k)` of `metagraph stats`, stats.cpp:72-76) when masking, else n - 1.
 inline uint64_t write_dbg(const std::string &base, const uint8_t *W, const uint64_t *last, uint64_t n,
-                          const uint64_t *F, uint64_t k, uint64_t mode, bool mask_dummy, int64_t suffix_length,
+                          const uint64_t *F, uint64_t k, uint64_t mode, int mask_dummy, int64_t suffix_length,
                           const uint32_t *weights, unsigned bits_per_count) {
+    if (mask_dummy == 2) {  // concatenate --clear-dummy: prune, then write the pruned graph and its mask
+        BossNav full(W, last, n, F, k);
+        Pruned p = prune_dummy_edges(full);
+        return write_dbg_arrays(base, p.W.data(), p.last.data(), p.n, p.F, k, mode, &p.valid, suffix_length,
+                                nullptr, 0);
+    }
+    std::vector<uint64_t> valid;
+    if (mask_dummy) {
+        BossNav nav(W, last, n, F, k);
+        valid = valid_edges(nav);
+    }
+    return write_dbg_arrays(base, W, last, n, F, k, mode, mask_dummy ? &valid : nullptr, suffix_length, weights,
+                            bits_per_count);
+}
+
+// the files of one BOSS table (+ its valid-edge mask when `valid`)
+inline uint64_t write_dbg_arrays(const std::string &base, const uint8_t *W, const uint64_t *last, uint64_t n,
+                                 const uint64_t *F, uint64_t k, uint64_t mode, const std::vector<uint64_t> *valid,
+                                 int64_t suffix_length, const uint32_t *weights, unsigned bits_per_count) {
     BossNav nav(W, last, n, F, k);
     uint64_t L = suffix_length < 0 ? std::min<uint64_t>(10, k) : std::min<uint64_t>((uint64_t)suffix_length, k);
     if (L * 2 > 63) L = 0;  // "Node ranges for k-mer suffixes longer than ... cannot be indexed"
@@ -503,12 +656,11 @@ inline uint64_t write_dbg(const std::string &base, const uint8_t *W, const uint6
         }
         if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".dbg");
     }
-    if (mask_dummy) {
-        const std::vector<uint64_t> valid = valid_edges(nav);
+    if (valid) {
         n_valid = 0;
-        for (uint64_t x : valid) n_valid += __builtin_popcountll(x);
+        for (uint64_t x : *valid) n_valid += __builtin_popcountll(x);
         std::ofstream o(base + ".edgemask", std::ios::binary);
-        put_bit_vector_small(o, valid, n);
+        put_bit_vector_small(o, *valid, n);
         if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".edgemask");
     }
     if (weights && bits_per_count) {  // the chunk's weights buffer renamed (node_weights.cpp:62-68)

@@ -65,9 +65,10 @@ def test_no_cpu_fallback_without_device():
         boss.IBOSSChunkConstructor.initialize(10)
 
 
-def test_suffix_and_unknown_container_are_not_silently_accepted():
-    # the checks come before device selection, so they run without a GPU too
-    with pytest.raises(RuntimeError, match="suffix filter"):
-        boss.IBOSSChunkConstructor.initialize(10, filter_suffix="A")
+def test_bad_suffix_and_unknown_container_are_not_silently_accepted():
+    # the checks come before device selection, so they run without a GPU too; a filter suffix
+    # must leave the node's first char and the label out (kmer_extractor.cpp:325)
+    with pytest.raises(RuntimeError, match="shorter than k"):
+        boss.IBOSSChunkConstructor.initialize(3, filter_suffix="ACGT")
     with pytest.raises(RuntimeError, match="unknown container"):
         boss.IBOSSChunkConstructor.initialize(10, container_type=7)
