@@ -25,8 +25,12 @@
  * Multi-GPU (one process per GPU, RCCL over xGMI): every rank calls the *_dist variant with its
  * own reads and gets the chunk of one range of BOSS order; the rank chunks concatenate in rank
  * order with BOSS::Chunk::extend (boss_chunk.cpp:230-270) into the chunk a single build of all
- * reads returns.  This replaces the reference's suffix-sharded `build --suffix` +
- * `concatenate` route (cli/build.cpp:106-148, 359-456) with one exchange-based build.
+ * reads returns: one exchange-based build where the reference shards by suffix.
+ *
+ * The suffix-sharded route itself (`build --suffix-len`, `concatenate --clear-dummy`,
+ * cli/build.cpp:102-155, 358-456) runs too: a constructor created with a filter_suffix builds the
+ * chunk of that node suffix, and mtg_boss_write_dbg with mask_dummy = 2 prunes the concatenated
+ * chunks' redundant source dummies.
  *
  * No torch types, no C++ types: plain pointers and sizes.  All functions are thread-safe
  * except that one constructor must not be built and added to at the same time.
@@ -51,7 +55,7 @@ extern "C" {
 #define MTG_OK 0
 #define MTG_ERR_INVALID_K -1        /* k not in [1, 84]      (reference: exit(1)) */
 #define MTG_ERR_COUNT_WIDTH -2      /* bits_per_count > 32   (reference: runtime_error) */
-#define MTG_ERR_UNSUPPORTED -3      /* suffix filter not on this path */
+#define MTG_ERR_UNSUPPORTED -3      /* a multi-GPU build with a filter suffix */
 #define MTG_ERR_DEVICE -4           /* HIP runtime / kernel failure */
 #define MTG_ERR_ARGUMENT -5
 #define MTG_ERR_NO_DEVICE -6        /* no MI355X visible: the product path never falls back */
@@ -60,7 +64,9 @@ typedef struct mtg_boss_params {
     uint64_t k;                  /* BOSS k (node length) = DBG k - 1, in [1, 84] */
     int both_strands;            /* canonical mode: add reverse complements */
     uint8_t bits_per_count;      /* 0 = no weights; else --count-width (<= 32) */
-    const char *filter_suffix;   /* must be NULL or "" on this path */
+    const char *filter_suffix;   /* NULL / "": the full construction; else chars of "$ACGT", shorter
+                                    than k + 1: the chunk of the (k+1)-mers whose node ends with it
+                                    (boss_chunk_construct.cpp:946-1013); copied at create */
     uint64_t num_threads;        /* host threads for input staging */
     double memory_preallocated;  /* bytes of device memory the build may use (0 = all free HBM);
                                     larger inputs are built in key-range batches */
@@ -215,8 +221,10 @@ int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64
 /*
  * The graph files `metagraph build` writes from a chunk (cli/build.cpp:323-352; DBGSuccinct::serialize,
  * dbg_succinct.cpp:754-790): <outbase>.dbg (BOSS F / k / state, W, last, the graph mode, the
- * suffix-range index), <outbase>.edgemask with mask_dummy (--mask-dummy: the valid edges of
- * mark_all_dummy_edges, dbg_succinct.cpp:839-870), <outbase>.dbg.weights when the chunk has
+ * suffix-range index), <outbase>.edgemask with mask_dummy (1 = --mask-dummy: the valid edges of
+ * mark_all_dummy_edges, dbg_succinct.cpp:839-870; 2 = concatenate --clear-dummy: the redundant
+ * source dummies of suffix chunks erased first, boss.cpp:1443-1650, and no weights file, as
+ * build_boss_from_chunks takes none), <outbase>.dbg.weights when the chunk has
  * weights (node_weights.cpp:62-68).  graph_mode: 0 basic, 1 canonical.  suffix_length < 0 = the
  * build's default min(10, k).  *n_valid (may be NULL) = edges left valid by the mask (`nodes (k)` of
  * `metagraph stats`), else n - 1.  Host code: needs no device.  The sdsl-lite containers inside are
