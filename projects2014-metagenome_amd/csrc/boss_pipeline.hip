@@ -57,7 +57,7 @@ class Workspace {
         MSD_CURSOR, MSD_GSTART, MSD_UCOUNT, MSD_USTART, MSD_OVF, MSD_GLIST, FB_K, FB_V, RC_ALT, RC_ALTC, REAL, REALC, SPLITS, DTCNT, DTOFF, INFLAG, HIST1, HIST_ROWS,
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
-        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR,
+        QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
     };
     ~Workspace() {
@@ -816,7 +816,8 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         // pass A: histogram of the top bits of every valid k-mer
         constexpr int TILE = ExtractTraits<1>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
-        const uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
+        uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
+        if (nrows > 1) nrows &= ~1u;  // an even number of rows: row pairs count pass B's tiles (stripes)
         const unsigned hb = FUSED_HB;
         const uint32_t nbh = 1u << hb;
         uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
@@ -861,6 +862,13 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
         HIP_CHECK(hipMemcpyAsync(dh1, h1.data(), h1.size() * 4, hipMemcpyHostToDevice, c.stream));
         HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
+        // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t mod S
+        static_assert(FusedTraits<COUNTED, 512>::TILE == 2 * ExtractTraits<1>::TILE, "a pass-B tile = 2 pass-A tiles");
+        const uint32_t stripes = std::max<uint32_t>(1, nrows / 2);
+        auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
+        unsigned long long *send = scur + (size_t)stripes * nb1;
+        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, hb, b1, stripes, dcur, scur, send);
+        HIP_CHECK(hipGetLastError());
         *ka = (Key<1> *)c.ws.get(Workspace::KA, std::max<uint64_t>(N, 1) * 8);
         *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(N, 1) * 8);
         *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
@@ -872,13 +880,19 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
             constexpr int B = decltype(blk)::value;
             const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, B>::TILE);
             extract_partition_kernel<COUNTED, B><<<dim3((unsigned)ftiles), dim3(B), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1, dcur,
-                dcur + nb1, *ka, COUNTED ? *ca : nullptr, &c.small->error);
+                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1,
+                stripes, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
-        launch(std::integral_constant<int, 512>());
+        if (!COUNTED && K <= 32) {
+            constexpr int B = 512;
+            extract_partition_fast_kernel<B><<<dim3((unsigned)ceil_div(npos, 16 * B)), dim3(B), 0, c.stream>>>(
+                in.seq, in.seq_len, K, canonical ? 1 : 0, b1, stripes, scur, send, *ka, &c.small->error);
+        } else {
+            launch(std::integral_constant<int, 512>());
+        }
         HIP_CHECK(hipGetLastError());
-        cursor_check_kernel<<<dim3((unsigned)ceil_div(nb1, 256)), dim3(256), 0, c.stream>>>(dcur, dcur + nb1, nb1,
-                                                                                           &c.small->error);
+        cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
+            scur, send, stripes * nb1, &c.small->error);
         HIP_CHECK(hipGetLastError());
         tm.mark();
         HIP_CHECK(hipStreamSynchronize(c.stream));  // `h1` / `cur` are host locals

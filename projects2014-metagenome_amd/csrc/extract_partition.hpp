@@ -138,7 +138,7 @@ template <bool COUNTED, int BLOCK_>
 __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
-    uint32_t cmax, unsigned b, unsigned long long *__restrict__ cursor,
+    uint32_t cmax, unsigned b, uint32_t stripes, unsigned long long *__restrict__ cursor,
     const unsigned long long *__restrict__ bend, Key<1> *__restrict__ kout, uint32_t *__restrict__ vout,
     uint32_t *__restrict__ error) {
     using F = FusedTraits<COUNTED, BLOCK_>;
@@ -185,8 +185,9 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
         const uint32_t i = tid * PER + q;
         if (i < nb) {
             s_cnt[i] = off;
-            unsigned long long g = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
-            if (c[q] && g + c[q] > bend[i]) {  // pass A counted this bucket differently: never
+            const size_t ci = (size_t)(blockIdx.x % stripes) * nb + i;  // this tile's stripe
+            unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
+            if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
                 atomicOr(error, 2u);            // write past its range (the host raises)
                 g = ~0ull;
             }
@@ -211,6 +212,178 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
         const uint64_t o = s_gbase[lb] + (p - s_cnt[lb]);
         kout[o] = key;
         if (COUNTED) vout[o] = s_vals[p];
+    }
+}
+
+// Pass B without counts for K <= 32 (u64 keys), VALU-lean: the tile's read bytes are packed once
+// in LDS (16 chars a word: 2-bit codes + a 16-bit invalid-char mask), and each thread forms its 16
+// windows from three packed words with constant-offset funnel shifts (v_alignbit), the reverse
+// complement by sliding one char a window, validity from the invalid-char mask -- no per-window
+// LDS reads and no per-window branches.  Same k-mers as slide_windows (forward and rc plain words,
+// plain_to_boss, rc < fwd picks rc), so the same output as extract_partition_kernel<false>.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical, unsigned b,
+    uint32_t stripes, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
+    Key<1> *__restrict__ kout, uint32_t *__restrict__ error) {
+    constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
+    constexpr int NBMAX = 512;
+    constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
+    __shared__ uint32_t s_pack[NW];
+    __shared__ uint32_t s_inv[NW];
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
+    __shared__ unsigned long long s_gbase[NBMAX];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nb = 1u << b;
+    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const bool aligned = (((uintptr_t)(seq + base)) & 15) == 0;
+    for (uint32_t w = tid; w < (uint32_t)NW; w += BLOCK) {  // word w = chars base + 16 w ..
+        const uint64_t p = base + 16ull * w;
+        uint32_t pk = 0, iv = 0;
+        if (aligned && p + 16 <= seq_len) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(seq + p);
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t c = encode_dna((vv[q] >> (8 * r)) & 0xffu);
+                    pk |= (c & 3u) << (2 * (4 * q + r));
+                    iv |= (c >> 2) << (4 * q + r);
+                }
+        } else {
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t c = p + i < seq_len ? encode_dna(seq[p + i]) : 4u;
+                pk |= (c & 3u) << (2 * i);
+                iv |= (c >> 2) << i;
+            }
+        }
+        s_pack[w] = pk;
+        s_inv[w] = iv;
+    }
+    __syncthreads();
+
+    // this thread's windows p0 + j (j < 16): chars 16 tid .. 16 tid + 47 of the tile
+    const uint32_t w0 = s_pack[tid], w1 = s_pack[tid + 1], w2 = s_pack[tid + 2];
+    const uint64_t inv = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) | ((uint64_t)s_inv[tid + 2] << 32);
+    const uint64_t p0 = base + 16ull * tid;
+    const uint32_t nwin = p0 < npos ? (uint32_t)min<uint64_t>(PPT, npos - p0) : 0u;
+    const uint64_t maskK = (1ull << K) - 1;                         // K <= 32 chars
+    const uint64_t maskP = K >= 32 ? ~0ull : ((1ull << (2 * K)) - 1);  // 2K bits
+    const uint64_t lowNode = (1ull << (2 * (K - 1))) - 1;
+    const unsigned sh = 2 * (K - 1);
+    // E: the chars entering windows 1..16 (char K + j - 1 for window j) as 2-bit groups
+    uint32_t E;
+    {
+        const unsigned s2 = 2 * K;  // 2 .. 64
+        if (s2 < 32) E = __builtin_amdgcn_alignbit(w1, w0, s2);
+        else if (s2 < 64) E = __builtin_amdgcn_alignbit(w2, w1, s2 - 32);
+        else E = w2;
+    }
+    const uint64_t P0 = ((uint64_t)w0 | ((uint64_t)w1 << 32)) & maskP;
+    uint64_t R = reverse_pairs64(~P0) >> (64 - 2 * K);  // rc of window 0, plain
+    uint64_t kk[PPT];
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const uint32_t lo32 = j ? __builtin_amdgcn_alignbit(w1, w0, 2 * j) : w0;
+        const uint32_t hi32 = j ? __builtin_amdgcn_alignbit(w2, w1, 2 * j) : w1;
+        const uint64_t P = (((uint64_t)hi32 << 32) | lo32) & maskP;
+        if (j) R = ((R << 2) | (3u - ((E >> (2 * (j - 1))) & 3u))) & maskP;
+        const uint64_t f = ((P & lowNode) << 2) | (P >> sh);
+        const uint64_t r = ((R & lowNode) << 2) | (R >> sh);
+        kk[j] = canonical && r < f ? r : f;
+        m |= (uint32_t)((uint32_t)j < nwin && ((inv >> j) & maskK) == 0) << j;
+    }
+    const unsigned bshift = 2 * K - b;
+    uint32_t r[PPT];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+        r[j] = (m & (1u << j)) ? atomicAdd(&s_cnt[(uint32_t)(kk[j] >> bshift)], 1u) : 0u;
+    __syncthreads();
+    uint32_t c[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        c[q] = i < nb ? s_cnt[i] : 0;
+        sum += c[q];
+    }
+    uint32_t total;
+    uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+    __syncthreads();  // every count is read before the offsets overwrite them
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nb) {
+            s_cnt[i] = off;
+            const size_t ci = (size_t)(blockIdx.x % stripes) * nb + i;  // this tile's stripe
+            unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
+            if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
+                atomicOr(error, 2u);            // write past its range (the host raises)
+                g = ~0ull;
+            }
+            s_gbase[i] = g;
+        }
+        off += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+        if (m & (1u << j)) s_keys[s_cnt[(uint32_t)(kk[j] >> bshift)] + r[j]] = kk[j];
+    __syncthreads();
+    for (uint32_t p = tid; p < total; p += BLOCK) {
+        const uint64_t key = s_keys[p];
+        const uint32_t lb = (uint32_t)(key >> bshift);
+        if (s_gbase[lb] == ~0ull) continue;
+        kout[s_gbase[lb] + (p - s_cnt[lb])].w[0] = key;
+    }
+}
+
+// Pass B's write cursors, one set per stripe.  All tiles scatter into the same 2^b level-1
+// buckets, so one cursor per bucket would take every tile's atomic (146 k tiles x 512 buckets at
+// the bench size, all on 512 words).  Pass A's workgroup r histograms tiles r, r + nrows, ...
+// (4096 windows each), so with nrows = 2 S rows, rows 2s and 2s + 1 together count exactly the
+// pass-B tiles t = s mod S (8192 windows = two pass-A tiles): stripe s of bucket i starts at the
+// bucket's start plus the stripe counts of stripes < s.  One workgroup per bucket, S <= 4 * 256.
+__global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__restrict__ rows, uint32_t nrows,
+                                                            unsigned hb, unsigned b, uint32_t stripes,
+                                                            const unsigned long long *__restrict__ bstart,
+                                                            unsigned long long *__restrict__ cursor,
+                                                            unsigned long long *__restrict__ bend) {
+    __shared__ uint32_t s_scan[256 / 64 + 1];
+    constexpr int PER = 4;
+    const uint32_t i = blockIdx.x, nb = 1u << b, f = 1u << (hb - b), nbh = 1u << hb;
+    uint32_t h[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t st = threadIdx.x * PER + q;
+        h[q] = 0;
+        if (st < stripes) {
+            for (uint32_t r = 2 * st; r < min(2 * st + 2, nrows); ++r)
+                for (uint32_t j = 0; j < f; ++j) h[q] += rows[(size_t)r * nbh + i * f + j];
+            if (stripes == 1)  // one stripe: every row
+                for (uint32_t r = 2; r < nrows; ++r)
+                    for (uint32_t j = 0; j < f; ++j) h[q] += rows[(size_t)r * nbh + i * f + j];
+        }
+        sum += h[q];
+    }
+    uint32_t total;
+    uint32_t off = block_exclusive_sum<256>(sum, s_scan, &total);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t st = threadIdx.x * PER + q;
+        if (st < stripes) {
+            cursor[(size_t)st * nb + i] = bstart[i] + off;
+            bend[(size_t)st * nb + i] = bstart[i] + off + h[q];
+        }
+        off += h[q];
     }
 }
 
