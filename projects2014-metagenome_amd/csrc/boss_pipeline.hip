@@ -816,8 +816,13 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         // pass A: histogram of the top bits of every valid k-mer
         constexpr int TILE = ExtractTraits<1>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
+        // rows in multiples of rps = pass-B tile / pass-A tile: rps consecutive rows count one
+        // stripe of pass B's tiles (stripe_cursor_kernel)
+        const bool fast_b = !COUNTED && K <= 32;
+        constexpr int FB = 512;  // pass-B workgroup (1024 measured the same: 7.72-7.86 vs 7.74-7.77 ms)
+        const uint32_t rps = (uint32_t)(16 * FB / TILE);
         uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
-        if (nrows > 1) nrows &= ~1u;  // an even number of rows: row pairs count pass B's tiles (stripes)
+        if (nrows >= rps) nrows -= nrows % rps;
         const unsigned hb = FUSED_HB;
         const uint32_t nbh = 1u << hb;
         uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
@@ -864,10 +869,11 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
         // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t mod S
         static_assert(FusedTraits<COUNTED, 512>::TILE == 2 * ExtractTraits<1>::TILE, "a pass-B tile = 2 pass-A tiles");
-        const uint32_t stripes = std::max<uint32_t>(1, nrows / 2);
+        const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
         auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
         unsigned long long *send = scur + (size_t)stripes * nb1;
-        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, hb, b1, stripes, dcur, scur, send);
+        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, hb, b1, stripes, rps, dcur, scur,
+                                                                     send);
         HIP_CHECK(hipGetLastError());
         *ka = (Key<1> *)c.ws.get(Workspace::KA, std::max<uint64_t>(N, 1) * 8);
         *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(N, 1) * 8);
@@ -883,8 +889,8 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
                 in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1,
                 stripes, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
-        if (!COUNTED && K <= 32) {
-            constexpr int B = 512;
+        if (fast_b) {
+            constexpr int B = FB;
             extract_partition_fast_kernel<B><<<dim3((unsigned)ceil_div(npos, 16 * B)), dim3(B), 0, c.stream>>>(
                 in.seq, in.seq_len, K, canonical ? 1 : 0, b1, stripes, scur, send, *ka, &c.small->error);
         } else {

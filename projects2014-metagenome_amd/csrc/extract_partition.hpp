@@ -352,7 +352,7 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
 // pass-B tiles t = s mod S (8192 windows = two pass-A tiles): stripe s of bucket i starts at the
 // bucket's start plus the stripe counts of stripes < s.  One workgroup per bucket, S <= 4 * 256.
 __global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__restrict__ rows, uint32_t nrows,
-                                                            unsigned hb, unsigned b, uint32_t stripes,
+                                                            unsigned hb, unsigned b, uint32_t stripes, uint32_t rps,
                                                             const unsigned long long *__restrict__ bstart,
                                                             unsigned long long *__restrict__ cursor,
                                                             unsigned long long *__restrict__ bend) {
@@ -366,11 +366,9 @@ __global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__re
         const uint32_t st = threadIdx.x * PER + q;
         h[q] = 0;
         if (st < stripes) {
-            for (uint32_t r = 2 * st; r < min(2 * st + 2, nrows); ++r)
+            const uint32_t r1 = stripes == 1 ? nrows : min(rps * st + rps, nrows);  // one stripe: every row
+            for (uint32_t r = rps * st; r < r1; ++r)
                 for (uint32_t j = 0; j < f; ++j) h[q] += rows[(size_t)r * nbh + i * f + j];
-            if (stripes == 1)  // one stripe: every row
-                for (uint32_t r = 2; r < nrows; ++r)
-                    for (uint32_t j = 0; j < f; ++j) h[q] += rows[(size_t)r * nbh + i * f + j];
         }
         sum += h[q];
     }
