@@ -828,8 +828,8 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
         uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, nbh * 4);
         HIP_CHECK(hipMemsetAsync(h12, 0, nbh * 4, c.stream));
-        extract_hist_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
-                                                                  tiles, rows);
+        extract_hist_fast_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K,
+                                                                       canonical ? 1 : 0, tiles, rows);
         HIP_CHECK(hipGetLastError());
         hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
                                   c.stream>>>(rows, nrows, nbh, h12);

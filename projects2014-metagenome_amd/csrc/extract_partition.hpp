@@ -5,7 +5,7 @@
 // extraction kernel itself scatters the k-mers into their level-1 buckets, so that pass and its
 // histogram pass disappear.  Bucket starts must be known before the scatter, hence two passes
 // over the read bytes (1.5 GB each at the bench size):
-//   A  extract_hist_kernel      -- extract, histogram of the top HB bits (HB = 12), no writes;
+//   A  extract_hist_fast_kernel -- extract, histogram of the top HB bits (HB = 12), no writes;
 //   B  extract_partition_kernel -- extract again, rank by bucket in LDS, reserve one run per
 //                                  (tile, bucket) with a cursor atomic, write the runs.
 // The window logic is slide_windows (boss_kernels.hpp), shared with extract_kernel, so both
@@ -39,86 +39,115 @@ __device__ __forceinline__ void stage_codes(const uint8_t *__restrict__ seq, uin
     for (uint32_t i = done + tid; i < n; i += BLOCK) s_code[i] = encode_dna(seq[base + i]);
 }
 
+// 16 read bytes -> 16 2-bit codes (invalid -> 0) and a 16-bit invalid-char mask
+__device__ __forceinline__ void pack16(const uint4 v, uint32_t &pk, uint32_t &iv) {
+    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+    pk = 0;
+    iv = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t c = encode_dna((vv[q] >> (8 * r)) & 0xffu);
+            pk |= (c & 3u) << (2 * (4 * q + r));
+            iv |= (c >> 2) << (4 * q + r);
+        }
+}
+
+// packed word w of a tile (chars base + 16 w ..), bytes past seq_len invalid
+__device__ __forceinline__ void pack_word(const uint8_t *__restrict__ seq, uint64_t seq_len, uint64_t p,
+                                          uint32_t &pk, uint32_t &iv) {
+    if (((((uintptr_t)(seq + p)) & 15) == 0) && p + 16 <= seq_len) {
+        pack16(*reinterpret_cast<const uint4 *>(seq + p), pk, iv);
+        return;
+    }
+    pk = 0;
+    iv = 0;
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t c = p + i < seq_len ? encode_dna(seq[p + i]) : 4u;
+        pk |= (c & 3u) << (2 * i);
+        iv |= (c >> 2) << i;
+    }
+}
+
+// reverse complement of a packed word: char i -> position 15 - i, code c -> 3 - c
+__device__ __forceinline__ uint32_t rc_word(uint32_t w) {
+    uint32_t x = __builtin_bitreverse32(w);
+    x = ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
+    return ~x;
+}
+
 // A: one LDS histogram per workgroup over its tiles (grid-stride), one row per workgroup.
 // The top HB bits of a 2-bit BOSS key are its node's last HB/2 chars a_{K-1} .. a_{K-HB/2}
 // (kmer_boss.hpp:58-72), and top(min(fwd, rc)) = min(top(fwd), top(rc)) (the tops decide the
 // comparison unless they are equal), so a window needs only those chars of each strand: rc's
 // top chars are comp(a_2) .. comp(a_{HB/2+1}).  Needs K - 1 >= HB/2 (callers check).
-__global__ __launch_bounds__(256) void extract_hist_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
-                                                           unsigned K, int canonical, uint64_t ntiles,
-                                                           uint32_t *__restrict__ rows) {
-    using T = ExtractTraits<1>;
-    constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
+// The tile is packed once (pack16); per window the forward top a_{K-6} .. a_{K-1} and the rc top
+// comp(a_7) .. comp(a_2) are constant-offset 12-bit fields of two precomputed 64/96-bit words,
+// validity a field of the invalid-char mask (round 2: 1.85 -> ~1.2 ms, VALU-bound before).
+__global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
+                                                                unsigned K, int canonical, uint64_t ntiles,
+                                                                uint32_t *__restrict__ rows) {
+    constexpr int BLOCK = 256, PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;
     constexpr uint32_t NB = 1u << FUSED_HB;
-    constexpr unsigned C = FUSED_HB / 2;  // chars per top
-    __shared__ __align__(16) uint8_t s_code[TILE + T::MAXK];
+    static_assert(FUSED_HB == 12, "6-char tops");
+    __shared__ uint32_t s_pack[NW];
+    __shared__ uint32_t s_inv[NW];
     __shared__ uint32_t s_h[NB];
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    // The grid strides over tiles, so the next tile's bytes are prefetched into registers (one
-    // 16-byte load per thread).  With the old switch-based encode this was slower (16 divergent
-    // switches per thread); with the table encode it saves 0.15 ms.
-    static_assert(TILE == 16 * BLOCK, "one 16-byte load per thread covers a tile");
-    const bool vec = ((uintptr_t)seq & 15) == 0;
+    const uint64_t maskK = (1ull << K) - 1;
+    const unsigned fs = 2 * (K - 7);  // K >= 7 (callers check K - 1 >= 6)
+    // the raw bytes of word tid of the next tile, loaded while the current tile is counted
     uint4 pre = make_uint4(0, 0, 0, 0);
-    auto fetch = [&](uint64_t t) {  // prefetch the next tile's bytes while this one is histogrammed
-        const uint64_t b = t * TILE;
-        if (t < ntiles && vec && b + TILE + T::MAXK <= seq_len) {
-            pre = reinterpret_cast<const uint4 *>(seq + b)[tid];
-            return true;
-        }
-        return false;
+    bool have = false;
+    auto fetch = [&](uint64_t t) {
+        const uint64_t p = t * TILE + 16ull * tid;
+        have = t < ntiles && ((((uintptr_t)(seq + p)) & 15) == 0) && p + 16 <= seq_len;
+        if (have) pre = *reinterpret_cast<const uint4 *>(seq + p);
     };
-    bool have = fetch(blockIdx.x);
+    fetch(blockIdx.x);
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t base = tile * TILE;
-        const uint64_t span_end = min(seq_len, base + TILE + K - 1);
-        __syncthreads();
-        if (have) {
-            const uint32_t in[4] = {pre.x, pre.y, pre.z, pre.w};
-            uint32_t o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                o[q] = encode_dna(in[q] & 0xff) | encode_dna((in[q] >> 8) & 0xff) << 8 |
-                       encode_dna((in[q] >> 16) & 0xff) << 16 | encode_dna(in[q] >> 24) << 24;
-            reinterpret_cast<uint4 *>(s_code)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
-            stage_codes<BLOCK>(seq, base + TILE, span_end, s_code + TILE, tid);
-        } else {
-            stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
+        uint32_t pk, iv;
+        if (have) pack16(pre, pk, iv);
+        else pack_word(seq, seq_len, base + 16ull * tid, pk, iv);
+        __syncthreads();  // the previous tile's words are read
+        s_pack[tid] = pk;
+        s_inv[tid] = iv;
+        if (tid < NW - BLOCK) {
+            uint32_t a, b;
+            pack_word(seq, seq_len, base + 16ull * (BLOCK + tid), a, b);
+            s_pack[BLOCK + tid] = a;
+            s_inv[BLOCK + tid] = b;
         }
-        have = fetch(tile + gridDim.x);
         __syncthreads();
-        const uint64_t p0 = base + (uint64_t)tid * PPT;
+        fetch(tile + gridDim.x);
+        const uint64_t p0 = base + 16ull * tid;
         if (p0 >= npos) continue;
-        const uint32_t r0 = tid * PPT;
-        const uint8_t *w0 = s_code + r0;  // window j: a_i = w0[j + i - 1]
-        int64_t last_bad = -1;            // window-relative index of the last invalid char seen
-        for (unsigned i = 0; i < K; ++i)
-            if (w0[i] == 4) last_bad = i;
-        // rolling tops: f = a_{K-1} .. a_{K-C} (w0[j+K-2] .. w0[j+K-1-C]), r = comp(a_2) .. comp(a_{C+1});
-        // 2 LDS reads per window instead of 2C (the byte reads are PPT bytes apart across lanes,
-        // so every read costs a 4-way bank conflict).  Invalid chars are masked: such windows are
-        // skipped, and a window's tops only hold chars of that window.
-        uint32_t f = 0, r = 0;
-#pragma unroll
-        for (unsigned q = 0; q < C; ++q) {
-            f = (f << 2) | (w0[K - 2 - q] & 3u);
-            r = (r << 2) | (3u - (w0[1 + q] & 3u));
+        const uint32_t nwin = (uint32_t)min<uint64_t>(PPT, npos - p0);
+        const uint32_t w0 = s_pack[tid], w1 = s_pack[tid + 1], w2 = s_pack[tid + 2];
+        const uint64_t inv = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) | ((uint64_t)s_inv[tid + 2] << 32);
+        // F = chars K-7 .. of the span (window j's forward top = F >> 2j)
+        uint32_t flo, fhi;
+        if (fs < 32) {
+            flo = __builtin_amdgcn_alignbit(w1, w0, fs);
+            fhi = __builtin_amdgcn_alignbit(w2, w1, fs);
+        } else {
+            flo = __builtin_amdgcn_alignbit(w2, w1, fs - 32);
+            fhi = w2 >> (fs - 32);
         }
-        uint32_t prev = w0[K - 1];  // a_K of window j - 1 = a_{K-1} of window j
+        // Q = the reverse complement of the 48 chars: char t at bits 2 (47 - t); window j's rc top
+        // comp(a_7) .. comp(a_2) = chars j + 6 .. j + 1 = Q >> 2 (41 - j)
+        const uint32_t q1 = rc_word(w1), q2 = rc_word(w0);
 #pragma unroll
         for (int j = 0; j < PPT; ++j) {
-            if (p0 + j >= npos) break;
-            if (j) {
-                const uint32_t c = w0[j + K - 1];
-                if (c == 4) last_bad = j + K - 1;
-                f = (f >> 2) | ((prev & 3u) << (2 * C - 2));
-                r = ((r << 2) & (NB - 1)) | (3u - (w0[j + C] & 3u));
-                prev = c;
-            }
-            if (last_bad >= (int64_t)j) continue;
-            atomicAdd(&s_h[canonical && r < f ? r : f], 1u);
+            const uint32_t f = (j ? __builtin_amdgcn_alignbit(fhi, flo, 2 * j) : flo) & (NB - 1);
+            const int sr = 2 * (41 - j);  // 52 .. 82
+            const uint32_t r = (sr >= 64 ? (q2 >> (sr - 64)) : __builtin_amdgcn_alignbit(q2, q1, sr - 32)) & (NB - 1);
+            const bool ok = (uint32_t)j < nwin && ((inv >> j) & maskK) == 0;
+            if (ok) atomicAdd(&s_h[canonical && r < f ? r : f], 1u);
         }
     }
     __syncthreads();

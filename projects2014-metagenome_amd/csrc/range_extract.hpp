@@ -3,7 +3,7 @@
 // The build collects the k-mers one key range at a time (boss_pipeline.hip: collect_ranges), so
 // every range re-scans the whole read buffer.  The scans must be cheap: a window is assigned to a
 // range by the top RB_CHARS chars of its key alone, which roll along the read in registers (as in
-// extract_hist_kernel), and only the windows of the current range build their full key, straight
+// the fused extraction's pass A), and only the windows of the current range build their full key, straight
 // from a 2-bit packed copy of the tile in LDS.
 //   count pass  -- per tile, how many k-mers fall in each of the 4^RB_CHARS top-char bins (u16);
 //                  their column sums balance the ranges, their row sums over a range's bins are
