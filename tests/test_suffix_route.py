@@ -159,3 +159,21 @@ def test_transcripts_suffix_chunks_nodes_golden(tmp_path, transcripts_1000, both
     base = str(tmp_path / "t")
     assert cat.write_dbg(base, canonical=both, mask_dummy=True, prune=True) == nodes
     assert cat.write_dbg(str(tmp_path / "m"), canonical=both, mask_dummy=True) == nodes
+
+
+def test_forward_and_reverse_equals_both_strands():
+    # `build --fwd-and-reverse` (cli/parse_sequences.hpp: every read and its reverse complement) in
+    # basic mode collects the k-mers of both strands with the counts of both strands -- the real-edge
+    # set and counts of CANONICAL_ONLY + add_reverse_complements -- so its chunk is the both_strands
+    # chunk (the graph mode of the .dbg stays basic)
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A", "N": "N"}
+    seqs = CONSTRUCT_SEQS + random_reads(13, 25, 5, 50, "ACGTN")
+    both = seqs + ["".join(comp[c] for c in reversed(s)) for s in seqs]
+    for k in (1, 2, 4, 9, 20):
+        for bits in (0, 8):
+            a = O.build_chunk(k, both, canonical=False, bits_per_count=bits)
+            b = O.build_chunk(k, seqs, canonical=True, bits_per_count=bits)
+            assert np.array_equal(a.W, b.W) and np.array_equal(a.last, b.last), k
+            assert np.array_equal(a.F, b.F), k
+            if bits:
+                assert np.array_equal(a.weights, b.weights), k
