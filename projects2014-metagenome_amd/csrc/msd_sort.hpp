@@ -412,8 +412,8 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
 template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
-          bool NODUP = false>
-__global__ __launch_bounds__(LB) void local_unique_kernel(
+          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1>
+__global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
     unsigned b, unsigned sbits, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
@@ -422,7 +422,11 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
     constexpr int SLOTS = SL;
     constexpr uint32_t LIMIT = SL / 2;
     constexpr uint64_t EMPTY = ~0ull;
+    // LIST: every new key records its slot (insertion order), so compaction gathers D slots
+    // instead of scanning all SLOTS (and needs no block scan)
+    constexpr bool LIST = KEYCAS && !NODUP;
     __shared__ Key<L> s_key[SLOTS];
+    __shared__ uint16_t s_slot[LIST ? LIMIT : 1];
     __shared__ uint32_t s_state[KEYCAS ? 1 : SLOTS];
     __shared__ uint32_t s_sum[COUNTED ? SLOTS : 1];
     __shared__ uint32_t s_hist[256];
@@ -541,7 +545,13 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
                                                        (unsigned long long)EMPTY,
                                                        (unsigned long long)key.w[0]);
                         if (old == EMPTY) {
-                            ++mynew;
+                            if (LIST) {
+                                const uint32_t pos = atomicAdd(&s_distinct, 1u);
+                                if (pos < LIMIT) s_slot[pos] = (uint16_t)h;
+                                else ovf = true;
+                            } else {
+                                ++mynew;
+                            }
                             break;
                         }
                         if (old == key.w[0]) break;
@@ -584,7 +594,46 @@ __global__ __launch_bounds__(LB) void local_unique_kernel(
         }
         const uint32_t D = s_distinct;
 
-        if constexpr (NODUP) {
+        if constexpr (LIST) {
+            // gather the D recorded slots, then write them compacted to s_key[0..D)
+            constexpr int PERL = (LIMIT + LB - 1) / LB;
+            Key<L> kk[PERL];
+            uint32_t ss[PERL];
+#pragma unroll
+            for (int q = 0; q < PERL; ++q) {
+                const uint32_t i = tid + q * LB;
+                if (i < D) {
+                    const uint32_t sl = s_slot[i];
+                    kk[q] = s_key[sl];
+                    if (COUNTED) ss[q] = s_sum[sl];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < PERL; ++q) {
+                const uint32_t i = tid + q * LB;
+                if (i < D) {
+                    s_key[i] = kk[q];
+                    if (COUNTED) s_sum[i] = ss[q];
+                }
+            }
+            __syncthreads();
+            if (D) {
+                const Key<L> ref = s_key[0];
+                int hb_local = -1;
+#pragma unroll
+                for (int q = 0; q < PERL; ++q) {
+                    if (tid + q * LB < D) {
+                        Key<L> dx;
+#pragma unroll
+                        for (int w = 0; w < L; ++w) dx.w[w] = kk[q].w[w] ^ ref.w[w];
+                        hb_local = max(hb_local, key_msb(dx));
+                    }
+                }
+                if (hb_local >= 0) atomicMax(&s_hb, hb_local);
+            }
+            __syncthreads();
+        } else if constexpr (NODUP) {
             // already compact: highest differing bit over s_key[0..D)
             if (D) {
                 const Key<L> ref = s_key[0];
