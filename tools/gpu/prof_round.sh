@@ -9,7 +9,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --outp
 echo "stats ok"
 python3 "$R/tools/kstats.py" "$OUT/stats" > "$OUT/kernel_stats.txt" 2>&1 || true
 [ "$2" = "stats" ] && exit 0
-KRE="msd_partition_kernel|msd_hist_kernel|local_unique|extract_partition|extract_hist|merge_kernel|merge_emit|dummy_sink"
+KRE="msd_partition_kernel|msd_hist_kernel|local_unique|extract_partition|extract_hist|merge_kernel|split_emit|dummy_sink|dummy_rank|group_gather|rc_map"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "copy8_kernel" -d "$OUT/calib_$ctr" -o run --output-format csv -- "$R/tools/stage_bench" calib > "$OUT/calib_$ctr.log" 2>&1 || { echo "calib $ctr failed"; exit 1; }
   timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-include-regex "$KRE" -d "$OUT/bench_$ctr" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --host-steps 0 > "$OUT/bench_$ctr.log" 2>&1 || { echo "bench $ctr failed"; exit 1; }
