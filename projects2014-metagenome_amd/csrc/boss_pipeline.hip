@@ -819,8 +819,11 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         // rows in multiples of rps = pass-B tile / pass-A tile: rps consecutive rows count one
         // stripe of pass B's tiles (stripe_cursor_kernel)
         const bool fast_b = !COUNTED && K <= 32;
-        constexpr int FB = 512;  // pass-B workgroup (1024 measured the same: 7.72-7.86 vs 7.74-7.77 ms)
-        const uint32_t rps = (uint32_t)(16 * FB / TILE);
+        // pass-B workgroup: 1024 threads (16 K-window tiles) for the packed kernel -- the same time as
+        // 512 (7.72-7.86 vs 7.74-7.77 ms per extract stage) but runs twice as long: PMC writes 11.1
+        // vs 12.5 GB (1.16 vs 1.30 x N w); the counted kernel keeps 8 K-window tiles
+        const int fbk = fast_b ? 1024 : 512;
+        const uint32_t rps = (uint32_t)(16 * fbk / TILE);
         uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
         if (nrows >= rps) nrows -= nrows % rps;
         const unsigned hb = FUSED_HB;
@@ -890,7 +893,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
                 stripes, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
         if (fast_b) {
-            constexpr int B = FB;
+            constexpr int B = 1024;
             extract_partition_fast_kernel<B><<<dim3((unsigned)ceil_div(npos, 16 * B)), dim3(B), 0, c.stream>>>(
                 in.seq, in.seq_len, K, canonical ? 1 : 0, b1, stripes, scur, send, *ka, &c.small->error);
         } else {
