@@ -458,7 +458,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         if (COUNTED) std::swap(*vals, *valt);
         b = bb;
     };
-    if (runs && runs->size() > 2 && runs->size() <= 129 && levels) {
+    if (runs && runs->size() >= 2 && runs->size() <= 129 && levels) {
         // bucket layout of the top T bits straight from the runs' own order
         const unsigned T = digit_end[levels];
         const uint32_t P = (uint32_t)runs->size() - 1;
@@ -1684,15 +1684,18 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA,
                                               Workspace::XAC, &xa, &xac, &runs);
         tr("exchange 1", n1);
-        K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
-        uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
-        // the P runs are sorted and disjoint within a run; duplicates across runs collapse and
-        // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover 1/P of
-        // the prefix space, hence the denser plan.
-        // the keys cover ~1/P of the prefix space: P times denser buckets than their count says
-        const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / d.P;
-        T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
-                                                  false, &runs);
+        if (d.P == 1) {  // one rank: its own sorted distinct k-mers came back unchanged
+            T.n_unique = n1;
+        } else {
+            K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
+            uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
+            // the P runs are sorted and distinct within a run; duplicates across runs collapse and
+            // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover ~1/P of
+            // the prefix space: P times denser buckets than their count says
+            const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / d.P;
+            T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
+                                                      false, &runs);
+        }
     }
     const uint64_t U = T.n_unique;
     tr("owner dedupe", U);
@@ -1723,13 +1726,33 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         const uint64_t n2 = exchange_runs<K2>(c, d, 2, arrs, COUNTED ? cnts : nullptr, soff, Workspace::REAL,
                                               Workspace::REALC, &ra, &rac, &runs);
         tr("exchange 2", n2);
-        K2 *rb = (K2 *)c.ws.get(Workspace::KB, n2 * sizeof(K2));
-        uint32_t *rbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, n2 * 4) : nullptr;
-        // all 2P runs are distinct keys (a canonical k-mer and its rc are different edges)
-        R = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rac, &rbc, n2, 2 * K, cmax, 1.0 / d.P, nullptr, true,
-                                         &runs);
-        E = ra;
-        Ec = rac;
+        // The P canonical runs (array 0) came from the owners of exchange 1, whose ranges are
+        // disjoint and increase with the rank, so laid out by source rank they are already one
+        // sorted array.  Only the P rc runs need sorting: the single build's rc sort with its
+        // local pass fused with the merge into the canonical keys (local_merge_kernel), the P
+        // sorted runs gathered by bucket instead of partitioned.  All keys are distinct (a
+        // canonical k-mer and its rc are different edges; even K's palindromes left the rc set).
+        const uint64_t ncan = runs[d.P], nrc = n2 - ncan;
+        K2 *out = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(n2, 1) * sizeof(K2));
+        uint32_t *outc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(n2, 1) * 4) : nullptr;
+        K2 *rkeys = ra + ncan;
+        uint32_t *rcc = COUNTED ? rac + ncan : nullptr;
+        K2 *ralt = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nrc, 1) * sizeof(K2));
+        uint32_t *rcalt = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nrc, 1) * 4) : nullptr;
+        std::vector<uint64_t> rc_runs(d.P + 1);
+        for (int j = 0; j <= d.P; ++j) rc_runs[j] = runs[d.P + j] - ncan;
+        RcMerge<L2> rm{ra, rac, ncan, out, outc};
+        // plan the buckets for rc + canonical keys together (the fused pass holds both, and a
+        // low range is mostly canonical), spread over 1/P of the prefix space: as dense as a
+        // single build of P * (nrc + ncan) / 2 rc keys
+        const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + ncan)) : 1.0;
+        const uint64_t nr = msd_sort_unique<L2, COUNTED>(c, &rkeys, &ralt, &rcc, &rcalt, nrc, 2 * K, cmax,
+                                                         dupm, nullptr, true, &rc_runs, false,
+                                                         ncan ? &rm : nullptr);
+        if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, ra, rac, ncan, rkeys, rcc, nr, K, out, outc, 0);
+        R = ncan + nr;
+        E = out;
+        Ec = outc;
     } else {
         bounds = b1;  // basic mode: exchange 1 already placed every edge at its final owner
     }
