@@ -438,12 +438,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         if (!COUNTED && bb - bp > 8) {  // wide digits: 1024-thread tiles keep the bucket runs long
             if constexpr (!COUNTED) {
                 constexpr int TILE2 = MsdTraits<L>::ITEMS * 1024;
-                msd_partition_kernel<L, false, 1024, true><<<dim3((unsigned)ceil_div(n, TILE2)), dim3(1024), 0,
+                msd_partition_kernel<L, false, 1024, true><<<dim3((unsigned)xcd_grid(ceil_div(n, TILE2))), dim3(1024), 0,
                                                              c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits, bb,
                                                                          bp, cur);
             }
         } else {
-            msd_partition_kernel<L, COUNTED><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(
+            msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
                 *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
         }
         HIP_CHECK(hipGetLastError());
@@ -831,8 +831,16 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
         uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, nbh * 4);
         HIP_CHECK(hipMemsetAsync(h12, 0, nbh * 4, c.stream));
+        // stripes of pass B's tiles: S = nrows / rps stripes of per_stripe consecutive pass-B tiles
+        // (= rps per_stripe pass-A tiles); pass-A row r counts the per_row pass-A tiles
+        // [r per_row, (r + 1) per_row), so rows rps s .. rps s + rps - 1 cover stripe s.  One stripe
+        // (fewer rows than rps) takes every row, each an equal share of the tiles.
+        const uint64_t tiles_b = ceil_div(npos, (uint64_t)16 * fbk);
+        const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
+        const uint64_t per_stripe = ceil_div(tiles_b, stripes);
+        const uint64_t per_row = stripes == 1 ? ceil_div(tiles_b * rps, nrows) : per_stripe;
         extract_hist_fast_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K,
-                                                                       canonical ? 1 : 0, tiles, rows);
+                                                                       canonical ? 1 : 0, tiles, per_row, rows);
         HIP_CHECK(hipGetLastError());
         hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
                                   c.stream>>>(rows, nrows, nbh, h12);
@@ -870,9 +878,8 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
         HIP_CHECK(hipMemcpyAsync(dh1, h1.data(), h1.size() * 4, hipMemcpyHostToDevice, c.stream));
         HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
-        // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t mod S
+        // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t / per_stripe
         static_assert(FusedTraits<COUNTED, 512>::TILE == 2 * ExtractTraits<1>::TILE, "a pass-B tile = 2 pass-A tiles");
-        const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
         auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
         unsigned long long *send = scur + (size_t)stripes * nb1;
         stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, hb, b1, stripes, rps, dcur, scur,
@@ -888,14 +895,15 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         auto launch = [&](auto blk) {
             constexpr int B = decltype(blk)::value;
             const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, B>::TILE);
-            extract_partition_kernel<COUNTED, B><<<dim3((unsigned)ftiles), dim3(B), 0, c.stream>>>(
+            extract_partition_kernel<COUNTED, B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
                 in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1,
-                stripes, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
+                per_stripe, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
         if (fast_b) {
             constexpr int B = 1024;
-            extract_partition_fast_kernel<B><<<dim3((unsigned)ceil_div(npos, 16 * B)), dim3(B), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, b1, stripes, scur, send, *ka, &c.small->error);
+            extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * B))), dim3(B), 0,
+                                                c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, per_stripe,
+                                                            scur, send, *ka, &c.small->error);
         } else {
             launch(std::integral_constant<int, 512>());
         }

@@ -85,9 +85,11 @@ __device__ __forceinline__ uint32_t rc_word(uint32_t w) {
 // The tile is packed once (pack16); per window the forward top a_{K-6} .. a_{K-1} and the rc top
 // comp(a_7) .. comp(a_2) are constant-offset 12-bit fields of two precomputed 64/96-bit words,
 // validity a field of the invalid-char mask (round 2: 1.85 -> ~1.2 ms, VALU-bound before).
+// Row r counts the per_row consecutive tiles [r * per_row, (r + 1) * per_row): rps consecutive rows
+// then cover one stripe of pass B's tiles (stripe_cursor_kernel).
 __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
                                                                 unsigned K, int canonical, uint64_t ntiles,
-                                                                uint32_t *__restrict__ rows) {
+                                                                uint64_t per_row, uint32_t *__restrict__ rows) {
     constexpr int BLOCK = 256, PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;
     constexpr uint32_t NB = 1u << FUSED_HB;
     static_assert(FUSED_HB == 12, "6-char tops");
@@ -107,8 +109,9 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
         have = t < ntiles && ((((uintptr_t)(seq + p)) & 15) == 0) && p + 16 <= seq_len;
         if (have) pre = *reinterpret_cast<const uint4 *>(seq + p);
     };
-    fetch(blockIdx.x);
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * per_row, t1 = min(ntiles, t0 + per_row);
+    fetch(t0);
+    for (uint64_t tile = t0; tile < t1; ++tile) {
         const uint64_t base = tile * TILE;
         uint32_t pk, iv;
         if (have) pack16(pre, pk, iv);
@@ -123,7 +126,8 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
             s_inv[BLOCK + tid] = b;
         }
         __syncthreads();
-        fetch(tile + gridDim.x);
+        if (tile + 1 < t1) fetch(tile + 1);
+        else have = false;
         const uint64_t p0 = base + 16ull * tid;
         if (p0 >= npos) continue;
         const uint32_t nwin = (uint32_t)min<uint64_t>(PPT, npos - p0);
@@ -167,7 +171,7 @@ template <bool COUNTED, int BLOCK_>
 __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
-    uint32_t cmax, unsigned b, uint32_t stripes, unsigned long long *__restrict__ cursor,
+    uint32_t cmax, unsigned b, uint64_t per_stripe, unsigned long long *__restrict__ cursor,
     const unsigned long long *__restrict__ bend, Key<1> *__restrict__ kout, uint32_t *__restrict__ vout,
     uint32_t *__restrict__ error) {
     using F = FusedTraits<COUNTED, BLOCK_>;
@@ -183,9 +187,12 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
 
     const uint32_t tid = threadIdx.x;
     const uint32_t nb = 1u << b;
-    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    // XCD-contiguous tiles (device_common.hpp: xcd_tile); stripe = tile / per_stripe
+    const uint64_t tile = xcd_tile((npos + TILE - 1) / TILE);
+    if (tile * TILE >= npos) return;
+    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    const uint64_t base = tile * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
     stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
     __syncthreads();
@@ -214,7 +221,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
         const uint32_t i = tid * PER + q;
         if (i < nb) {
             s_cnt[i] = off;
-            const size_t ci = (size_t)(blockIdx.x % stripes) * nb + i;  // this tile's stripe
+            const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
             unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
             if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
                 atomicOr(error, 2u);            // write past its range (the host raises)
@@ -253,7 +260,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical, unsigned b,
-    uint32_t stripes, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
+    uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
     Key<1> *__restrict__ kout, uint32_t *__restrict__ error) {
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
     constexpr int NBMAX = 512;
@@ -267,9 +274,12 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
 
     const uint32_t tid = threadIdx.x;
     const uint32_t nb = 1u << b;
-    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    // XCD-contiguous tiles (device_common.hpp: xcd_tile); stripe = tile / per_stripe
+    const uint64_t tile = xcd_tile((npos + TILE - 1) / TILE);
+    if (tile * TILE >= npos) return;
+    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    const uint64_t base = tile * TILE;
     const bool aligned = (((uintptr_t)(seq + base)) & 15) == 0;
     for (uint32_t w = tid; w < (uint32_t)NW; w += BLOCK) {  // word w = chars base + 16 w ..
         const uint64_t p = base + 16ull * w;
@@ -351,7 +361,7 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
         const uint32_t i = tid * PER + q;
         if (i < nb) {
             s_cnt[i] = off;
-            const size_t ci = (size_t)(blockIdx.x % stripes) * nb + i;  // this tile's stripe
+            const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
             unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
             if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
                 atomicOr(error, 2u);            // write past its range (the host raises)
@@ -376,10 +386,12 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
 
 // Pass B's write cursors, one set per stripe.  All tiles scatter into the same 2^b level-1
 // buckets, so one cursor per bucket would take every tile's atomic (146 k tiles x 512 buckets at
-// the bench size, all on 512 words).  Pass A's workgroup r histograms tiles r, r + nrows, ...
-// (4096 windows each), so with nrows = 2 S rows, rows 2s and 2s + 1 together count exactly the
-// pass-B tiles t = s mod S (8192 windows = two pass-A tiles): stripe s of bucket i starts at the
-// bucket's start plus the stripe counts of stripes < s.  One workgroup per bucket, S <= 4 * 256.
+// the bench size, all on 512 words).  A pass-B tile is rps pass-A tiles; stripe s is the pass-B
+// tiles [s C, (s + 1) C), and pass A's row r counts the pass-A tiles [r C, (r + 1) C), so with
+// nrows = rps S rows, rows rps s .. rps s + rps - 1 count exactly stripe s: stripe s of bucket i
+// starts at the bucket's start plus the stripe counts of stripes < s.  Contiguous stripes keep the
+// runs of neighbouring tiles (which one XCD runs together, xcd_tile) next to each other in a
+// bucket.  One workgroup per bucket, S <= 4 * 256.
 __global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__restrict__ rows, uint32_t nrows,
                                                             unsigned hb, unsigned b, uint32_t stripes, uint32_t rps,
                                                             const unsigned long long *__restrict__ bstart,

@@ -203,7 +203,9 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
 
     const uint32_t tid = threadIdx.x;
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t tile = xcd_tile((n + TILE - 1) / TILE);  // grid = xcd_grid(tiles)
+    if (tile * TILE >= n) return;
+    const uint64_t base = tile * TILE;
     const unsigned sub = b - bp;
     const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
     for (int i = tid; i < (int)wsize; i += BLOCK) s_cnt[i] = 0;

@@ -253,6 +253,82 @@ __global__ __launch_bounds__(1024) void part_vec_kernel(const Key<1> *__restrict
     }
 }
 
+// the product kernel staging its tile through LDS in ROUNDS slices of TILE / ROUNDS positions (the
+// tile's bucket-ordered positions, so every run except the ones crossing a slice edge is written in
+// one piece): 16K-key tiles in 128 / ROUNDS KiB of LDS, two workgroups per CU at ROUNDS >= 2
+// XCD: workgroup b runs tile (b % 8) * per + b / 8, so each XCD (dispatch round-robin over 8)
+// walks its own contiguous eighth of the tiles and its L2 sees neighbouring runs of a bucket
+template <int ROUNDS, bool XCD = false>
+__global__ __launch_bounds__(1024) void part_rounds_kernel(const Key<1> *__restrict__ kin, Key<1> *__restrict__ kout,
+                                                           uint64_t n, unsigned nbits, unsigned b, unsigned bp,
+                                                           unsigned long long *__restrict__ cursor) {
+    constexpr int ITEMS = 16, BLOCK = 1024, TILE = ITEMS * BLOCK, W = 512, SLICE = TILE / ROUNDS;
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    const uint64_t per = (ntiles + 7) / 8;
+    const uint64_t tile = XCD ? (uint64_t)(blockIdx.x % 8) * per + blockIdx.x / 8 : blockIdx.x;
+    if (tile >= ntiles) return;
+    __shared__ Key<1> s_keys[SLICE];
+    __shared__ uint32_t s_cnt[W];
+    __shared__ uint32_t s_loff[W];
+    __shared__ unsigned long long s_gbase[W];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = tile * TILE;
+    const unsigned sub = b - bp;
+    const uint32_t wsize = min((uint32_t)W, 1u << sub);
+    if (tid < wsize) s_cnt[tid] = 0;
+    const uint32_t wbase = key_prefix(kin[base], nbits, bp) << sub;
+    __syncthreads();
+    Key<1> k[ITEMS];
+    uint32_t r[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * BLOCK + tid;
+        if (i < n) k[j] = load_key(kin + i, true);
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        r[j] = 0xFFFFFFFFu;
+        if (base + (uint64_t)j * BLOCK + tid < n) {
+            const uint32_t lb = key_prefix(k[j], nbits, b) - wbase;
+            if (lb < wsize) {
+                r[j] = atomicAdd(&s_cnt[lb], 1u);
+            } else {
+                const unsigned long long o = atomicAdd(&cursor[lb + wbase], 1ull);
+                kout[o] = k[j];
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = tid < wsize ? s_cnt[tid] : 0;
+    uint32_t total;
+    const uint32_t off = block_exclusive_sum<BLOCK>(cnt, s_scan, &total);
+    if (tid < wsize) {
+        s_loff[tid] = off;
+        s_gbase[tid] = cnt ? atomicAdd(&cursor[wbase + tid], (unsigned long long)cnt) : 0;
+    }
+    __syncthreads();
+    // positions become tile-order positions; r[j] = that position (or ~0)
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        if (r[j] != 0xFFFFFFFFu) r[j] += s_loff[key_prefix(k[j], nbits, b) - wbase];
+#pragma unroll
+    for (int q = 0; q < ROUNDS; ++q) {
+        const uint32_t lo = q * SLICE;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            if (r[j] - lo < (uint32_t)SLICE) s_keys[r[j] - lo] = k[j];
+        __syncthreads();
+        const uint32_t hi = min(total, lo + SLICE);
+        for (uint32_t p = lo + tid; p < hi; p += BLOCK) {
+            const Key<1> key = s_keys[p - lo];
+            const uint32_t lb = key_prefix(key, nbits, b) - wbase;
+            store_key(kout + s_gbase[lb] + (p - s_loff[lb]), key, true);
+        }
+        if (q + 1 < ROUNDS) __syncthreads();
+    }
+}
+
 // ---- atomic-free reservation: per-tile counts of the tile's window (the level-1 segment of its
 // first key), a column scan per segment, and the partition pass reading its row of offsets
 constexpr int PT_TILE = 16384, PT_W = 512;
@@ -456,37 +532,39 @@ int main(int argc, char **argv) {
         copy_nt_kernel<<<dim3((unsigned)ceil_div(n / 2, 1024)), dim3(256), 0, s>>>((const ulonglong2 *)a, (ulonglong2 *)o, n / 2);
     });
     run("product 1024 nt (9-bit)", 18, [&] {
-        msd_partition_kernel<1, false, 1024, true><<<dim3((unsigned)ceil_div(n, 16384)), dim3(1024), 0, s>>>(
+        msd_partition_kernel<1, false, 1024, true><<<dim3((unsigned)xcd_grid(ceil_div(n, 16384))), dim3(1024), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
     run("product 1024 (9-bit)", 18, [&] {
-        msd_partition_kernel<1, false, 1024, false><<<dim3((unsigned)ceil_div(n, 16384)), dim3(1024), 0, s>>>(
+        msd_partition_kernel<1, false, 1024, false><<<dim3((unsigned)xcd_grid(ceil_div(n, 16384))), dim3(1024), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
     run("product 512 nt (9-bit, 8K tiles)", 18, [&] {
-        msd_partition_kernel<1, false, 512, true><<<dim3((unsigned)ceil_div(n, 8192)), dim3(512), 0, s>>>(
+        msd_partition_kernel<1, false, 512, true><<<dim3((unsigned)xcd_grid(ceil_div(n, 8192))), dim3(512), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
     run("product 1024 nt (8-bit)", 17, [&] {
-        msd_partition_kernel<1, false, 1024, true><<<dim3((unsigned)ceil_div(n, 16384)), dim3(1024), 0, s>>>(
+        msd_partition_kernel<1, false, 1024, true><<<dim3((unsigned)xcd_grid(ceil_div(n, 16384))), dim3(1024), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 17, bp, cur);
     });
     const unsigned g16 = (unsigned)ceil_div(n, 16384);
-    run("vec: 16B loads, nt", 18, [&] {
-        part_vec_kernel<true, true, false><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
+    run("rounds=1 (product layout)", 18, [&] {
+        part_rounds_kernel<1><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
     });
-    run("vec: 16B stores, nt", 18, [&] {
-        part_vec_kernel<true, false, true><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
+    run("rounds=2 (64 KiB LDS, 2 WG/CU)", 18, [&] {
+        part_rounds_kernel<2><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
     });
-    run("vec: 16B loads + stores, nt", 18, [&] {
-        part_vec_kernel<true, true, true><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
+    const unsigned g16x = (unsigned)(8 * ((g16 + 7) / 8));
+    run("rounds=1, XCD-contiguous tiles", 18, [&] {
+        part_rounds_kernel<1, true><<<dim3(g16x), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
     });
-    run("vec: 16B loads + stores", 18, [&] {
-        part_vec_kernel<false, true, true><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
+    run("rounds=2, XCD-contiguous tiles", 18, [&] {
+        part_rounds_kernel<2, true><<<dim3(g16x), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
     });
-    run("vec: 16B loads + stores, nt, 8-bit", 17, [&] {
-        part_vec_kernel<true, true, true><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 17, bp, cur);
+    run("rounds=2, 8-bit", 17, [&] {
+        part_rounds_kernel<2><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 17, bp, cur);
     });
+    if (argc > 3) {
     {  // atomic-free reservation
         const uint64_t nt = ceil_div(n, PT_TILE);
         uint32_t *rows, *tseg, *extra;
@@ -549,5 +627,6 @@ int main(int argc, char **argv) {
     run("persistent grid=CUs (no nt)", 18, [&] {
         part_persist_kernel<false><<<dim3(cus), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur, ceil_div(n, 16384));
     });
+    }
     return 0;
 }

@@ -307,10 +307,10 @@ static void partition_bench(hipStream_t s, uint64_t n) {
                 t = time_ms(s, 3, [&] {
                     HIP_CHECK(hipMemcpyAsync(cur2, st2.data(), (1u << bits) * 8, hipMemcpyHostToDevice, s));
                     if (blk == 512)
-                        msd_partition_kernel<1, false, 512><<<dim3((unsigned)ptiles), dim3(512), 0, s>>>(
+                        msd_partition_kernel<1, false, 512><<<dim3((unsigned)xcd_grid(ptiles)), dim3(512), 0, s>>>(
                             a, b, nullptr, nullptr, n, 62, bits, 0, cur2);
                     else
-                        msd_partition_kernel<1, false, 1024><<<dim3((unsigned)ptiles), dim3(1024), 0, s>>>(
+                        msd_partition_kernel<1, false, 1024><<<dim3((unsigned)xcd_grid(ptiles)), dim3(1024), 0, s>>>(
                             a, b, nullptr, nullptr, n, 62, bits, 0, cur2);
                 });
                 printf("mode %d partition bits=%u block=%d: %.3f ms = %.0f GB/s\n", mode, bits, blk, t,
