@@ -435,17 +435,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
         EventTimer tm(c.stream);
         tm.mark();
-        if (!COUNTED && bb - bp > 8) {  // wide digits: 1024-thread tiles keep the bucket runs long
-            if constexpr (!COUNTED) {
-                constexpr int TILE2 = MsdTraits<L>::ITEMS * 1024;
-                msd_partition_kernel<L, false, 1024, true><<<dim3((unsigned)xcd_grid(ceil_div(n, TILE2))), dim3(1024), 0,
-                                                             c.stream>>>(*keys, *alt, nullptr, nullptr, n, nbits, bb,
-                                                                         bp, cur);
-            }
-        } else {
-            msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
-                *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
-        }
+        // 512-thread tiles (8 K keys, two workgroups per CU) on XCD-contiguous tiles: 3.77 ms for the
+        // cfg2 level-2 pass vs 4.09 with 1024-thread tiles (16 K keys, one per CU) -- before the XCD
+        // mapping the longer runs of the big tiles won (4.65 vs 5.3 ms); nontemporal access measured
+        // the same (tools/part_bench.hip)
+        msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
         HIP_CHECK(hipGetLastError());
         tm.mark();
         if (c.track_partition && c.radix_launches == 0) {  // first partition launch of the sort
@@ -819,10 +814,11 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         // rows in multiples of rps = pass-B tile / pass-A tile: rps consecutive rows count one
         // stripe of pass B's tiles (stripe_cursor_kernel)
         const bool fast_b = !COUNTED && K <= 32;
-        // pass-B workgroup: 1024 threads (16 K-window tiles) for the packed kernel -- the same time as
-        // 512 (7.72-7.86 vs 7.74-7.77 ms per extract stage) but runs twice as long: PMC writes 11.1
-        // vs 12.5 GB (1.16 vs 1.30 x N w); the counted kernel keeps 8 K-window tiles
-        const int fbk = fast_b ? 1024 : 512;
+        // pass-B workgroup: 512 threads (8 K-window tiles, two workgroups per CU).  With XCD-contiguous
+        // tiles and stripes the short runs of neighbouring tiles meet in one L2: extract stage 6.97 ->
+        // 5.61 ms vs 1024-thread tiles (16 K windows), which won before the XCD mapping (their longer
+        // runs: PMC writes 1.16 vs 1.30 x N w)
+        const int fbk = 512;
         const uint32_t rps = (uint32_t)(16 * fbk / TILE);
         uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
         if (nrows >= rps) nrows -= nrows % rps;
@@ -900,7 +896,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
                 per_stripe, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
         if (fast_b) {
-            constexpr int B = 1024;
+            constexpr int B = 512;
             extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * B))), dim3(B), 0,
                                                 c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, per_stripe,
                                                             scur, send, *ka, &c.small->error);

@@ -258,14 +258,16 @@ __global__ __launch_bounds__(1024) void part_vec_kernel(const Key<1> *__restrict
 // one piece): 16K-key tiles in 128 / ROUNDS KiB of LDS, two workgroups per CU at ROUNDS >= 2
 // XCD: workgroup b runs tile (b % 8) * per + b / 8, so each XCD (dispatch round-robin over 8)
 // walks its own contiguous eighth of the tiles and its L2 sees neighbouring runs of a bucket
-template <int ROUNDS, bool XCD = false>
+// XCD 2: chunks of G consecutive tiles dealt round-robin to the XCDs (all XCDs stay in one region)
+template <int ROUNDS, int XCD = 0, int G = 32>
 __global__ __launch_bounds__(1024) void part_rounds_kernel(const Key<1> *__restrict__ kin, Key<1> *__restrict__ kout,
                                                            uint64_t n, unsigned nbits, unsigned b, unsigned bp,
                                                            unsigned long long *__restrict__ cursor) {
     constexpr int ITEMS = 16, BLOCK = 1024, TILE = ITEMS * BLOCK, W = 512, SLICE = TILE / ROUNDS;
     const uint64_t ntiles = (n + TILE - 1) / TILE;
     const uint64_t per = (ntiles + 7) / 8;
-    const uint64_t tile = XCD ? (uint64_t)(blockIdx.x % 8) * per + blockIdx.x / 8 : blockIdx.x;
+    const uint64_t slot = blockIdx.x / 8, xcd = blockIdx.x % 8;
+    const uint64_t tile = XCD == 1 ? xcd * per + slot : XCD == 2 ? ((slot / G) * 8 + xcd) * G + slot % G : blockIdx.x;
     if (tile >= ntiles) return;
     __shared__ Key<1> s_keys[SLICE];
     __shared__ uint32_t s_cnt[W];
@@ -548,21 +550,13 @@ int main(int argc, char **argv) {
             a, o, nullptr, nullptr, n, nbits, 17, bp, cur);
     });
     const unsigned g16 = (unsigned)ceil_div(n, 16384);
-    run("rounds=1 (product layout)", 18, [&] {
-        part_rounds_kernel<1><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
+    run("product 256 nt (9-bit, 4K tiles)", 18, [&] {
+        msd_partition_kernel<1, false, 256, true><<<dim3((unsigned)xcd_grid(ceil_div(n, 4096))), dim3(256), 0, s>>>(
+            a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
-    run("rounds=2 (64 KiB LDS, 2 WG/CU)", 18, [&] {
-        part_rounds_kernel<2><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
-    });
-    const unsigned g16x = (unsigned)(8 * ((g16 + 7) / 8));
-    run("rounds=1, XCD-contiguous tiles", 18, [&] {
-        part_rounds_kernel<1, true><<<dim3(g16x), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
-    });
-    run("rounds=2, XCD-contiguous tiles", 18, [&] {
-        part_rounds_kernel<2, true><<<dim3(g16x), dim3(1024), 0, s>>>(a, o, n, nbits, 18, bp, cur);
-    });
-    run("rounds=2, 8-bit", 17, [&] {
-        part_rounds_kernel<2><<<dim3(g16), dim3(1024), 0, s>>>(a, o, n, nbits, 17, bp, cur);
+    run("product 512 (9-bit, 8K tiles, no nt)", 18, [&] {
+        msd_partition_kernel<1, false, 512, false><<<dim3((unsigned)xcd_grid(ceil_div(n, 8192))), dim3(512), 0, s>>>(
+            a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
     if (argc > 3) {
     {  // atomic-free reservation
