@@ -58,7 +58,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -1090,14 +1090,15 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
 template <int L2, bool COUNTED>
 static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<L2> *ka,
                          uint32_t *ca, uint64_t U, Key<L2> *buf, uint32_t *bufc, Key<L2> **rk,
-                         uint32_t **rkc, RcMerge<L2> *rm = nullptr) {
-    // rm: merge the sorted rc keys straight into rm->out (rm->done), when the MSD local pass can
+                         uint32_t **rkc, RcMerge<L2> *rm = nullptr, bool sort = true) {
+    // rm: merge the sorted rc keys straight into rm->out (rm->done), when the MSD local pass can;
+    // !sort: leave the rc keys unsorted in buf (the multi-GPU build routes them to their owners)
     using K2 = Key<L2>;
     uint64_t Urc = U;
     uint32_t *rc_hist = nullptr;
     if (K & 1) {
         unsigned rc_hist_bits = 0;
-        if (!c.use_lsd) {
+        if (!c.use_lsd && sort) {
             const MsdPlan plan = msd_plan<L2>(c, U, 2 * K, 1.0);
             if (plan.levels) {
                 rc_hist_bits = plan.digit_end[1];
@@ -1118,6 +1119,11 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
             &c.small->counter, &c.small->total, &c.small->error);
         HIP_CHECK(hipGetLastError());
         Urc = read_u64(c, &c.small->total);
+    }
+    if (!sort) {
+        *rk = buf;
+        *rkc = bufc;
+        return Urc;
     }
     K2 *ra = buf, *rb = (K2 *)c.ws.get(Workspace::RC_ALT, Urc * sizeof(K2));
     uint32_t *rca = bufc, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
@@ -1524,7 +1530,10 @@ static uint64_t *prefix_index(Ctx &c, const Dist &d, Workspace::Slot slot, const
 // also returns every array's slice offsets for those ranges (host, P + 1 each)
 template <int L2>
 static std::vector<uint64_t> dist_ranges(Ctx &c, Dist &d, int na, const Key<L2> *const *arrs,
-                                         const uint64_t *ns, std::vector<std::vector<uint64_t>> *soff) {
+                                         const uint64_t *ns, std::vector<std::vector<uint64_t>> *soff,
+                                         unsigned rc_K = 0) {
+    // rc_K (canonical mode): also count the rc keys of arrs[0] (sampled), so the ranges balance
+    // both strands of the real-edge set
     uint64_t *hist = (uint64_t *)c.ws.get(Workspace::XHIST, d.nb * 8);
     std::vector<std::vector<uint64_t>> starts(na);
     for (int a = 0; a < na; ++a) {
@@ -1533,6 +1542,13 @@ static std::vector<uint64_t> dist_ranges(Ctx &c, Dist &d, int na, const Key<L2> 
         HIP_CHECK(hipGetLastError());
         starts[a].resize(d.nb + 1);
         HIP_CHECK(hipMemcpyAsync(starts[a].data(), st, (d.nb + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+    }
+    if (rc_K && ns[0]) {
+        const uint64_t stride = std::max<uint64_t>(1, ns[0] >> 22);
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(ceil_div(ns[0], stride), 256), 4096));
+        rc_prefix_sample_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(
+            arrs[0], ns[0], rc_K, d.shift2, 2 * d.m, stride, (unsigned long long *)hist);
+        HIP_CHECK(hipGetLastError());
     }
     const int e0 = d.tm->mark();
     d.comm.allreduce_sum_u64(hist, d.nb, c.stream);
@@ -1600,7 +1616,7 @@ static uint64_t exchange_runs(Ctx &c, Dist &d, int na, const T *const *arrs, con
 template <int L, int MODE>
 static std::vector<uint64_t> route(Ctx &c, const Dist &d, const Key<L> *in, uint64_t n, unsigned K,
                                    unsigned pshift, unsigned pbits, const std::vector<uint64_t> &bounds,
-                                   Key<L> *out) {
+                                   Key<L> *out, const uint32_t *in_v = nullptr, uint32_t *out_v = nullptr) {
     const int P = d.P;
     std::vector<uint64_t> soff(P + 1, 0);
     if (!n) return soff;
@@ -1620,7 +1636,7 @@ static std::vector<uint64_t> route(Ctx &c, const Dist &d, const Key<L> *in, uint
                                                                       &c.small->counter, &c.small->error);
     HIP_CHECK(hipGetLastError());
     route_write_kernel<L, MODE><<<dim3((unsigned)ntiles), dim3(RT_BLOCK), 0, c.stream>>>(
-        in, n, K, pshift, pbits, db, (uint32_t)P, toff, ntiles, out);
+        in, n, K, pshift, pbits, db, (uint32_t)P, toff, ntiles, out, in_v, out_v);
     HIP_CHECK(hipGetLastError());
     uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, (P + 1) * 8);
     gather_strided_kernel<<<1, 256, 0, c.stream>>>(toff, ntiles, (uint32_t)P + 1, g);
@@ -1674,9 +1690,11 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     std::vector<std::vector<uint64_t>> soff;
     std::vector<uint64_t> b1;
     {
+        // canonical mode: the ranges balance both strands (the canonical keys and their rc keys)
+        // and are final, so exchange 2 moves only the rc keys
         const K2 *arrs[1] = {ka};
         const uint64_t ns[1] = {Ul};
-        b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff);
+        b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff, canonical ? K : 0);
     }
     tr("ranges 1");
     K2 *xa;
@@ -1706,59 +1724,53 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     debug_check_sorted(c, "owned k-mers", xa, U);
     const int ev_unique = tm.mark();
 
-    // ---- canonical: rc of the owned canonical set, exchange 2 of both strands by final range
+    // ---- canonical: rc of the owned canonical set, routed to the owners of the rc keys
     K2 *E = xa;
     uint32_t *Ec = xac;
     uint64_t R = U;
-    std::vector<uint64_t> bounds;
+    std::vector<uint64_t> bounds = b1;  // final in both modes
     if (canonical) {
+        // rc keys of the owned canonical set, unsorted (even K: palindromes stay out with their
+        // counts doubled, boss_chunk_construct.cpp:188-200)
         K2 *rbuf = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U, 1) * sizeof(K2));
         uint32_t *rbufc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U, 1) * 4) : nullptr;
         K2 *rk = rbuf;
         uint32_t *rkc = rbufc;
         uint64_t Urc = 0;
-        if (U) Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, xa, xac, U, rbuf, rbufc, &rk, &rkc);
-        const K2 *arrs[2] = {xa, rk};
-        const uint32_t *cnts[2] = {xac, rkc};
-        const uint64_t ns[2] = {U, Urc};
+        if (U) Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, xa, xac, U, rbuf, rbufc, &rk, &rkc, nullptr, false);
         tr("rc", Urc);
-        bounds = dist_ranges<L2>(c, d, 2, arrs, ns, &soff);
-        tr("ranges 2");
-        K2 *ra;
-        uint32_t *rac = nullptr;
-        std::vector<uint64_t> runs;
-        const uint64_t n2 = exchange_runs<K2>(c, d, 2, arrs, COUNTED ? cnts : nullptr, soff, Workspace::REAL,
-                                              Workspace::REALC, &ra, &rac, &runs);
-        tr("exchange 2", n2);
-        // The P canonical runs (array 0) came from the owners of exchange 1, whose ranges are
-        // disjoint and increase with the rank, so laid out by source rank they are already one
-        // sorted array.  Only the P rc runs need sorting: the single build's rc sort with its
-        // local pass fused with the merge into the canonical keys (local_merge_kernel), the P
-        // sorted runs gathered by bucket instead of partitioned.  All keys are distinct (a
-        // canonical k-mer and its rc are different edges; even K's palindromes left the rc set).
-        const uint64_t ncan = runs[d.P], nrc = n2 - ncan;
-        K2 *out = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(n2, 1) * sizeof(K2));
-        uint32_t *outc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(n2, 1) * 4) : nullptr;
-        K2 *rkeys = ra + ncan;
-        uint32_t *rcc = COUNTED ? rac + ncan : nullptr;
+        K2 *rsend = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(Urc, 1) * sizeof(K2));
+        uint32_t *rsendc = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_SENDC, std::max<uint64_t>(Urc, 1) * 4) : nullptr;
+        std::vector<std::vector<uint64_t>> roff(1);
+        roff[0] = route<L2, 1>(c, d, rk, Urc, K, d.shift2, 2 * d.m, bounds, rsend, COUNTED ? rkc : nullptr, rsendc);
+        tr("route rc", Urc);
+        // exchange 2: the rc keys only.  Every owned canonical key has exactly one owner, so the
+        // received rc keys are distinct, and distinct from the canonical keys (a palindrome has no
+        // rc key)
+        K2 *rkeys;
+        uint32_t *rcc = nullptr;
+        const K2 *arrs[1] = {rsend};
+        const uint32_t *cnts[1] = {rsendc};
+        const uint64_t nrc = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, roff, Workspace::REAL,
+                                               Workspace::REALC, &rkeys, &rcc);
+        tr("exchange 2", nrc);
+        // the single build's rc sort, its local pass fused with the merge into the owned canonical
+        // keys (local_merge_kernel); the keys cover ~1/P of the prefix space, so the plan is told
+        // they are as dense as P * (nrc + U) / 2 rc keys of a single build
+        K2 *out = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U + nrc, 1) * sizeof(K2));
+        uint32_t *outc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U + nrc, 1) * 4) : nullptr;
         K2 *ralt = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nrc, 1) * sizeof(K2));
         uint32_t *rcalt = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nrc, 1) * 4) : nullptr;
-        std::vector<uint64_t> rc_runs(d.P + 1);
-        for (int j = 0; j <= d.P; ++j) rc_runs[j] = runs[d.P + j] - ncan;
-        RcMerge<L2> rm{ra, rac, ncan, out, outc};
-        // plan the buckets for rc + canonical keys together (the fused pass holds both, and a
-        // low range is mostly canonical), spread over 1/P of the prefix space: as dense as a
-        // single build of P * (nrc + ncan) / 2 rc keys
-        const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + ncan)) : 1.0;
-        const uint64_t nr = msd_sort_unique<L2, COUNTED>(c, &rkeys, &ralt, &rcc, &rcalt, nrc, 2 * K, cmax,
-                                                         dupm, nullptr, true, &rc_runs, false,
-                                                         ncan ? &rm : nullptr);
-        if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, ra, rac, ncan, rkeys, rcc, nr, K, out, outc, 0);
-        R = ncan + nr;
+        RcMerge<L2> rm{xa, xac, U, out, outc};
+        const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + U)) : 1.0;
+        uint64_t nr = 0;
+        if (nrc)
+            nr = msd_sort_unique<L2, COUNTED>(c, &rkeys, &ralt, &rcc, &rcalt, nrc, 2 * K, cmax, dupm, nullptr, true,
+                                              nullptr, false, U ? &rm : nullptr);
+        if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, xa, xac, U, rkeys, rcc, nr, K, out, outc, 0);
+        R = U + nr;
         E = out;
         Ec = outc;
-    } else {
-        bounds = b1;  // basic mode: exchange 1 already placed every edge at its final owner
     }
     T.n_real = R;
     tr("owner merge", R);

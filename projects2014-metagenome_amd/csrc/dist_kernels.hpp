@@ -85,7 +85,9 @@ template <int L, int MODE>
 __global__ __launch_bounds__(RT_BLOCK) void route_write_kernel(
     const Key<L> *__restrict__ in, uint64_t n, unsigned K, unsigned pshift, unsigned pbits,
     const uint64_t *__restrict__ bounds, uint32_t P, const uint64_t *__restrict__ toff,
-    uint64_t ntiles, Key<L> *__restrict__ out) {
+    uint64_t ntiles, Key<L> *__restrict__ out, const uint32_t *__restrict__ in_v = nullptr,
+    uint32_t *__restrict__ out_v = nullptr) {
+    // in_v / out_v (optional): a count per key, moved with it
     __shared__ uint64_t s_b[MAX_RANKS + 1];
     __shared__ uint64_t s_base[MAX_RANKS];
     __shared__ uint32_t s_c[MAX_RANKS];
@@ -119,7 +121,25 @@ __global__ __launch_bounds__(RT_BLOCK) void route_write_kernel(
             if (valid && o == lo) pos = b + (uint32_t)__popcll(same & lanemask_lt());
             active &= ~same;
         }
-        if (valid) out[s_base[o] + pos] = y;
+        if (valid) {
+            out[s_base[o] + pos] = y;
+            if (in_v) out_v[s_base[o] + pos] = in_v[i];
+        }
+    }
+}
+
+// Balancing samples of the reverse-complement set: every stride-th canonical key x adds stride
+// to hist[prefix of rc(x)] (the rc keys of the owned canonical set go to those prefixes' owners,
+// so the ranges are balanced on both strands before the first exchange)
+template <int L>
+__global__ void rc_prefix_sample_kernel(const Key<L> *__restrict__ keys, uint64_t n, unsigned K,
+                                        unsigned pshift, unsigned pbits, uint64_t stride,
+                                        unsigned long long *__restrict__ hist) {
+    const uint64_t ns = (n + stride - 1) / stride;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gs) {
+        const Key<L> r = revcomp2(keys[j * stride], K);
+        atomicAdd(&hist[bits_at(shr(r, pshift), 0, pbits)], (unsigned long long)stride);
     }
 }
 
