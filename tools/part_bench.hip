@@ -458,6 +458,28 @@ __global__ __launch_bounds__(1024) void part_pre_kernel(const Key<1> *__restrict
     }
 }
 
+// exclusive scan of h[b0 .. b0 + nb) plus base into cur[b0 ..) (one workgroup of 1024)
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__restrict__ h, uint32_t b0, uint32_t nb,
+                                                          unsigned long long base, unsigned long long *__restrict__ cur) {
+    __shared__ unsigned long long s[1024];
+    const uint32_t per = (nb + 1023) / 1024, i0 = threadIdx.x * per;
+    unsigned long long t = 0;
+    for (uint32_t j = 0; j < per && i0 + j < nb; ++j) t += h[b0 + i0 + j];
+    s[threadIdx.x] = t;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const unsigned long long v = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long acc = base + s[threadIdx.x] - t;
+    for (uint32_t j = 0; j < per && i0 + j < nb; ++j) {
+        cur[b0 + i0 + j] = acc;
+        acc += h[b0 + i0 + j];
+    }
+}
+
 int main(int argc, char **argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1200000000ull;
     const int reps = argc > 2 ? atoi(argv[2]) : 3;
@@ -533,7 +555,7 @@ int main(int argc, char **argv) {
     run("copy (one-shot nt 16B)", 0, [&] {
         copy_nt_kernel<<<dim3((unsigned)ceil_div(n / 2, 1024)), dim3(256), 0, s>>>((const ulonglong2 *)a, (ulonglong2 *)o, n / 2);
     });
-    run("product 1024 nt (9-bit)", 18, [&] {
+    if (argc > 4) run("product 1024 nt (9-bit)", 18, [&] {
         msd_partition_kernel<1, false, 1024, true><<<dim3((unsigned)xcd_grid(ceil_div(n, 16384))), dim3(1024), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
@@ -555,6 +577,39 @@ int main(int argc, char **argv) {
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
     run("product 512 (9-bit, 8K tiles, no nt)", 18, [&] {
+        msd_partition_kernel<1, false, 512, false><<<dim3((unsigned)xcd_grid(ceil_div(n, 8192))), dim3(512), 0, s>>>(
+            a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
+    });
+    // level 2 chunk by chunk (C level-1 buckets each): histogram, scan, partition of the same
+    // chunk back to back, so the partition re-reads the chunk from the MALL instead of HBM
+    for (unsigned C : {2u, 4u, 8u, 16u, 64u}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "chunked hist+part C=%u", C);
+        run(nm, 0, [&] {
+            HIP_CHECK(hipMemsetAsync(h, 0, (1u << 18) * 4, s));
+            for (unsigned b = 0; b < 512; b += C) {
+                const uint64_t lo = (uint64_t)(((unsigned __int128)b * n + 511) / 512);
+                const uint64_t hi = std::min<uint64_t>(n, (uint64_t)(((unsigned __int128)(b + C) * n + 511) / 512));
+                const uint64_t m = hi - lo;
+                msd_hist_kernel<1><<<dim3((unsigned)ceil_div(m, MsdTraits<1>::TILE)), dim3(MSD_BLOCK), 0, s>>>(a + lo, m, nbits, 18, bp, h);
+                chunk_scan_kernel<<<1, 1024, 0, s>>>(h, b << 9, C << 9, lo, cur);
+                msd_partition_kernel<1, false, 512, false><<<dim3((unsigned)xcd_grid(ceil_div(m, 8192))), dim3(512), 0, s>>>(
+                    a + lo, o, nullptr, nullptr, m, nbits, 18, bp, cur);
+            }
+        });
+        // check with the 18-bit prefix order
+        uint32_t bd = 0;
+        HIP_CHECK(hipMemsetAsync(bad, 0, 4, s));
+        HIP_CHECK(hipMemsetAsync(sum, 0, 8, s));
+        check_kernel<<<8192, 256, 0, s>>>(o, n, nbits - 18, sum, bad);
+        HIP_CHECK(hipMemcpyAsync(&bd, bad, 4, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        printf("   18-bit order: %s\n", bd ? "WRONG" : "ok");
+    }
+    run("global hist + part 512 (product)", 0, [&] {
+        HIP_CHECK(hipMemsetAsync(h, 0, (1u << 18) * 4, s));
+        msd_hist_kernel<1><<<dim3((unsigned)ceil_div(n, MsdTraits<1>::TILE)), dim3(MSD_BLOCK), 0, s>>>(a, n, nbits, 18, bp, h);
+        chunk_scan_kernel<<<1, 1024, 0, s>>>(h, 0, 1u << 18, 0, cur);
         msd_partition_kernel<1, false, 512, false><<<dim3((unsigned)xcd_grid(ceil_div(n, 8192))), dim3(512), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
