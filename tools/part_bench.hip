@@ -480,6 +480,18 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__rest
     }
 }
 
+// level-2 histogram by one global atomic per key (the cost of counting inside K1 pass B)
+__global__ __launch_bounds__(256) void atomic_hist_kernel(const Key<1> *__restrict__ k, uint64_t n, uint32_t *__restrict__ h) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+        const ulonglong2 a = *(const ulonglong2 *)(k + i), b = *(const ulonglong2 *)(k + i + 2);
+        atomicAdd(&h[a.x >> 44], 1u);
+        atomicAdd(&h[a.y >> 44], 1u);
+        atomicAdd(&h[b.x >> 44], 1u);
+        atomicAdd(&h[b.y >> 44], 1u);
+    }
+}
+
 int main(int argc, char **argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1200000000ull;
     const int reps = argc > 2 ? atoi(argv[2]) : 3;
@@ -580,6 +592,16 @@ int main(int argc, char **argv) {
         msd_partition_kernel<1, false, 512, false><<<dim3((unsigned)xcd_grid(ceil_div(n, 8192))), dim3(512), 0, s>>>(
             a, o, nullptr, nullptr, n, nbits, 18, bp, cur);
     });
+    run("atomic level-2 hist (1 atomic/key)", 0, [&] {
+        HIP_CHECK(hipMemsetAsync(h, 0, (1u << 18) * 4, s));
+        atomic_hist_kernel<<<dim3(8192), dim3(256), 0, s>>>(a, n, h);
+        copy_nt_kernel<<<1, 256, 0, s>>>((const ulonglong2 *)a, (ulonglong2 *)o, 0);
+    });
+    run("msd_hist level 2 (product)", 0, [&] {
+        HIP_CHECK(hipMemsetAsync(h, 0, (1u << 18) * 4, s));
+        msd_hist_kernel<1><<<dim3((unsigned)ceil_div(n, MsdTraits<1>::TILE)), dim3(MSD_BLOCK), 0, s>>>(a, n, nbits, 18, bp, h);
+    });
+    if (argc > 4)
     // level 2 chunk by chunk (C level-1 buckets each): histogram, scan, partition of the same
     // chunk back to back, so the partition re-reads the chunk from the MALL instead of HBM
     for (unsigned C : {2u, 4u, 8u, 16u, 64u}) {
