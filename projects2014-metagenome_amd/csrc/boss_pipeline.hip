@@ -2142,6 +2142,7 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
     c->params.filter_suffix = nullptr;  // the caller's string need not outlive the call
     c->suffix = suffix;
     c->device = p->device_id;
+    c->stage.enable_mirror(c->device);
     try {
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
@@ -2413,7 +2414,7 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
     try {
         HIP_CHECK(hipSetDevice(c->device));
         hipStream_t s = c->ctx.stream;
-        const HostStage &st = c->stage;
+        HostStage &st = c->stage;
         const uint64_t len = st.size();
         const uint64_t nr = st.n_reads();
         uint64_t kmc_bytes = 0, kmc_reads = 0;
@@ -2429,9 +2430,13 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
             split_fasta_files(c, nullptr, &sb, nullptr, nullptr, &fa_reads, true);
         }
         const uint64_t total_len = len + kmc_bytes + fa_bytes, total_reads = nr + kmc_reads + fa_reads;
-        uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
         const auto t_h2d = std::chrono::steady_clock::now();
-        if (len) HIP_CHECK(hipMemcpyAsync(dseq, st.data(), len, hipMemcpyHostToDevice, s));
+        // reads only: the stage's device mirror already holds them (copied while they were staged)
+        uint8_t *dseq = len && total_len == len ? (uint8_t *)c->stage.mirror_wait() : nullptr;
+        if (!dseq) {
+            dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
+            if (len) HIP_CHECK(hipMemcpyAsync(dseq, st.data(), len, hipMemcpyHostToDevice, s));
+        }
         uint64_t *dstarts = nullptr;
         uint32_t *dcounts = nullptr;
         const bool per_read = c->params.bits_per_count && per_read_inputs && total_reads;

@@ -5,13 +5,17 @@
 // (cli/build.cpp:31-56 -> KmerCollector::add_sequences, kmer_collector.cpp:194-226, which enqueues
 // the batch on a thread pool under a mutex).  Here a batch reserves its byte range under a short
 // exclusive lock and is copied in under a shared lock, so concurrent adders copy in parallel and
-// only a buffer growth serialises them.  The buffer is pinned host memory, so the build's single
-// host-to-device copy of the reads runs at PCIe/xGMI DMA speed instead of through a bounce buffer.
+// only a buffer growth serialises them.  The buffer is pinned host memory, and every adder thread
+// hands each 32 MiB piece it has copied to a copy stream that DMAs it into a device mirror of the
+// buffer, so the reads' host-to-device copy runs while later reads are still being staged (the
+// build then only waits for the last pieces).
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -24,6 +28,18 @@
 #include <vector>
 
 namespace mtg {
+
+// sets the calling thread's HIP device for a scope and restores the previous one
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 // Pinned host blocks, recycled: a returned block is kept for the next request of at most its size
 // (a steady stream of builds allocates no pinned memory; pinning is the slow part of a hipHostMalloc).
@@ -94,7 +110,19 @@ static void parallel_ranges(uint64_t n, unsigned threads, uint64_t min_per_threa
 class HostStage {
   public:
     ~HostStage() {
+        if (stream_) {
+            DeviceGuard g(device_);
+            (void)hipStreamSynchronize(stream_);
+            (void)hipStreamDestroy(stream_);
+        }
+        if (dmirror_) (void)hipFree(dmirror_);
         if (data_) (void)hipHostFree(data_);
+    }
+
+    // copy staged pieces to a device mirror on `device` as they are written (see the header)
+    void enable_mirror(int device) {
+        device_ = device;
+        mirror_ = true;
     }
 
     // n reads: read i is `lens[i]` bytes at ptrs[i]; counts may be null (all 1).
@@ -129,6 +157,13 @@ class HostStage {
         {
             std::unique_lock<std::shared_mutex> ex(grow_);
             if (size_ + total > cap_) grow(std::max<uint64_t>(size_ + total, cap_ + cap_ / 2));
+            if (mirror_ && !mirror_ready()) {
+                try {
+                    grow_mirror();
+                } catch (const std::exception &) {
+                    mirror_ = false;  // no device memory for a mirror: the build copies the reads itself
+                }
+            }
             off = size_;
             size_ += total;
             uint64_t pos = off;
@@ -150,17 +185,35 @@ class HostStage {
         }
         std::shared_lock<std::shared_mutex> sh(grow_);  // a growth waits for the copy
         char *dst = data_ + off;
+        const bool mirror = mirror_ready();
         parallel_ranges(t, t, 1, [&](uint64_t c0, uint64_t c1) {
+            std::unique_ptr<DeviceGuard> g;
+            if (mirror) g.reset(new DeviceGuard(device_));
             for (uint64_t c = c0; c < c1; ++c) {
-                uint64_t o = cbase[c];
+                uint64_t o = cbase[c], piece = o;
                 for (uint64_t i = n * c / t; i < n * (c + 1) / t; ++i) {
                     const uint64_t l = len(i);
                     std::memcpy(dst + o, ptr(i), l);
                     dst[o + l] = '$';
                     o += l + 1;
+                    if (mirror && o - piece >= kPiece) {
+                        send(off + piece, o - piece);
+                        piece = o;
+                    }
                 }
+                if (mirror && o > piece) send(off + piece, o - piece);
             }
         });
+    }
+
+    // the device mirror holds (or has in flight) every staged byte
+    bool mirror_ready() const { return mirror_ && dmirror_ && dcap_ >= cap_; }
+    // wait for the mirror's copies; returns the device copy of data() (null: no mirror)
+    const uint8_t *mirror_wait() {
+        if (!mirror_ready() || mirror_failed_) return nullptr;
+        DeviceGuard g(device_);
+        if (hipStreamSynchronize(stream_) != hipSuccess || mirror_failed_) return nullptr;
+        return dmirror_;
     }
 
     const char *data() const { return data_; }
@@ -172,6 +225,11 @@ class HostStage {
     // the build consumed the staged reads (the pinned buffer is kept for the next batch)
     void clear() {
         std::unique_lock<std::shared_mutex> ex(grow_);
+        if (stream_) {
+            DeviceGuard g(device_);
+            (void)hipStreamSynchronize(stream_);
+        }
+        mirror_failed_ = false;
         size_ = 0;
         run_end_ = ~0ull;
         starts_.clear();
@@ -181,8 +239,40 @@ class HostStage {
     std::shared_mutex &lock() { return grow_; }
 
   private:
+    static constexpr uint64_t kPiece = 32ull << 20;
+
+    void send(uint64_t at, uint64_t bytes) {
+        if (hipMemcpyAsync(dmirror_ + at, data_ + at, bytes, hipMemcpyHostToDevice, stream_) != hipSuccess)
+            mirror_failed_ = true;  // the build falls back to its own copy
+    }
+
+    // device mirror of the host capacity (under the exclusive lock); keeps the bytes staged so far
+    void grow_mirror() {
+        DeviceGuard g(device_);
+        if (!stream_ && hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess)
+            throw std::runtime_error("copy stream");
+        uint8_t *p = nullptr;
+        if (hipMalloc((void **)&p, cap_ + 64) != hipSuccess) throw std::runtime_error("mirror allocation");
+        if (hipStreamSynchronize(stream_) != hipSuccess ||
+            (size_ && dmirror_ && hipMemcpyAsync(p, dmirror_, size_, hipMemcpyDeviceToDevice, stream_) != hipSuccess) ||
+            hipStreamSynchronize(stream_) != hipSuccess) {
+            (void)hipFree(p);
+            throw std::runtime_error("mirror copy");
+        }
+        if (size_ && !dmirror_) {  // staged before the mirror existed
+            if (hipMemcpyAsync(p, data_, size_, hipMemcpyHostToDevice, stream_) != hipSuccess) mirror_failed_ = true;
+        }
+        if (dmirror_) (void)hipFree(dmirror_);
+        dmirror_ = p;
+        dcap_ = cap_;
+    }
+
     void grow(uint64_t want) {
         want = std::max<uint64_t>(want, 1u << 20);
+        if (stream_) {  // in-flight mirror copies read the old buffer
+            DeviceGuard g(device_);
+            (void)hipStreamSynchronize(stream_);
+        }
         char *p = nullptr;
         if (hipHostMalloc((void **)&p, want, hipHostMallocDefault) != hipSuccess || !p)
             throw std::runtime_error("pinned host allocation of " + std::to_string(want) + " bytes failed");
@@ -193,6 +283,12 @@ class HostStage {
     }
 
     std::shared_mutex grow_;
+    int device_ = 0;
+    bool mirror_ = false;
+    std::atomic<bool> mirror_failed_{false};
+    hipStream_t stream_ = nullptr;
+    uint8_t *dmirror_ = nullptr;
+    uint64_t dcap_ = 0;
     char *data_ = nullptr;
     uint64_t size_ = 0, cap_ = 0;
     std::vector<uint64_t> starts_;
