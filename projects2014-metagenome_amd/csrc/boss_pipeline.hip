@@ -58,7 +58,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -2083,6 +2083,31 @@ struct mtg_boss_ctor {
     }
 };
 
+// staged reads (host_stage.hpp) -> one byte per char: ACGT, or 'N' for every char that breaks a
+// k-mer window (separators, alignment gaps, N and the rest); one 32-char word per thread
+__global__ void unpack_reads_kernel(const uint64_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+                                    uint64_t nw, uint8_t *__restrict__ out) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint64_t c = codes[w];
+    const uint32_t v = valid[w];
+    uint32_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int j = 4 * q + b;
+            const uint32_t ch = (v >> j) & 1u ? (0x54474341u >> (8 * ((c >> (2 * j)) & 3u))) & 0xFFu : (uint32_t)'N';
+            word |= ch << (8 * b);
+        }
+        o[q] = word;
+    }
+    uint4 *dst = (uint4 *)(out + 32 * w);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
 // one packed `last` word per thread: bit j of word w = last[64 w + j] (sdsl bit_vector layout)
 __global__ void pack_bits_kernel(const uint8_t *__restrict__ bytes, uint64_t n, uint64_t *__restrict__ words) {
     const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2431,11 +2456,22 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         }
         const uint64_t total_len = len + kmc_bytes + fa_bytes, total_reads = nr + kmc_reads + fa_reads;
         const auto t_h2d = std::chrono::steady_clock::now();
-        // reads only: the stage's device mirror already holds them (copied while they were staged)
-        uint8_t *dseq = len && total_len == len ? (uint8_t *)c->stage.mirror_wait() : nullptr;
-        if (!dseq) {
-            dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
-            if (len) HIP_CHECK(hipMemcpyAsync(dseq, st.data(), len, hipMemcpyHostToDevice, s));
+        uint8_t *dseq = (uint8_t *)c->ctx.ws.get(Workspace::SEQ, total_len + 1);
+        if (len) {
+            // the staged 2-bit codes + valid mask: on the device already (the stage's mirror, copied
+            // while the reads were staged), else copied now; unpacked to one byte per char
+            const uint64_t nw = len / 32;
+            const uint64_t *dcodes = nullptr;
+            const uint32_t *dvalid = nullptr;
+            if (!st.mirror_wait(&dcodes, &dvalid)) {
+                uint64_t *pk = (uint64_t *)c->ctx.ws.get(Workspace::PACKED, nw * 12);
+                HIP_CHECK(hipMemcpyAsync(pk, st.codes(), nw * 8, hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(pk + nw, st.valid(), nw * 4, hipMemcpyHostToDevice, s));
+                dcodes = pk;
+                dvalid = (const uint32_t *)(pk + nw);
+            }
+            unpack_reads_kernel<<<dim3((unsigned)ceil_div(nw, 256)), dim3(256), 0, s>>>(dcodes, dvalid, nw, dseq);
+            HIP_CHECK(hipGetLastError());
         }
         uint64_t *dstarts = nullptr;
         uint32_t *dcounts = nullptr;
