@@ -27,7 +27,11 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include "device_common.hpp"
+#include "host_stage.hpp"
 
 namespace mtg {
 
@@ -48,26 +52,50 @@ struct FastaInput {
 inline FastaInput load_fasta_file(const std::string &path) {
     FastaInput in;
     in.path = path;
-    gzFile f = gzopen(path.c_str(), "rb");  // reads plain files too (transparent mode)
-    if (!f) throw std::runtime_error("ERROR: Cannot read from file " + path);
-    gzbuffer(f, 1u << 20);
-    uint64_t cap = 0;
+    uint64_t fsize = 0;
+    bool gz = false;
     {
-        FILE *p = std::fopen(path.c_str(), "rb");
-        if (p) {
-            std::fseek(p, 0, SEEK_END);
-            const long s = std::ftell(p);
-            std::fclose(p);
-            cap = s > 0 ? (uint64_t)s : 0;
+        const int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) throw std::runtime_error("ERROR: Cannot read from file " + path);
+        const off_t end = ::lseek(fd, 0, SEEK_END);
+        fsize = end > 0 ? (uint64_t)end : 0;
+        unsigned char magic[2] = {0, 0};
+        gz = fsize >= 2 && ::pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        if (!gz) {
+            // plain file: straight into a pinned block from the pool (steady-state builds pin
+            // nothing new), large reads, no zlib copy
+            char *buf = (char *)PinnedPool::get().take(fsize + 1);
+            uint64_t size = 0;
+            while (size < fsize) {
+                const ssize_t got = ::pread(fd, buf + size, (size_t)std::min<uint64_t>(fsize - size, 1ull << 30), (off_t)size);
+                if (got < 0) {
+                    ::close(fd);
+                    if (!PinnedPool::get().give(buf)) (void)hipHostFree(buf);
+                    throw std::runtime_error("ERROR: Cannot read from file " + path);
+                }
+                if (got == 0) break;
+                size += (uint64_t)got;
+            }
+            ::close(fd);
+            in.data = buf;
+            in.size = size;
+        } else {
+            ::close(fd);
         }
     }
-    cap = std::max<uint64_t>(cap + (1u << 16), 1u << 20);
-    char *buf = nullptr;
+    char *buf = in.data;
+    uint64_t size = in.size;
+    if (gz) {
+    gzFile f = gzopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("ERROR: Cannot read from file " + path);
+    gzbuffer(f, 1u << 20);
+    uint64_t cap = std::max<uint64_t>(fsize + (1u << 16), 1u << 20);
+    buf = nullptr;
     if (hipHostMalloc((void **)&buf, cap, hipHostMallocDefault) != hipSuccess) {
         gzclose(f);
         throw std::runtime_error("pinned host allocation failed for " + path);
     }
-    uint64_t size = 0;
+    size = 0;
     while (true) {
         if (size == cap) {  // compressed input: grow (x2) and keep what is read
             char *nb = nullptr;
@@ -92,6 +120,7 @@ inline FastaInput load_fasta_file(const std::string &path) {
         size += (uint64_t)got;
     }
     gzclose(f);
+    }
     in.data = buf;
     in.size = size;
     uint64_t i = 0;
@@ -109,7 +138,7 @@ inline FastaInput load_fasta_file(const std::string &path) {
 }
 
 inline void free_fasta(FastaInput &in) {
-    if (in.data) (void)hipHostFree(in.data);
+    if (in.data && !PinnedPool::get().give(in.data)) (void)hipHostFree(in.data);
     in.data = nullptr;
 }
 

@@ -85,7 +85,7 @@ class PinnedPool {
     }
 
   private:
-    static constexpr size_t kKeep = 8;
+    static constexpr size_t kKeep = 16;
     std::mutex mu_;
     std::multimap<size_t, void *> free_;
     std::unordered_map<void *, size_t> size_;
