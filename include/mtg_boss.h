@@ -130,8 +130,9 @@ typedef struct mtg_boss_timings {
     uint64_t n_sent;             /* multi-GPU: elements sent to other ranks */
     uint64_t world;              /* ranks of the build (1 = single GPU) */
     /* host-buffer builds (mtg_boss_ctor_build_chunk): wall times of the host-side stages */
-    double stage_ms;             /* add_* calls since the previous build (copy into pinned memory) */
-    double h2d_ms;               /* reads -> HBM */
+    double stage_ms;             /* add_* calls since the previous build (reads packed to 2-bit codes + a
+                                    valid mask in pinned memory, DMA'd to HBM piece by piece meanwhile) */
+    double h2d_ms;               /* the wait for the last read pieces + their unpack in HBM */
     double d2h_ms;               /* W, packed last, weights -> pinned host blocks */
     double host_total_ms;        /* the whole build_chunk call */
     uint64_t n_batches;          /* key-range batches of the build (1 = the input fit at once) */
