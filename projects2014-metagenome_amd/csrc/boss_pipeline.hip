@@ -58,7 +58,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -2078,8 +2078,11 @@ struct mtg_boss_ctor {
     std::atomic<uint64_t> stage_ns{0};  // host time spent staging since the last build
     std::mutex fa_mu;
     std::vector<mtg::FastaInput> fasta;  // FASTA / FASTQ files, split into reads on the device
+    uint8_t *w4_host = nullptr;          // pinned landing buffer of the 4-bit W copy
+    uint64_t w4_cap = 0;
     ~mtg_boss_ctor() {
         for (auto &f : fasta) mtg::free_fasta(f);
+        if (w4_host) (void)hipHostFree(w4_host);
     }
 };
 
@@ -2419,6 +2422,112 @@ static double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// W (values 0..9) crosses PCIe as 4-bit codes: packed on the device, copied in pieces, and
+// unpacked by the host threads as the pieces land (half the bytes of the largest D2H)
+__global__ void pack_w4_kernel(const uint8_t *__restrict__ w, uint64_t n, uint8_t *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16 output bytes each
+    const uint64_t b0 = i * 32;
+    if (b0 >= n) return;
+    uint32_t o[4] = {0, 0, 0, 0};
+    if (b0 + 32 <= n) {
+        const uint4 a = *(const uint4 *)(w + b0), b = *(const uint4 *)(w + b0 + 16);
+        const uint32_t in[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {  // 4 W bytes -> 2 packed bytes
+            const uint32_t v = in[q];
+            const uint32_t p = (v & 0xF) | ((v >> 4) & 0xF0) | (((v >> 16) & 0xF) << 8) | (((v >> 24) & 0xF) << 12);
+            o[q / 2] |= p << (16 * (q & 1));
+        }
+    } else {
+        for (uint64_t j = b0; j < n; ++j) {
+            const uint32_t k = (uint32_t)(j - b0);
+            o[k / 8] |= (uint32_t)(w[j] & 0xF) << (4 * (k % 8));
+        }
+    }
+    const uint64_t nb = (n + 1) / 2, ob = b0 / 2;
+    if (ob + 16 <= nb) {
+        *(uint4 *)(out + ob) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+        for (uint64_t j = ob; j < nb; ++j) out[j] = (uint8_t)(o[(j - ob) / 4] >> (8 * ((j - ob) % 4)));
+    }
+}
+
+__attribute__((target("avx2"))) static void unpack_w4_avx2(const uint8_t *in, uint64_t nbytes, uint8_t *out) {
+    uint64_t i = 0;
+    const __m256i m = _mm256_set1_epi8(0x0F);
+    for (; i + 32 <= nbytes; i += 32) {
+        const __m256i v = _mm256_loadu_si256((const __m256i *)(in + i));
+        const __m256i lo = _mm256_and_si256(v, m), hi = _mm256_and_si256(_mm256_srli_epi16(v, 4), m);
+        const __m256i a = _mm256_unpacklo_epi8(lo, hi), b = _mm256_unpackhi_epi8(lo, hi);
+        _mm256_storeu_si256((__m256i *)(out + 2 * i), _mm256_permute2x128_si256(a, b, 0x20));
+        _mm256_storeu_si256((__m256i *)(out + 2 * i + 32), _mm256_permute2x128_si256(a, b, 0x31));
+    }
+    for (; i < nbytes; ++i) {
+        out[2 * i] = in[i] & 0xF;
+        out[2 * i + 1] = in[i] >> 4;
+    }
+}
+
+static void unpack_w4(const uint8_t *in, uint64_t nbytes, uint8_t *out) {
+    if (__builtin_cpu_supports("avx2")) return unpack_w4_avx2(in, nbytes, out);
+    for (uint64_t i = 0; i < nbytes; ++i) {
+        out[2 * i] = in[i] & 0xF;
+        out[2 * i + 1] = in[i] >> 4;
+    }
+}
+
+static unsigned stage_threads(const mtg_boss_ctor *c);
+
+// W[0..n) on the device -> host W (out, n bytes): 4-bit pieces of 16 MiB, unpacked as they land
+static void copy_w_to_host(mtg_boss_ctor *c, const uint8_t *dW, uint64_t n, uint8_t *out) {
+    if (!n) return;
+    hipStream_t s = c->ctx.stream;
+    if (n < (64ull << 20)) {  // small W: one plain copy (the pieces' sync and thread costs do not pay)
+        HIP_CHECK(hipMemcpyAsync(out, dW, n, hipMemcpyDeviceToHost, s));
+        return;
+    }
+    const uint64_t nb = (n + 1) / 2;
+    uint8_t *d4 = (uint8_t *)c->ctx.ws.get(Workspace::W4, nb + 16);
+    pack_w4_kernel<<<dim3((unsigned)ceil_div(ceil_div(n, 32), 256)), dim3(256), 0, s>>>(dW, n, d4);
+    HIP_CHECK(hipGetLastError());
+    if (c->w4_cap < nb + 16) {  // the ctor's pinned landing buffer, grown on demand
+        if (c->w4_host) (void)hipHostFree(c->w4_host);
+        c->w4_host = nullptr;
+        c->w4_cap = 0;
+        HIP_CHECK(hipHostMalloc((void **)&c->w4_host, nb + nb / 4 + 16, hipHostMallocDefault));
+        c->w4_cap = nb + nb / 4 + 16;
+    }
+    uint8_t *h4 = c->w4_host;
+    constexpr uint64_t PIECE = 16ull << 20;  // packed bytes per piece
+    const uint64_t np = ceil_div(nb, PIECE);
+    std::vector<hipEvent_t> ev(np);
+    for (uint64_t p = 0; p < np; ++p) {
+        const uint64_t b0 = p * PIECE, len = std::min(PIECE, nb - b0);
+        HIP_CHECK(hipEventCreateWithFlags(&ev[p], hipEventDisableTiming));
+        HIP_CHECK(hipMemcpyAsync(h4 + b0, d4 + b0, len, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipEventRecord(ev[p], s));
+    }
+    const unsigned T = std::max(1u, std::min<unsigned>(stage_threads(c), (unsigned)np));
+    std::atomic<bool> failed{false};
+    parallel_ranges(T, T, 1, [&](uint64_t t0, uint64_t t1) {
+        DeviceGuard g(c->device);
+        for (uint64_t t = t0; t < t1; ++t)
+            for (uint64_t p = t; p < np; p += T) {
+                if (hipEventSynchronize(ev[p]) != hipSuccess) {
+                    failed = true;
+                    return;
+                }
+                const uint64_t b0 = p * PIECE, len = std::min(PIECE, nb - b0);
+                // the last packed byte of an odd n holds one W value
+                const uint64_t full = (b0 + len == nb && (n & 1)) ? len - 1 : len;
+                unpack_w4(h4 + b0, full, out + 2 * b0);
+                if (full < len) out[2 * (b0 + full)] = h4[b0 + full] & 0xF;
+            }
+    });
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (failed) throw std::runtime_error("W copy to the host failed");
+}
+
 // build_chunk on the staged reads: one H2D copy of the pinned read buffer (+ KMC records), the
 // device path, then W / packed last / weights D2H into pinned blocks the chunk owns
 static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *out) {
@@ -2527,12 +2636,12 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         PinnedPool &pool = PinnedPool::get();
         out->W = (uint8_t *)pool.take(o.n);
         out->last = (uint64_t *)pool.take(std::max<uint64_t>(nwords, 1) * 8);
-        HIP_CHECK(hipMemcpyAsync(out->W, o.W, o.n, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipMemcpyAsync(out->last, dbits, nwords * 8, hipMemcpyDeviceToHost, s));
         if (o.weights) {
             out->weights = (uint32_t *)pool.take(o.n * 4);
             HIP_CHECK(hipMemcpyAsync(out->weights, o.weights, o.n * 4, hipMemcpyDeviceToHost, s));
         }
+        copy_w_to_host(c, o.W, o.n, out->W);
         HIP_CHECK(hipStreamSynchronize(s));
         mtg_boss_timings &T = c->ctx.timings;
         T.d2h_ms = ms_since(t_d2h);

@@ -8,7 +8,8 @@ boss_chunk.cpp:32-133).
 * configs[0]: `build -k 12` on the whole transcripts_1000.fa (k_b = 11), basic and canonical;
 * k = 63 (2-bit u128 keys, lifted u256) on more than 4 M windows;
 * the full bench size (10 M reads, 1.2e9 windows), where the oracle would take minutes: the build
-  is invariant under the order of the reads and its size identities hold.
+  is invariant under the order of the reads, its size identities hold, and the host ABI (packed
+  staging, 4-bit W copy) returns the device arrays.
 """
 import importlib
 
@@ -124,3 +125,11 @@ def test_full_bench_size_order_invariant():
     a, b = out
     assert a[:3] == b[:3]
     assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+    # the same reads through the host ABI at full size: packed staging (2-bit codes + valid mask,
+    # DMA'd while staging, unpacked on the device) and the 4-bit W copy back equal the device arrays
+    host = seq.view(n_reads, L + 1)[:, :L].contiguous().cpu().numpy()
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, num_threads=16)
+    ctor.add_packed(host.reshape(-1), np.arange(n_reads + 1, dtype=np.uint64) * L)
+    ch = ctor.build_chunk()
+    assert len(ch.W) == a[0] and list(ch.F) == a[2]
+    assert np.array_equal(ch.W, a[3]) and np.array_equal(ch.last, a[4])
