@@ -2482,7 +2482,7 @@ static unsigned stage_threads(const mtg_boss_ctor *c);
 static void copy_w_to_host(mtg_boss_ctor *c, const uint8_t *dW, uint64_t n, uint8_t *out) {
     if (!n) return;
     hipStream_t s = c->ctx.stream;
-    if (n < (64ull << 20)) {  // small W: one plain copy (the pieces' sync and thread costs do not pay)
+    if (n < (128ull << 20)) {  // small W: one plain copy (the pieces' sync and thread costs do not pay)
         HIP_CHECK(hipMemcpyAsync(out, dW, n, hipMemcpyDeviceToHost, s));
         return;
     }
