@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reads", type=int, default=5_000_000)
     ap.add_argument("--k", type=int, default=31)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--no-single", action="store_true", help="skip the single build (profiling the ranks only)")
     args = ap.parse_args()
     import torch
     boss = importlib.import_module("projects2014-metagenome_amd.boss")
@@ -37,15 +38,17 @@ def main():
     whole = torch.cat(seqs)
     torch.cuda.synchronize()
     kb = args.k - 1
-    single = boss.IBOSSChunkConstructor.initialize(kb, both_strands=True)
-    for _ in range(2):
-        single.build_device(whole.data_ptr(), whole.numel())
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dc = single.build_device(whole.data_ptr(), whole.numel())
-    t_single = (time.perf_counter() - t0) / args.steps
-    ts = single.timings().as_dict()
-    rows_single = dc.n
+    t_single, ts, rows_single = 0.0, {}, None
+    if not args.no_single:
+        single = boss.IBOSSChunkConstructor.initialize(kb, both_strands=True)
+        for _ in range(2):
+            single.build_device(whole.data_ptr(), whole.numel())
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            dc = single.build_device(whole.data_ptr(), whole.numel())
+        t_single = (time.perf_counter() - t0) / args.steps
+        ts = single.timings().as_dict()
+        rows_single = dc.n
 
     comms = boss.Comm.local_group(P)
     ctors = [boss.IBOSSChunkConstructor.initialize(kb, both_strands=True) for _ in range(P)]
@@ -68,7 +71,7 @@ def main():
         step()
     t_dist = (time.perf_counter() - t0) / args.steps
     rows_dist = sum(c.n for c in res) - (P - 1)
-    assert rows_dist == rows_single, (rows_dist, rows_single)
+    assert rows_single is None or rows_dist == rows_single, (rows_dist, rows_single)
     per_rank = [c.timings().as_dict() for c in ctors]
     keys = ("extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms", "merge_ms", "emit_ms",
             "total_ms", "exchange_ms")
