@@ -190,3 +190,52 @@ def test_chunk_files_roundtrip(tmp_path, transcripts_1000):
         assert np.array_equal(back.W, want.W) and np.array_equal(back.last, want.last)
         assert list(back.F) == list(want.F)
         assert (back.weights is None) if not bits else np.array_equal(back.weights, want.weights)
+
+
+def test_concurrent_adds_and_stage_growth():
+    # host_stage.hpp: many adder threads at once (each batch reserves a 32-char-aligned range,
+    # packs 2-bit codes + the valid mask, DMAs its pieces to the device mirror), many small
+    # batches (the pinned buffers and the mirror grow under in-flight copies), single reads with
+    # counts, reads of every length mod 32 with N / lowercase / U, all in one build
+    import threading
+    rng = np.random.default_rng(77)
+    batches = []
+    for b in range(48):
+        n = int(rng.integers(1, 300))
+        lens = rng.integers(0, 460, size=n)  # ~1.7 M chars: the 1 M-char first buffer grows
+        reads = []
+        for L in lens:
+            r = rng.choice(np.frombuffer(b"ACGTacgtUuNn", dtype=np.uint8), size=int(L),
+                           p=[0.22, 0.22, 0.22, 0.22, 0.02, 0.02, 0.02, 0.02, 0.01, 0.01, 0.01, 0.01])
+            reads.append(r.tobytes())
+        counts = rng.integers(1, 70, size=n).tolist()
+        batches.append((reads, counts))
+    for canonical, bits in ((True, 8), (False, 0)):
+        ctor = boss.IBOSSChunkConstructor.initialize(20, both_strands=canonical, bits_per_count=bits,
+                                                     num_threads=4)
+
+        def worker(j):
+            for b in range(j, len(batches), 6):
+                reads, counts = batches[b]
+                if b % 3 == 0:
+                    ctor.add_sequences(list(zip(reads, counts)) if bits else reads)
+                elif b % 3 == 1:
+                    for r, c in zip(reads[:5], counts[:5]):
+                        ctor.add_sequence(r, c if bits else 1)
+                    ctor.add_sequences(list(zip(reads[5:], counts[5:])) if bits else reads[5:])
+                else:
+                    off = np.zeros(len(reads) + 1, dtype=np.uint64)
+                    off[1:] = np.cumsum([len(r) for r in reads])
+                    ctor.add_packed(b"".join(reads), off,
+                                    np.array(counts, dtype=np.uint64) if bits else None)
+
+        th = [threading.Thread(target=worker, args=(j,)) for j in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        got = ctor.build_chunk()
+        seqs = [r for reads, _ in batches for r in reads]
+        cnts = [c for _, counts in batches for c in counts] if bits else None
+        want = O.build_chunk(20, seqs, canonical=canonical, bits_per_count=bits, counts=cnts)
+        assert_same(got, want, "concurrent adds canonical=%s bits=%d" % (canonical, bits))
