@@ -36,9 +36,15 @@ CONFIGS = {
     "cfg2": {"k": 31, "reads": 10_000_000},
     "cfg3": {"k": 63, "reads": 100_000_000, "host_steps": 0, "cpu_sample_reads": 500_000,
              "steps": 2, "warmup": 1},
-    # configs[4]'s counting path (--count-kmers: SortedMultiset<uint8_t> saturating merge, 8-bit
-    # weights) on the cfg2 reads; the KMC1 input of that config is parity-tested (tests/test_kmc.py)
-    "cfg5": {"k": 31, "reads": 10_000_000, "count_width": 8, "fasta_reads": 0},
+    # configs[3]: k=31, 1 B reads over 8 GPUs = 125 M reads per GPU on one shared genome (10x over
+    # all ranks' reads); one share does not fit one pass, so every rank collects in key batches
+    "cfg4": {"k": 31, "reads": 125_000_000, "host_steps": 0, "fasta_reads": 0,
+             "cpu_sample_reads": 500_000, "steps": 2, "warmup": 1},
+    # configs[4]: --count-kmers (SortedMultiset<uint8_t> saturating merge, 8-bit weights) on a KMC1
+    # database of the canonical k=31 counts of every rank's reads (written by the builder's own GPU
+    # counter, untimed), decoded into HBM before the timed region; across ranks the records of one
+    # k-mer meet at its owner and their counts add (the count-aggregating merge)
+    "cfg5": {"k": 31, "reads": 10_000_000, "count_width": 8, "fasta_reads": 0, "kmc": True},
 }
 
 
@@ -62,6 +68,8 @@ def parse():
                     help="steps of the host-buffer leg (0 = skip)")
     ap.add_argument("--fasta-reads", type=int, default=2_000_000,
                     help="reads of the FASTA-file leg (0 = skip)")
+    ap.add_argument("--kmc", action="store_true",
+                    help="build from a KMC1 database of the reads' canonical k-mer counts (configs[4])")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
     if args.config:
@@ -174,6 +182,64 @@ def cpu_baseline(args, kb, boss):
               "what": "GPU build (host C ABI) of the cpu_baseline sample vs the oracle: W, last, F, "
                       "weights bit for bit"}
     return base, parity
+
+
+def cpu_baseline_kmc(args, kb, boss, kmc_base, n_records):
+    """configs[4]'s CPU baseline: the oracle on a bounded sample of the KMC database's records (the
+    first `cpu_sample_reads`, each one k-mer with its count, as the reference's KMC branch feeds
+    them, cli/parse_sequences.hpp:50-101); the same sample through the GPU's host C ABI is the
+    parity check."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import kmc_oracle
+    import oracle_ctypes
+    canonical = args.mode == "canonical"
+    recs = kmc_oracle.read_kmers(kmc_base, not canonical)[:args.cpu_sample_reads]
+    seqs = [r for r, _ in recs]
+    counts = [c for _, c in recs]
+    t0 = time.perf_counter()
+    c = oracle_ctypes.build_chunk(kb, seqs, canonical=canonical, bits_per_count=args.count_width,
+                                  counts=counts)
+    dt = time.perf_counter() - t0
+    base = {"value": len(seqs) / dt, "unit": "k-mers/s", "cores": cpu_threads(), "kind": "port",
+            "sample": "the first %d of %d KMC records (k=%d counts of %d reads), %s, %.1f s, %d rows"
+                      % (len(seqs), n_records, args.k, args.reads, args.mode, dt, len(c.W))}
+    ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=canonical,
+                                                 bits_per_count=args.count_width,
+                                                 num_threads=cpu_threads())
+    ctor.add_sequences(seqs, counts)
+    g = ctor.build_chunk()
+    same = (len(g.W) == len(c.W) and np.array_equal(g.W, c.W) and np.array_equal(g.last, c.last)
+            and np.array_equal(g.F, c.F) and np.array_equal(g.weights, c.weights))
+    parity = {"ok": bool(same), "rows": int(len(c.W)),
+              "what": "GPU build (host C ABI) of the cpu_baseline record sample vs the oracle: W, last, "
+                      "F, weights bit for bit"}
+    return base, parity
+
+
+def kmc_path(args, kb, boss, kmc_base, steps, n_records):
+    """configs[4] from the database file: add_kmc (both files read into host memory) + build_chunk
+    (records decoded on the device, the device path, host arrays out) -- the PCIe-inclusive rate."""
+    canonical = args.mode == "canonical"
+    ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=canonical,
+                                                 bits_per_count=args.count_width,
+                                                 num_threads=cpu_threads())
+    rows = []
+    for it in range(steps + 1):  # the first build sizes the buffers (untimed)
+        t0 = time.perf_counter()
+        ctor.add_kmc(kmc_base)
+        t1 = time.perf_counter()
+        ch = ctor.build_chunk()
+        dt = time.perf_counter() - t0
+        t = ctor.timings()
+        if it:
+            rows.append((dt, t1 - t0, t.input_ms, t.total_ms, t.d2h_ms))
+        del ch
+    m = [sum(r[i] for r in rows) / len(rows) for i in range(5)]
+    return {"value": n_records / m[0], "unit": "k-mers/s", "ms_per_step": m[0] * 1e3,
+            "stages_ms": {"read_files": m[1] * 1e3, "h2d_and_decode_on_device": m[2],
+                          "device_path": m[3], "d2h_W_last_weights": m[4]},
+            "steps": steps, "what": "add_kmc + build_chunk through the C ABI, host arrays out"}
 
 
 def host_path(args, kb, boss, seq, steps):
@@ -332,16 +398,36 @@ def main():
     seq = make_reads_device(torch, args.reads, args.read_len, 1000 + rank, args.data,
                             args.coverage, device, world)
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # the genome and the generator's temporaries (the library allocates itself)
     ctor = boss.IBOSSChunkConstructor.initialize(kb, both_strands=args.mode == "canonical",
                                                  bits_per_count=args.count_width,
-                                                 device_id=local)
+                                                 device_id=local, num_threads=cpu_threads())
     stream = torch.cuda.current_stream(device).cuda_stream
     comm = None
     if world > 1:
         uid = share_comm_id(rank, boss.Comm.unique_id)
         comm = boss.Comm.rccl(uid, world, rank, local)
 
+    kmers_per_rank = args.reads * (args.read_len - args.k + 1)
+    kmc_dir = kmc_base = dreads = None
+    if args.kmc:
+        # configs[4]'s input: the canonical k-mer counts of this rank's reads as a KMC1 database
+        # (GPU counter, untimed), decoded into HBM; one k-mer per record
+        import tempfile
+        kmc_dir = tempfile.mkdtemp(prefix="mtg_kmc_r%d_" % rank)
+        kmc_base = os.path.join(kmc_dir, "reads")
+        t0 = time.perf_counter()
+        n_records = ctor.write_kmc(seq.data_ptr(), seq.numel(), kmc_base, args.k, canonical=True)
+        kmc_write_s = time.perf_counter() - t0
+        del seq
+        torch.cuda.empty_cache()
+        dreads = boss.DeviceReads(kmc_base, call_both_from_canonical=args.mode != "canonical",
+                                  device_id=local)
+        kmers_per_rank = dreads.n_reads
+
     def step():
+        if dreads is not None:
+            return ctor.build_device(*dreads.build_args(), stream=stream, comm=comm)
         return ctor.build_device(seq.data_ptr(), seq.numel(), stream=stream, comm=comm)
 
     for _ in range(args.warmup):
@@ -360,7 +446,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, device)
-    kmers_per_rank = args.reads * (args.read_len - args.k + 1)
     value = job_throughput(kmers_per_rank, world, args.steps, elapsed)
     last = timings[-1]
     # size-independent sanity of the result
@@ -405,10 +490,13 @@ def main():
         "dtype": "u64" if 2 * args.k <= 64 else "u128" if 2 * args.k <= 128 else "u256",
         "data": "synthetic (%s-sampled %d bp reads, %gx coverage, seeded per rank)"
                 % (args.data, args.read_len, args.coverage),
-        "config": {"workload": "metagraph build -k %d --mode %s%s, %d synthetic %d bp reads per GPU"
-                               % (args.k, args.mode,
-                                  " --count-kmers --count-width %d" % args.count_width
-                                  if args.count_width else "", args.reads, args.read_len),
+        "config": {"workload": ("metagraph build -k %d --mode %s%s, %d synthetic %d bp reads per GPU"
+                                % (args.k, args.mode,
+                                   " --count-kmers --count-width %d" % args.count_width
+                                   if args.count_width else "", args.reads, args.read_len))
+                               + (" as a KMC1 database of their canonical %d-mer counts (%d records per GPU)"
+                                  % (args.k, kmers_per_rank) if args.kmc else ""),
+                   "preset": args.config,
                    "k": args.k, "reads_per_gpu": args.reads, "read_len": args.read_len,
                    "key": "KMerBOSS<uint64_t,2>" if 2 * args.k <= 64 else
                           "KMerBOSS<uint128_t,2>" if 2 * args.k <= 128 else "KMerBOSS<uint256_t,2>",
@@ -431,12 +519,25 @@ def main():
                                            "peak_bytes")},
         "exchange_ms": last["exchange_ms"],
     }
+    if args.kmc:
+        result["kmc_input"] = {"records_per_gpu": kmers_per_rank, "write_s": kmc_write_s,
+                               "what": "GPU k-mer counter -> KMC1 files (untimed), mtg_kmc_load_device -> HBM"}
     if rank == 0 and args.host_steps > 0 and world == 1:
-        result["host_path"] = host_path(args, kb, boss, seq, args.host_steps)
+        if args.kmc:
+            result["kmc_path"] = kmc_path(args, kb, boss, kmc_base, args.host_steps, kmers_per_rank)
+        else:
+            result["host_path"] = host_path(args, kb, boss, seq, args.host_steps)
         if args.fasta_reads > 0:
             result["fasta_path"] = fasta_path(args, kb, boss, args.host_steps, args.fasta_reads)
     if rank == 0 and not args.no_cpu_baseline:
-        result["cpu_baseline"], result["parity"] = cpu_baseline(args, kb, boss)
+        if args.kmc:
+            result["cpu_baseline"], result["parity"] = cpu_baseline_kmc(args, kb, boss, kmc_base, kmers_per_rank)
+        else:
+            result["cpu_baseline"], result["parity"] = cpu_baseline(args, kb, boss)
+    if kmc_dir:
+        import shutil
+        del dreads
+        shutil.rmtree(kmc_dir, ignore_errors=True)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -178,6 +178,37 @@ int mtg_boss_ctor_add_fasta(mtg_boss_ctor *ctor, const char *path);
 int mtg_boss_ctor_add_kmc(mtg_boss_ctor *ctor, const char *kmc_path, uint64_t min_count,
                           uint64_t max_count, int call_both_from_canonical);
 
+/*
+ * A KMC1 database decoded straight into device memory, as mtg_boss_ctor_add_kmc decodes it at build
+ * time (k bases + '$' per record, its reverse complement after it with call_both_from_canonical on
+ * a canonical database), with per-read starts and counts: the input of mtg_boss_build_device[_dist]
+ * for a build whose KMC input is already resident in HBM (BASELINE config 5).  Free with
+ * mtg_device_reads_free.
+ */
+typedef struct mtg_device_reads {
+    uint8_t *seq;                /* device pointers */
+    uint64_t seq_len;
+    uint64_t *read_starts;
+    uint32_t *counts;
+    uint64_t n_reads;            /* records (x2 with reverse complements) */
+    int device_id;
+} mtg_device_reads;
+int mtg_kmc_load_device(const char *kmc_path, uint64_t min_count, uint64_t max_count,
+                        int call_both_from_canonical, int device_id, mtg_device_reads *out);
+void mtg_device_reads_free(mtg_device_reads *reads);
+
+/*
+ * The builder's own k-mer counter: counts the k-mers (k <= 32; canonical = KMC's canonical form,
+ * the lexicographically smaller strand) of device-resident reads on the constructor's device and
+ * writes them as a KMC1 database <outbase>.kmc_pre / .kmc_suf (record order, prefix table and
+ * header as KMC writes them; counts saturate at the counter_size-byte maximum).  Input generator
+ * for BASELINE config 5 (the reference takes its KMC databases from KMC itself).  *n_written (may
+ * be NULL) = records written.
+ */
+int mtg_kmc_write_device(mtg_boss_ctor *ctor, const uint8_t *d_seq, uint64_t seq_len, unsigned k,
+                         int canonical, unsigned counter_size, unsigned lut_len, const char *outbase,
+                         uint64_t *n_written);
+
 /* builds from everything added so far, returns host arrays; clears the added input */
 int mtg_boss_ctor_build_chunk(mtg_boss_ctor *ctor, mtg_boss_chunk *out);
 void mtg_boss_chunk_free(mtg_boss_chunk *chunk);
@@ -250,6 +281,11 @@ typedef struct mtg_dbg_file {
 } mtg_dbg_file;
 int mtg_boss_read_dbg(const char *outbase, mtg_dbg_file *out);
 void mtg_dbg_file_free(mtg_dbg_file *file);
+
+/* the library's pool of pinned host blocks (chunk arrays, staged FASTA files): bytes held by spare
+   blocks (at most 4 GiB; blocks above that are unpinned when freed), and a trim that unpins them all */
+uint64_t mtg_host_pool_bytes(void);
+void mtg_host_pool_trim(void);
 
 /* encode table of the extractor (kmer/alphabets.hpp:127-143) evaluated by the device function on
    the host: out[c] in {0, 1, 2, 3, 4 = invalid} for every byte c (256 entries) */

@@ -148,6 +148,23 @@ def build_chunk(k, seqs, canonical=False, bits_per_count=0, counts=None):
     return Chunk(out)
 
 
+def build_chunk_packed(k, data, offsets, canonical=False, bits_per_count=0, counts=None):
+    """build_chunk on one packed buffer (uint8 array or bytes; sequence i = data[off[i]:off[i+1]]),
+    for inputs too big for a list of Python strings (the bench-size parity checks)."""
+    buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray))
+                               else data, dtype=np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    cnt = None if counts is None else np.ascontiguousarray(counts, dtype=np.uint64)
+    out = OracleChunk()
+    rc = lib().oracle_build_chunk(k, int(canonical), int(bits_per_count), buf.ctypes.data_as(ctypes.c_char_p),
+                                  off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                  cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)) if cnt is not None else None,
+                                  len(off) - 1, ctypes.byref(out))
+    if rc != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    return Chunk(out)
+
+
 def build_suffix_chunk(k, seqs, suffix, both_strands=False, bits_per_count=0, counts=None):
     """The suffix-filtered route (boss_chunk_construct.cpp:946-1013) for one filter suffix."""
     data, offsets = pack_sequences(seqs)

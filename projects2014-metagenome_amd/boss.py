@@ -46,6 +46,11 @@ class _DeviceChunk(ctypes.Structure):
                 ("n_dummy", ctypes.c_uint64)]
 
 
+class _DeviceReads(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_void_p), ("seq_len", ctypes.c_uint64), ("read_starts", ctypes.c_void_p),
+                ("counts", ctypes.c_void_p), ("n_reads", ctypes.c_uint64), ("device_id", ctypes.c_int)]
+
+
 class _DbgFile(ctypes.Structure):
     _fields_ = [(name, ctypes.c_uint64) for name in ("k", "n")] + \
                [("F", ctypes.c_uint64 * 5)] + \
@@ -84,7 +89,9 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
            "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
            "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free",
-           "mtg_boss_ctor_add_fasta", "mtg_device_copy")
+           "mtg_boss_ctor_add_fasta", "mtg_device_copy", "mtg_kmc_load_device",
+           "mtg_device_reads_free", "mtg_kmc_write_device", "mtg_host_pool_bytes",
+           "mtg_host_pool_trim")
 
 COMM_ID_BYTES = 128
 
@@ -151,6 +158,13 @@ def lib():
         L.mtg_boss_write_dbg.argtypes = [P(_Chunk), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int64, P(ctypes.c_uint64)]
         L.mtg_boss_read_dbg.argtypes = [ctypes.c_char_p, P(_DbgFile)]
+        L.mtg_kmc_load_device.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_int, P(_DeviceReads)]
+        L.mtg_device_reads_free.argtypes = [P(_DeviceReads)]
+        L.mtg_host_pool_bytes.restype = ctypes.c_uint64
+        L.mtg_kmc_write_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint,
+                                           ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_char_p,
+                                           P(ctypes.c_uint64)]
         L.mtg_dbg_file_free.argtypes = [P(_DbgFile)]
         for name in EXPORTS:
             getattr(L, name)
@@ -355,6 +369,18 @@ class BOSSChunkConstructor:
         _check(lib().mtg_boss_ctor_add_kmc(self._h, os.fsencode(kmc_path), min_count, max_count,
                                            int(bool(call_both_from_canonical))))
 
+    def write_kmc(self, d_seq, seq_len, outbase, k, canonical=True, counter_size=1, lut_len=None):
+        """Count the k-mers of device-resident reads on the GPU and write them as a KMC1 database
+        (<outbase>.kmc_pre / .kmc_suf), the input BASELINE config 5 feeds `metagraph build`.
+        Returns the records written."""
+        if lut_len is None:
+            # KMC's prefix length: at most 11 bases, leaving at least one suffix byte
+            lut_len = next((L for L in range(min(k, 11), -1, -1) if (k - L) % 4 == 0 and k - L >= 4), k)
+        n = ctypes.c_uint64(0)
+        _check(lib().mtg_kmc_write_device(self._h, d_seq, seq_len, k, int(bool(canonical)), counter_size,
+                                          lut_len, os.fsencode(outbase), ctypes.byref(n)))
+        return n.value
+
     def build_chunk(self, comm=None):
         """BOSS::Chunk of everything added; with `comm`, this rank's range of the global build
         (concatenate the ranks' chunks in rank order with Chunk.extend)."""
@@ -425,6 +451,33 @@ class BOSSConstructor(BOSSChunkConstructor):
         return IBOSSChunkConstructor.initialize(k, canonical, bits_per_count, filter_suffix,
                                                 num_threads, memory_preallocated,
                                                 container_type)
+
+
+class DeviceReads:
+    """A KMC1 database decoded into device memory (mtg_kmc_load_device): the read buffer, per-read
+    starts and counts that build_device takes, as add_kmc would decode them at build time."""
+
+    def __init__(self, kmc_path, min_count=1, max_count=2**32 - 1, call_both_from_canonical=False,
+                 device_id=0):
+        self._r = _DeviceReads()
+        _check(lib().mtg_kmc_load_device(os.fsencode(kmc_path), min_count, max_count,
+                                         int(bool(call_both_from_canonical)), device_id,
+                                         ctypes.byref(self._r)))
+
+    seq = property(lambda self: self._r.seq)
+    seq_len = property(lambda self: self._r.seq_len)
+    read_starts = property(lambda self: self._r.read_starts)
+    counts = property(lambda self: self._r.counts)
+    n_reads = property(lambda self: self._r.n_reads)
+
+    def build_args(self):
+        """(d_seq, seq_len, d_read_starts, d_counts, n_reads) for build_device."""
+        return self.seq, self.seq_len, self.read_starts, self.counts, self.n_reads
+
+    def __del__(self):
+        r, self._r = getattr(self, "_r", None), None
+        if r is not None and _lib is not None:
+            _lib.mtg_device_reads_free(ctypes.byref(r))
 
 
 class Comm:
@@ -546,6 +599,15 @@ def dna_encode_table():
     buf = ctypes.create_string_buffer(256)
     lib().mtg_dna_encode_table(buf)
     return np.frombuffer(buf.raw, dtype=np.uint8).copy()
+
+
+def host_pool_bytes():
+    """Bytes of spare pinned host blocks the library keeps for reuse (bounded by 4 GiB)."""
+    return lib().mtg_host_pool_bytes()
+
+
+def host_pool_trim():
+    lib().mtg_host_pool_trim()
 
 
 def device_count():

@@ -1040,8 +1040,10 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
         K2 *kb = (K2 *)c.ws.get(Workspace::KB, nj * sizeof(K2));
         uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nj * 4) : nullptr;
         uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nj * 4) : nullptr;
-        range_tile_counts_kernel<<<dim3((unsigned)ceil_div(tiles, 256)), dim3(256), 0, c.stream>>>(tbins, tiles, lo,
-                                                                                                   hi, tcnt);
+        BinSet sel{};
+        sel.add(lo, hi);
+        range_tile_counts_kernel<<<dim3((unsigned)ceil_div(tiles, 4)), dim3(256), 0, c.stream>>>(tbins, tiles, sel,
+                                                                                                 tcnt);
         HIP_CHECK(hipGetLastError());
         uint32_t ep;
         const uint64_t st = ceil_div(tiles, 4096);
@@ -1051,7 +1053,7 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
                                                                           &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
         range_write_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, cmax, lo, hi, toff, ka, ca);
+            in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, cmax, sel, toff, ka, ca);
         HIP_CHECK(hipGetLastError());
         const uint64_t N = read_u64(c, (const unsigned long long *)(toff + tiles));
         if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
@@ -1646,6 +1648,194 @@ static std::vector<uint64_t> route(Ctx &c, const Dist &d, const Key<L> *in, uint
     return soff;
 }
 
+// ------------------------------------------------- multi-GPU: the bounded-memory (batched) collect
+//
+// A rank share too big for one pass (BASELINE configs[3]: 125 M reads = 1.5e10 windows per GPU)
+// is collected in rounds.  The owner ranges are intervals of the range kernels' top-char bins
+// (RB_CHARS node chars, range_extract.hpp), balanced on the global bin histogram; every owner range
+// is cut into `rounds` consecutive batches balanced on the same histogram.  Round r: every rank
+// extracts the k-mers of the r-th batch of every owner from its own reads (both strands in canonical
+// mode: exactly the real-edge set, see collect_ranges), sorts and dedupes them, and sends each owner
+// its slice; the owner merges the P sorted runs (saturating count addition, sorted_multiset.cpp:54-84)
+// and appends them to its real edges.  The batches of one owner are consecutive in BOSS order, so
+// the appended array is sorted, and no rc stage or second exchange is needed.  The reference bounds
+// a multi-machine build by suffix instead (cli/build.cpp:106-148); this build keeps one exchange per
+// round and one BOSS table.
+
+// rounds of the batched collect: 1 (the single-pass dist path) when every rank's single-pass
+// footprint fits its budget; else the most any rank needs (all ranks agree through an all-gather)
+template <int L2, bool COUNTED>
+static uint32_t plan_rounds_dist(Ctx &c, Dist &d, unsigned K, bool canonical, const BuildInput &in) {
+    uint64_t want = 1;
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    // bins of RB_CHARS node chars keep every emission group on one rank only for k - 1 >= RB_CHARS
+    const bool can = K >= RB_CHARS + 2;
+    if (can && c.force_ranges) {
+        want = c.force_ranges;
+    } else if (can) {
+        const double per_key = (double)sizeof(Key<L2>) + (COUNTED ? 4.0 : 0.0);
+        double budget = c.mem_budget;
+        if (budget <= 0) {
+            size_t fr = 0, tot = 0;
+            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            budget = 0.9 * ((double)fr + (double)c.ws.held());
+        }
+        // single pass: KA + KB over every window, the exchange buffers and the owned real edges
+        if ((double)npos * per_key * 3.0 > budget || c.disk) {
+            const double keys = (double)npos * (canonical ? 2.0 : 1.0);
+            // a round holds its extracted keys twice (sort ping-pong), the received runs twice
+            want = (uint64_t)std::ceil(keys * per_key * 4.0 / (0.4 * budget));
+            want = std::max<uint64_t>(want, (uint64_t)std::ceil(keys / 2.0e9));
+            want = std::max<uint64_t>(want, 2);
+        }
+    }
+    uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, (1 + (uint64_t)d.P) * 8);
+    HIP_CHECK(hipMemcpyAsync(dv, &want, 8, hipMemcpyHostToDevice, c.stream));
+    const int e0 = d.tm->mark();
+    d.comm.allgather_u64(dv, dv + 1, 1, c.stream);
+    d.xev.push_back({e0, d.tm->mark()});
+    std::vector<uint64_t> all(d.P);
+    HIP_CHECK(hipMemcpyAsync(all.data(), dv + 1, (uint64_t)d.P * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // `want` is a host local
+    uint64_t r = 1;
+    for (uint64_t v : all) r = std::max(r, v);
+    return (uint32_t)std::min<uint64_t>(r, RB_BINS);
+}
+
+template <int L2, bool COUNTED>
+static uint64_t collect_ranges_dist(Ctx &c, Dist &d, unsigned K, bool canonical, uint32_t cmax,
+                                    const BuildInput &in, uint32_t rounds, Key<L2> **real, uint32_t **realc,
+                                    std::vector<uint64_t> *owner_bounds, Tracer &tr) {
+    using K2 = Key<L2>;
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    c.timings.n_positions = npos;
+    c.timings.n_batches = rounds;
+    const int both = canonical ? 1 : 0;
+    constexpr int TILE = RangeTraits<L2>::TILE;
+    const uint64_t tiles = ceil_div(npos, TILE);
+    // count pass over this rank's reads, then the global bin histogram
+    auto *dh = (unsigned long long *)c.ws.get(Workspace::XHIST, RB_BINS * 8);
+    HIP_CHECK(hipMemsetAsync(dh, 0, RB_BINS * 8, c.stream));
+    uint16_t *tbins = (uint16_t *)c.ws.get(Workspace::RANGE_BINS, std::max<uint64_t>(tiles, 1) * RB_BINS * 2);
+    if (tiles) {
+        range_count_kernel<L2><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, both, tbins);
+        HIP_CHECK(hipGetLastError());
+        range_bins_reduce_kernel<<<dim3((unsigned)std::min<uint64_t>(tiles, 2048)), dim3(RB_BINS), 0, c.stream>>>(
+            tbins, tiles, dh);
+        HIP_CHECK(hipGetLastError());
+    }
+    std::vector<uint64_t> local(RB_BINS), glob(RB_BINS);
+    HIP_CHECK(hipMemcpyAsync(local.data(), dh, RB_BINS * 8, hipMemcpyDeviceToHost, c.stream));
+    const int e0 = d.tm->mark();
+    d.comm.allreduce_sum_u64((uint64_t *)dh, RB_BINS, c.stream);
+    d.xev.push_back({e0, d.tm->mark()});
+    HIP_CHECK(hipMemcpyAsync(glob.data(), dh, RB_BINS * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    tr("range count", tiles);
+    // owner intervals, then each cut into `rounds` batches
+    const std::vector<uint64_t> ob = balanced_bounds(glob.data(), RB_BINS, d.P);
+    std::vector<std::vector<uint64_t>> bb(d.P);
+    for (int o = 0; o < d.P; ++o) {
+        bb[o] = balanced_bounds(glob.data() + ob[o], ob[o + 1] - ob[o], (int)rounds);
+        for (auto &v : bb[o]) v += ob[o];
+    }
+    *owner_bounds = ob;
+    uint64_t own_total = 0;
+    for (uint64_t b = ob[d.me]; b < ob[d.me + 1]; ++b) own_total += glob[b];
+    uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
+    uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
+    uint64_t off = 0, cap = 0, extracted = 0;
+    *real = nullptr;
+    *realc = nullptr;
+    for (uint32_t r = 0; r < rounds; ++r) {
+        BinSet sel{};
+        for (int o = 0; o < d.P; ++o) sel.add((uint32_t)bb[o][r], (uint32_t)bb[o][r + 1]);
+        uint64_t nj = 0;
+        for (uint32_t b = 0; b < RB_BINS; ++b)
+            if (sel.has(b)) nj += local[b];
+        K2 *ka = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(nj, 1) * sizeof(K2));
+        K2 *kb = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nj, 1) * sizeof(K2));
+        uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(nj, 1) * 4) : nullptr;
+        uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nj, 1) * 4) : nullptr;
+        uint64_t Ul = 0;
+        if (nj) {
+            range_tile_counts_kernel<<<dim3((unsigned)ceil_div(tiles, 4)), dim3(256), 0, c.stream>>>(tbins, tiles, sel,
+                                                                                                     tcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t st = ceil_div(tiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, tiles, toff, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            range_write_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+                in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, cmax, sel, toff, ka, ca);
+            HIP_CHECK(hipGetLastError());
+            const uint64_t N = read_u64(c, (const unsigned long long *)(toff + tiles));
+            if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
+            const double spread = (double)RB_BINS / (double)std::max<uint32_t>(1, sel.size());
+            const double dup = estimate_dup<L2>(c, ka, N, 8.0) / spread;
+            c.track_partition = r == 0;  // the roofline's partition pass: the first round's first level
+            Ul = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, N, 2 * K, cmax, dup);
+            c.track_partition = false;
+        }
+        extracted += nj;
+        tr("round collect", nj, Ul);
+        // every owner's slice of the sorted local keys: the bin index of the keys at the owner bounds
+        std::vector<std::vector<uint64_t>> soff(1, std::vector<uint64_t>(d.P + 1, 0));
+        if (Ul) {
+            uint64_t *st = prefix_index<L2>(c, d, Workspace::XSTART_A, ka, Ul);
+            std::vector<uint64_t> starts(RB_BINS + 1);
+            HIP_CHECK(hipMemcpyAsync(starts.data(), st, (RB_BINS + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            for (int j = 0; j <= d.P; ++j) soff[0][j] = starts[ob[j]];
+        }
+        K2 *xa = ka;
+        uint32_t *xac = ca;
+        uint64_t U = Ul;
+        if (d.P > 1) {
+            const K2 *arrs[1] = {ka};
+            const uint32_t *cnts[1] = {ca};
+            std::vector<uint64_t> runs;
+            const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA,
+                                                  Workspace::XAC, &xa, &xac, &runs);
+            U = n1;
+            if (n1) {
+                K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
+                uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
+                // the keys fill this owner's batch of the bins: plan as if spread over all of them
+                const double spread = (double)RB_BINS / (double)std::max<uint64_t>(1, bb[d.me][r + 1] - bb[d.me][r]);
+                const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / spread;
+                U = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr, false,
+                                                 &runs);
+            }
+            tr("round exchange + merge", n1, U);
+        }
+        if (off + U > cap) {
+            // first filled round: size the owned real edges from its share of the owner's range
+            uint64_t gr = 0;
+            for (uint64_t b = bb[d.me][r]; b < bb[d.me][r + 1]; ++b) gr += glob[b];
+            const uint64_t want = off == 0 && gr ? (uint64_t)((double)U / (double)gr * (double)own_total * 1.25) + U
+                                                 : (off + U) + (off + U) / 4;
+            cap = std::max(want, off + U);
+            *real = (K2 *)c.ws.get(Workspace::REAL, cap * sizeof(K2), off * sizeof(K2), c.stream);
+            if (COUNTED) *realc = (uint32_t *)c.ws.get(Workspace::REALC, cap * 4, off * 4, c.stream);
+        }
+        if (U) {
+            HIP_CHECK(hipMemcpyAsync(*real + off, xa, U * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+            if (COUNTED) HIP_CHECK(hipMemcpyAsync(*realc + off, xac, U * 4, hipMemcpyDeviceToDevice, c.stream));
+        }
+        off += U;
+    }
+    if (!*real) {
+        *real = (K2 *)c.ws.get(Workspace::REAL, sizeof(K2));
+        if (COUNTED) *realc = (uint32_t *)c.ws.get(Workspace::REALC, 4);
+    }
+    c.timings.n_extracted = extracted / (canonical ? 2 : 1);  // valid windows (one k-mer per strand each)
+    return off;
+}
+
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, unsigned bits,
                               const BuildInput &in, BuildOutput *out) {
@@ -1663,114 +1853,132 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     Dist d{comm, comm.size(), comm.rank(), 0, 0, 1, &tm, {}};
     if (d.P > MAX_RANKS) throw std::runtime_error("more ranks than the routing kernels support");
     T.world = (uint64_t)d.P;
+    T.n_batches = 1;
     // ranges on the top m node chars, m <= k - 1 keeps every emission group inside one rank
     d.m = std::min(8u, k >= 2 ? k - 1 : 0u);
     d.shift2 = 2 * K - 2 * d.m;
     d.nb = 1ull << (2 * d.m);
 
-    // ---- K1-K3 on this rank's reads
-    K2 *ka, *kb;
-    uint32_t *ca, *cb;
     Tracer tr{c, d.me};
-    uint64_t N = 0;
-    double dup = 0;
-    const uint32_t *hist1 = nullptr;
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
-    if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
-        N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
-    const int ev_extract = tm.mark();
-    tr("extract", N);
-    const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
-    const int ev_sort = tm.mark();
-    tr("local collect", Ul);
+    int ev_extract, ev_sort, ev_unique;
+    K2 *E = nullptr;
+    uint32_t *Ec = nullptr;
+    uint64_t R = 0;
+    std::vector<uint64_t> bounds;
+    const uint32_t rounds = plan_rounds_dist<L2, COUNTED>(c, d, K, canonical, in);
+    if (rounds > 1) {
+        // ---- K1-K4 in rounds of key batches (both strands in canonical mode): the owned real edges
+        d.m = RB_CHARS;
+        d.shift2 = 2 * K - 2 * d.m;
+        d.nb = RB_BINS;
+        ev_extract = tm.mark();
+        R = collect_ranges_dist<L2, COUNTED>(c, d, K, canonical, cmax, in, rounds, &E, &Ec, &bounds, tr);
+        ev_sort = ev_unique = tm.mark();
+        T.n_unique = R;
+    } else {
+        // ---- K1-K3 on this rank's reads
+        K2 *ka, *kb;
+        uint32_t *ca, *cb;
+        uint64_t N = 0;
+        double dup = 0;
+        const uint32_t *hist1 = nullptr;
+        if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+            N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
+        ev_extract = tm.mark();
+        tr("extract", N);
+        const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
+        ev_sort = tm.mark();
+        tr("local collect", Ul);
 
-    // ---- exchange 1: the distinct k-mers by range of their own prefix, merged at the owner
-    std::vector<std::vector<uint64_t>> soff;
-    std::vector<uint64_t> b1;
-    {
-        // canonical mode: the ranges balance both strands (the canonical keys and their rc keys)
-        // and are final, so exchange 2 moves only the rc keys
-        const K2 *arrs[1] = {ka};
-        const uint64_t ns[1] = {Ul};
-        b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff, canonical ? K : 0);
-    }
-    tr("ranges 1");
-    K2 *xa;
-    uint32_t *xac = nullptr;
-    {
-        const K2 *arrs[1] = {ka};
-        const uint32_t *cnts[1] = {ca};
-        std::vector<uint64_t> runs;
-        const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA,
-                                              Workspace::XAC, &xa, &xac, &runs);
-        tr("exchange 1", n1);
-        if (d.P == 1) {  // one rank: its own sorted distinct k-mers came back unchanged
-            T.n_unique = n1;
-        } else {
-            K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
-            uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
-            // the P runs are sorted and distinct within a run; duplicates across runs collapse and
-            // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover ~1/P of
-            // the prefix space: P times denser buckets than their count says
-            const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / d.P;
-            T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
-                                                      false, &runs);
+        // ---- exchange 1: the distinct k-mers by range of their own prefix, merged at the owner
+        std::vector<std::vector<uint64_t>> soff;
+        std::vector<uint64_t> b1;
+        {
+            // canonical mode: the ranges balance both strands (the canonical keys and their rc keys)
+            // and are final, so exchange 2 moves only the rc keys
+            const K2 *arrs[1] = {ka};
+            const uint64_t ns[1] = {Ul};
+            b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff, canonical ? K : 0);
         }
-    }
-    const uint64_t U = T.n_unique;
-    tr("owner dedupe", U);
-    debug_check_sorted(c, "owned k-mers", xa, U);
-    const int ev_unique = tm.mark();
+        tr("ranges 1");
+        K2 *xa;
+        uint32_t *xac = nullptr;
+        {
+            const K2 *arrs[1] = {ka};
+            const uint32_t *cnts[1] = {ca};
+            std::vector<uint64_t> runs;
+            const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA,
+                                                  Workspace::XAC, &xa, &xac, &runs);
+            tr("exchange 1", n1);
+            if (d.P == 1) {  // one rank: its own sorted distinct k-mers came back unchanged
+                T.n_unique = n1;
+            } else {
+                K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
+                uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
+                // the P runs are sorted and distinct within a run; duplicates across runs collapse and
+                // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover ~1/P of
+                // the prefix space: P times denser buckets than their count says
+                const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / d.P;
+                T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
+                                                          false, &runs);
+            }
+        }
+        const uint64_t U = T.n_unique;
+        tr("owner dedupe", U);
+        debug_check_sorted(c, "owned k-mers", xa, U);
+        ev_unique = tm.mark();
 
-    // ---- canonical: rc of the owned canonical set, routed to the owners of the rc keys
-    K2 *E = xa;
-    uint32_t *Ec = xac;
-    uint64_t R = U;
-    std::vector<uint64_t> bounds = b1;  // final in both modes
-    if (canonical) {
-        // rc keys of the owned canonical set, unsorted (even K: palindromes stay out with their
-        // counts doubled, boss_chunk_construct.cpp:188-200)
-        K2 *rbuf = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U, 1) * sizeof(K2));
-        uint32_t *rbufc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U, 1) * 4) : nullptr;
-        K2 *rk = rbuf;
-        uint32_t *rkc = rbufc;
-        uint64_t Urc = 0;
-        if (U) Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, xa, xac, U, rbuf, rbufc, &rk, &rkc, nullptr, false);
-        tr("rc", Urc);
-        K2 *rsend = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(Urc, 1) * sizeof(K2));
-        uint32_t *rsendc = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_SENDC, std::max<uint64_t>(Urc, 1) * 4) : nullptr;
-        std::vector<std::vector<uint64_t>> roff(1);
-        roff[0] = route<L2, 1>(c, d, rk, Urc, K, d.shift2, 2 * d.m, bounds, rsend, COUNTED ? rkc : nullptr, rsendc);
-        tr("route rc", Urc);
-        // exchange 2: the rc keys only.  Every owned canonical key has exactly one owner, so the
-        // received rc keys are distinct, and distinct from the canonical keys (a palindrome has no
-        // rc key)
-        K2 *rkeys;
-        uint32_t *rcc = nullptr;
-        const K2 *arrs[1] = {rsend};
-        const uint32_t *cnts[1] = {rsendc};
-        const uint64_t nrc = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, roff, Workspace::REAL,
-                                               Workspace::REALC, &rkeys, &rcc);
-        tr("exchange 2", nrc);
-        // the single build's rc sort, its local pass fused with the merge into the owned canonical
-        // keys (local_merge_kernel); the keys cover ~1/P of the prefix space, so the plan is told
-        // they are as dense as P * (nrc + U) / 2 rc keys of a single build
-        K2 *out = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U + nrc, 1) * sizeof(K2));
-        uint32_t *outc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U + nrc, 1) * 4) : nullptr;
-        K2 *ralt = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nrc, 1) * sizeof(K2));
-        uint32_t *rcalt = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nrc, 1) * 4) : nullptr;
-        RcMerge<L2> rm{xa, xac, U, out, outc};
-        const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + U)) : 1.0;
-        uint64_t nr = 0;
-        if (nrc)
-            nr = msd_sort_unique<L2, COUNTED>(c, &rkeys, &ralt, &rcc, &rcalt, nrc, 2 * K, cmax, dupm, nullptr, true,
-                                              nullptr, false, U ? &rm : nullptr);
-        if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, xa, xac, U, rkeys, rcc, nr, K, out, outc, 0);
-        R = U + nr;
-        E = out;
-        Ec = outc;
+        // ---- canonical: rc of the owned canonical set, routed to the owners of the rc keys
+        E = xa;
+        Ec = xac;
+        R = U;
+        bounds = b1;  // final in both modes
+        if (canonical) {
+            // rc keys of the owned canonical set, unsorted (even K: palindromes stay out with their
+            // counts doubled, boss_chunk_construct.cpp:188-200)
+            K2 *rbuf = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U, 1) * sizeof(K2));
+            uint32_t *rbufc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U, 1) * 4) : nullptr;
+            K2 *rk = rbuf;
+            uint32_t *rkc = rbufc;
+            uint64_t Urc = 0;
+            if (U) Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, xa, xac, U, rbuf, rbufc, &rk, &rkc, nullptr, false);
+            tr("rc", Urc);
+            K2 *rsend = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(Urc, 1) * sizeof(K2));
+            uint32_t *rsendc = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_SENDC, std::max<uint64_t>(Urc, 1) * 4) : nullptr;
+            std::vector<std::vector<uint64_t>> roff(1);
+            roff[0] = route<L2, 1>(c, d, rk, Urc, K, d.shift2, 2 * d.m, bounds, rsend, COUNTED ? rkc : nullptr, rsendc);
+            tr("route rc", Urc);
+            // exchange 2: the rc keys only.  Every owned canonical key has exactly one owner, so the
+            // received rc keys are distinct, and distinct from the canonical keys (a palindrome has no
+            // rc key)
+            K2 *rkeys;
+            uint32_t *rcc = nullptr;
+            const K2 *arrs[1] = {rsend};
+            const uint32_t *cnts[1] = {rsendc};
+            const uint64_t nrc = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, roff, Workspace::REAL,
+                                                   Workspace::REALC, &rkeys, &rcc);
+            tr("exchange 2", nrc);
+            // the single build's rc sort, its local pass fused with the merge into the owned canonical
+            // keys (local_merge_kernel); the keys cover ~1/P of the prefix space, so the plan is told
+            // they are as dense as P * (nrc + U) / 2 rc keys of a single build
+            K2 *out = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(U + nrc, 1) * sizeof(K2));
+            uint32_t *outc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(U + nrc, 1) * 4) : nullptr;
+            K2 *ralt = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nrc, 1) * sizeof(K2));
+            uint32_t *rcalt = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nrc, 1) * 4) : nullptr;
+            RcMerge<L2> rm{xa, xac, U, out, outc};
+            const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + U)) : 1.0;
+            uint64_t nr = 0;
+            if (nrc)
+                nr = msd_sort_unique<L2, COUNTED>(c, &rkeys, &ralt, &rcc, &rcalt, nrc, 2 * K, cmax, dupm, nullptr, true,
+                                                  nullptr, false, U ? &rm : nullptr);
+            if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, xa, xac, U, rkeys, rcc, nr, K, out, outc, 0);
+            R = U + nr;
+            E = out;
+            Ec = outc;
+        }
     }
     T.n_real = R;
     tr("owner merge", R);
@@ -2037,6 +2245,35 @@ static void run_suffix_dispatch(Ctx &c, unsigned k, bool both, unsigned bits, co
         if (bits) run_suffix<4, true>(c, k, both, bits, suf, all_sentinel, in, out);
         else run_suffix<4, false>(c, k, both, bits, suf, all_sentinel, in, out);
     }
+}
+
+// the builder's KMC1 writer (kmc.hpp): every k-mer of the reads with count 1, mapped to KMC words,
+// sorted + counted (saturating at 2^32 - 1), then written on the host; returns the records
+static uint64_t kmc_count_write(Ctx &c, const BuildInput &in, unsigned K, bool canonical, unsigned counter_size,
+                                unsigned lut_len, const std::string &base, unsigned threads) {
+    if (K < 1 || K > 32) throw std::runtime_error("KMC writer: k must be in [1, 32]");
+    HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
+    Key<1> *ka, *kb;
+    uint32_t *ca, *cb;
+    const uint64_t N = stage_extract<1, true>(c, K, false, 0xFFFFFFFFu, in, &ka, &kb, &ca, &cb);
+    uint64_t U = 0;
+    if (N) {
+        kmc_key_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(N, 256), 65536)), dim3(256), 0, c.stream>>>(
+            (uint64_t *)ka, N, K, canonical ? 1 : 0);
+        HIP_CHECK(hipGetLastError());
+        const double dup = estimate_dup<1>(c, ka, N, 8.0);
+        U = msd_sort_unique<1, true>(c, &ka, &kb, &ca, &cb, N, 2 * K, 0xFFFFFFFFu, dup);
+    }
+    check_error_word(c);
+    std::vector<uint64_t> keys(U);
+    std::vector<uint32_t> counts(U);
+    if (U) {
+        HIP_CHECK(hipMemcpyAsync(keys.data(), ka, U * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(counts.data(), ca, U * 4, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+    kmc_write_files(base, keys.data(), counts.data(), U, K, lut_len, counter_size, canonical, threads);
+    return U;
 }
 
 template <int L2, int L3>
@@ -2648,8 +2885,8 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         T.h2d_ms = h2d_ms;
         T.input_ms = input_ms;
         T.stage_ms = (double)c->stage_ns.exchange(0) * 1e-6;
+        c->stage.clear_locked();  // under the build's exclusive lock: a waiting add lands in the next batch
         stage_lock.unlock();
-        c->stage.clear();
         c->kmc.clear();
         for (auto &f : c->fasta) free_fasta(f);
         c->fasta.clear();
@@ -2660,6 +2897,81 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         mtg_boss_chunk_free(out);
         return MTG_ERR_DEVICE;
     }
+}
+
+int mtg_kmc_write_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_len, unsigned k, int canonical,
+                         unsigned counter_size, unsigned lut_len, const char *outbase, uint64_t *n_written) {
+    if (!c || !outbase || (seq_len && !d_seq)) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    try {
+        HIP_CHECK(hipSetDevice(c->device));
+        BuildInput in{d_seq, seq_len, nullptr, nullptr, 0};
+        const uint64_t n = mtg::kmc_count_write(c->ctx, in, k, canonical != 0, counter_size, lut_len, outbase,
+                                                stage_threads(c));
+        if (n_written) *n_written = n;
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_DEVICE;
+    }
+}
+
+int mtg_kmc_load_device(const char *kmc_path, uint64_t min_count, uint64_t max_count, int call_both_from_canonical,
+                        int device_id, mtg_device_reads *out) {
+    if (!kmc_path || !out) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::memset(out, 0, sizeof(*out));
+    out->device_id = device_id;
+    uint64_t *dlut = nullptr;
+    uint8_t *drec = nullptr;
+    try {
+        KmcInput m = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0);
+        HIP_CHECK(hipSetDevice(device_id));
+        const uint64_t per = m.both ? 2 : 1;
+        out->seq_len = m.total * (m.k + 1) * per;
+        out->n_reads = m.total * per;
+        HIP_CHECK(hipMalloc(&out->seq, out->seq_len + 1));
+        HIP_CHECK(hipMalloc(&out->read_starts, std::max<uint64_t>(out->n_reads, 1) * 8));
+        HIP_CHECK(hipMalloc(&out->counts, std::max<uint64_t>(out->n_reads, 1) * 4));
+        if (m.total) {
+            HIP_CHECK(hipMalloc(&dlut, m.lut.size() * 8));
+            HIP_CHECK(hipMalloc(&drec, m.records.size() + 1));
+            HIP_CHECK(hipMemcpy(dlut, m.lut.data(), m.lut.size() * 8, hipMemcpyHostToDevice));
+            HIP_CHECK(hipMemcpy(drec, m.records.data(), m.records.size(), hipMemcpyHostToDevice));
+            kmc_decode_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m.total, 256), 65536))),
+                                dim3(256)>>>(drec, dlut, m.lut.size(), m.total, m.k, m.lut_len, m.counter_size,
+                                             m.min_count, m.max_count, m.both ? 1 : 0, out->seq, 0, out->read_starts,
+                                             out->counts, 0);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipDeviceSynchronize());
+            (void)hipFree(dlut);
+            (void)hipFree(drec);
+        }
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        if (dlut) (void)hipFree(dlut);
+        if (drec) (void)hipFree(drec);
+        mtg_device_reads_free(out);
+        return MTG_ERR_DEVICE;
+    }
+}
+
+void mtg_device_reads_free(mtg_device_reads *r) {
+    if (!r) return;
+    (void)hipSetDevice(r->device_id);
+    if (r->seq) (void)hipFree(r->seq);
+    if (r->read_starts) (void)hipFree(r->read_starts);
+    if (r->counts) (void)hipFree(r->counts);
+    r->seq = nullptr;
+    r->read_starts = nullptr;
+    r->counts = nullptr;
+    r->seq_len = r->n_reads = 0;
 }
 
 int mtg_boss_build_device(mtg_boss_ctor *c, const uint8_t *d_seq, uint64_t seq_len,
@@ -2825,6 +3137,10 @@ void mtg_dbg_file_free(mtg_dbg_file *f) {
     f->ranges = nullptr;
     f->valid = nullptr;
 }
+
+uint64_t mtg_host_pool_bytes(void) { return PinnedPool::get().spare_bytes(); }
+
+void mtg_host_pool_trim(void) { PinnedPool::get().trim(); }
 
 void mtg_dna_encode_table(uint8_t *out) {
     for (uint32_t c = 0; c < 256; ++c) out[c] = (uint8_t)encode_dna(c);

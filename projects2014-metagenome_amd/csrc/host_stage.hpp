@@ -44,6 +44,9 @@ struct DeviceGuard {
 
 // Pinned host blocks, recycled: a returned block is kept for the next request of at most its size
 // (a steady stream of builds allocates no pinned memory; pinning is the slow part of a hipHostMalloc).
+// The spare blocks are bounded -- at most kKeep blocks and kKeepBytes in total; a returned block
+// bigger than that is unpinned at once -- so one large build (tens of GB of W and weights) does not
+// hold unswappable host memory after its chunk is freed; trim() drops every spare block.
 class PinnedPool {
   public:
     static PinnedPool &get() {
@@ -57,13 +60,17 @@ class PinnedPool {
             auto it = free_.lower_bound(bytes);
             if (it != free_.end() && it->first <= 2 * bytes + (64u << 20)) {
                 void *p = it->second;
+                spare_ -= it->first;
                 free_.erase(it);
                 return p;
             }
         }
         void *p = nullptr;
-        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess || !p)
-            throw std::runtime_error("pinned host allocation of " + std::to_string(bytes) + " bytes failed");
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess || !p) {
+            trim();  // spare blocks may be what exhausted the pinnable memory: retry once without them
+            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess || !p)
+                throw std::runtime_error("pinned host allocation of " + std::to_string(bytes) + " bytes failed");
+        }
         std::lock_guard<std::mutex> lk(mu_);
         size_[p] = bytes;
         return p;
@@ -74,21 +81,45 @@ class PinnedPool {
         std::lock_guard<std::mutex> lk(mu_);
         auto it = size_.find(p);
         if (it == size_.end()) return false;
-        free_.emplace(it->second, p);
-        while (free_.size() > kKeep) {  // drop the smallest spare block
+        const size_t bytes = it->second;
+        if (bytes > kKeepBytes) {  // never kept
+            size_.erase(it);
+            (void)hipHostFree(p);
+            return true;
+        }
+        free_.emplace(bytes, p);
+        spare_ += bytes;
+        while (free_.size() > kKeep || spare_ > kKeepBytes) {  // drop the smallest spare block
             auto f = free_.begin();
+            spare_ -= f->first;
             size_.erase(f->second);
             (void)hipHostFree(f->second);
             free_.erase(f);
         }
         return true;
     }
+    // unpin every spare block
+    void trim() {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto &f : free_) {
+            size_.erase(f.second);
+            (void)hipHostFree(f.second);
+        }
+        free_.clear();
+        spare_ = 0;
+    }
+    size_t spare_bytes() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return spare_;
+    }
 
   private:
     static constexpr size_t kKeep = 16;
+    static constexpr size_t kKeepBytes = size_t(4) << 30;
     std::mutex mu_;
     std::multimap<size_t, void *> free_;
     std::unordered_map<void *, size_t> size_;
+    size_t spare_ = 0;
 };
 
 // copy `n` items with `threads` host threads (ranges of items; `fn(i0, i1)`)
@@ -335,6 +366,11 @@ class HostStage {
     // the build consumed the staged reads (the pinned buffers are kept for the next batch)
     void clear() {
         std::unique_lock<std::shared_mutex> ex(grow_);
+        clear_locked();
+    }
+    // the same with grow_ already held exclusively by the caller (the build): no add can slip in
+    // between the end of the build and the clear
+    void clear_locked() {
         if (stream_) {
             DeviceGuard g(device_);
             (void)hipStreamSynchronize(stream_);

@@ -20,10 +20,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace mtg {
@@ -168,6 +171,96 @@ __global__ void kmc_decode_kernel(const uint8_t *__restrict__ rec, const uint64_
             }
         }
     }
+}
+
+// ------------------------------------------------------------------------ KMC1 writer
+//
+// The builder's own k-mer counter output, for the KMC input of BASELINE config 5 (`metagraph
+// build` on a KMC database of k = 31 counts): the counted k-mers of device reads, sorted in KMC's
+// record order and written in the layout above, so the reference's KMC branch (and kmc_open here)
+// reads them back.  KMC's order is lexicographic with the first base most significant, and its
+// canonical form is the lexicographically smaller of a k-mer and its reverse complement
+// (tests/test_kmc.py pins both on the reference's fixtures).
+
+// 2-bit chars of a 64-bit word in reverse order (char i <-> char 31 - i)
+__device__ __forceinline__ uint64_t rev_chars64(uint64_t x) {
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    return __builtin_bswap64(x);
+}
+
+// in place: the 2-bit BOSS key of a K-mer a_1..a_K (kmer_boss.hpp:58-72: a_K in the low two bits,
+// a_i at bit 2i) -> its KMC word sum a_i << 2 (K - i); canonical: min(word, word of the rc).  With
+// p = sum a_i << 2 (i - 1) (the plain co-lex word), word = rev_K(p) and the rc's word = ~p.
+__global__ void kmc_key_kernel(uint64_t *__restrict__ keys, uint64_t n, unsigned K, int canonical) {
+    const uint64_t mask = K >= 32 ? ~0ull : (1ull << (2 * K)) - 1;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const uint64_t b = keys[i];
+        const uint64_t plain = (b >> 2) | ((b & 3ull) << (2 * (K - 1)));
+        const uint64_t w = rev_chars64(plain) >> (64 - 2 * K);
+        const uint64_t rc = ~plain & mask;
+        keys[i] = canonical && rc < w ? rc : w;
+    }
+}
+
+// the files: `<base>.kmc_pre` (prefix table + the 64-byte header) and `<base>.kmc_suf` (records)
+// from keys[0..n) sorted in KMC order with their counts (saturated at the counter's maximum)
+static void kmc_write_files(const std::string &base, const uint64_t *keys, const uint32_t *counts, uint64_t n,
+                            unsigned k, unsigned lut_len, unsigned counter_size, bool canonical, unsigned threads) {
+    if (k == 0 || k > 32 || lut_len > k || (k - lut_len) % 4 || counter_size < 1 || counter_size > 4 || lut_len > 16)
+        throw std::runtime_error("KMC writer: unsupported layout");
+    const unsigned slen = (k - lut_len) / 4, rsize = slen + counter_size;
+    const uint64_t nlut = 1ull << (2 * lut_len);
+    const unsigned sbits = 2 * (k - lut_len);
+    const uint64_t cmax = counter_size >= 4 ? 0xFFFFFFFFull : (1ull << (8 * counter_size)) - 1;
+    threads = std::max(1u, threads);
+    std::vector<uint8_t> rec(4 + n * rsize + 4);
+    memcpy(rec.data(), "KMCS", 4);
+    memcpy(rec.data() + rec.size() - 4, "KMCS", 4);
+    std::vector<uint64_t> lut(nlut + 1, 0);
+    // records in parallel; the prefix table from the (sorted) prefixes: lut[p] = first record of
+    // prefix p = the number of records with a smaller prefix
+    std::vector<std::thread> pool;
+    const uint64_t per = (n + threads - 1) / threads;
+    for (unsigned t = 0; t < threads; ++t)
+        pool.emplace_back([&, t] {
+            const uint64_t r0 = std::min(n, t * per), r1 = std::min(n, r0 + per);
+            for (uint64_t r = r0; r < r1; ++r) {
+                uint8_t *o = rec.data() + 4 + r * rsize;
+                const uint64_t suf = sbits >= 64 ? keys[r] : keys[r] & ((1ull << sbits) - 1);
+                for (unsigned i = 0; i < slen; ++i) o[i] = (uint8_t)(suf >> (sbits - 8 * (i + 1)));
+                const uint64_t c = std::min<uint64_t>(counts ? counts[r] : 1, cmax);
+                for (unsigned b = 0; b < counter_size; ++b) o[slen + b] = (uint8_t)(c >> (8 * b));
+                // prefix boundaries: record r starts every prefix in (prefix(r - 1), prefix(r)]
+                const uint64_t pr = sbits >= 64 ? 0 : keys[r] >> sbits;
+                const uint64_t pp = r ? (sbits >= 64 ? 0 : keys[r - 1] >> sbits) + 1 : 0;
+                for (uint64_t q = pp; q <= pr && q < nlut; ++q) lut[q] = r;
+            }
+        });
+    for (auto &th : pool) th.join();
+    const uint64_t plast = n ? (sbits >= 64 ? 0 : keys[n - 1] >> sbits) + 1 : 0;
+    for (uint64_t q = plast; q < nlut; ++q) lut[q] = n;  // prefixes past the last record
+    // header (the fixtures' 64-byte layout): k, mode 0, counter size, prefix length, min count 1,
+    // max count 10^9 (KMC's default cut-offs for a -ci1 run), total, flags (bit 0: single strand),
+    // padding, version 0
+    uint8_t h[64] = {0};
+    const uint32_t f[6] = {k, 0, counter_size, lut_len, 1, 1000000000u};
+    memcpy(h, f, 24);
+    memcpy(h + 24, &n, 8);
+    const uint32_t flags = canonical ? 0u : 1u;
+    memcpy(h + 32, &flags, 4);
+    auto put = [&](const std::string &path, const std::vector<const void *> &parts, const std::vector<size_t> &sizes) {
+        FILE *fp = fopen(path.c_str(), "wb");
+        if (!fp) throw std::runtime_error("KMC writer: cannot create " + path);
+        bool ok = true;
+        for (size_t i = 0; i < parts.size(); ++i) ok = ok && fwrite(parts[i], 1, sizes[i], fp) == sizes[i];
+        ok = (fclose(fp) == 0) && ok;
+        if (!ok) throw std::runtime_error("KMC writer: short write to " + path);
+    };
+    const uint32_t hsize = 64;
+    put(base + ".kmc_pre", {"KMCP", lut.data(), h, &hsize, "KMCP"}, {4, nlut * 8, 64, 4, 4});
+    put(base + ".kmc_suf", {rec.data()}, {rec.size()});
 }
 
 }  // namespace mtg

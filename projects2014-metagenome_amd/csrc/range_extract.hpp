@@ -22,6 +22,21 @@ namespace mtg {
 constexpr unsigned RB_CHARS = 4;                 // top node chars that pick a window's bin
 constexpr uint32_t RB_BINS = 1u << (2 * RB_CHARS);  // 256
 
+// the bins one range (or one round of the multi-GPU batched build: one bin interval per owner
+// rank) collects, as a 256-bit set passed by value
+struct BinSet {
+    uint32_t m[RB_BINS / 32];
+    __host__ __device__ bool has(uint32_t b) const { return (m[b >> 5] >> (b & 31)) & 1u; }
+    __host__ void add(uint32_t lo, uint32_t hi) {
+        for (uint32_t b = lo; b < hi; ++b) m[b >> 5] |= 1u << (b & 31);
+    }
+    __host__ uint32_t size() const {
+        uint32_t s = 0;
+        for (uint32_t w : m) s += (uint32_t)__builtin_popcount(w);
+        return s;
+    }
+};
+
 template <int L>
 struct RangeTraits {
     static constexpr int BLOCK = 256;
@@ -121,24 +136,33 @@ __global__ __launch_bounds__(256) void range_bins_reduce_kernel(const uint16_t *
     if (s) atomicAdd(&hist[threadIdx.x], s);
 }
 
-// one range's k-mers per tile: the tile's counts over bins [blo, bhi)
+// one range's k-mers per tile: the tile's counts over the bins of `sel`; one wave per tile
+// (each lane sums 4 bins of the tile's 512-byte row, then a wave reduction)
 __global__ __launch_bounds__(256) void range_tile_counts_kernel(const uint16_t *__restrict__ tbins, uint64_t tiles,
-                                                                uint32_t blo, uint32_t bhi,
-                                                                uint32_t *__restrict__ tcnt) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                                BinSet sel, uint32_t *__restrict__ tcnt) {
+    static_assert(RB_BINS == 256, "4 bins per lane");
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
     if (t >= tiles) return;
-    const uint16_t *row = tbins + t * RB_BINS;
-    uint32_t s = 0;
-    for (uint32_t b = blo; b < bhi; ++b) s += row[b];
-    tcnt[t] = s;
+    const uint2 v = reinterpret_cast<const uint2 *>(tbins + t * RB_BINS)[lane];
+    uint32_t word = 0;  // constant-index selects: no dynamic indexing into the kernel argument
+#pragma unroll
+    for (int i = 0; i < (int)(RB_BINS / 32); ++i)
+        if ((lane >> 3) == (uint32_t)i) word = sel.m[i];
+    const uint32_t bits = (word >> (4 * (lane & 7))) & 0xFu;
+    uint32_t s = ((bits & 1u) ? (v.x & 0xFFFFu) : 0u) + ((bits & 2u) ? (v.x >> 16) : 0u) +
+                 ((bits & 4u) ? (v.y & 0xFFFFu) : 0u) + ((bits & 8u) ? (v.y >> 16) : 0u);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) tcnt[t] = s;
 }
 
-// write pass of the range [blo, bhi) of bins: the tile's k-mers in it at toff[tile]
+// write pass of the bins of `sel`: the tile's k-mers in them at toff[tile]
 template <int L, bool COUNTED>
 __global__ __launch_bounds__(256) void range_write_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int both,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
-    uint32_t cmax, uint32_t blo, uint32_t bhi, const uint64_t *__restrict__ toff, Key<L> *__restrict__ out,
+    uint32_t cmax, BinSet sel, const uint64_t *__restrict__ toff, Key<L> *__restrict__ out,
     uint32_t *__restrict__ out_counts) {
     using T = RangeTraits<L>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
@@ -146,7 +170,11 @@ __global__ __launch_bounds__(256) void range_write_kernel(
     __shared__ uint32_t s_pack[T::PACK];
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
     __shared__ uint16_t s_item[2 * TILE];
+    __shared__ uint32_t s_sel[RB_BINS / 32];
     const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < (int)(RB_BINS / 32); ++i)
+        if (tid == (uint32_t)i) s_sel[i] = sel.m[i];
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
@@ -175,8 +203,8 @@ __global__ __launch_bounds__(256) void range_write_kernel(
 #pragma unroll
         for (int j = 0; j < PPT; ++j) {
             if (!((m >> j) & 1u)) continue;
-            if (fb[j] >= blo && fb[j] < bhi) emit |= 1u << j;
-            if (both && rb[j] >= blo && rb[j] < bhi) emit |= 1u << (16 + j);
+            if ((s_sel[fb[j] >> 5] >> (fb[j] & 31)) & 1u) emit |= 1u << j;
+            if (both && (s_sel[rb[j] >> 5] >> (rb[j] & 31)) & 1u) emit |= 1u << (16 + j);
         }
     }
     // compact the tile's emitted k-mers into an LDS list (window << 1 | strand), then build and

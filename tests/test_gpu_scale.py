@@ -133,3 +133,94 @@ def test_full_bench_size_order_invariant():
     ch = ctor.build_chunk()
     assert len(ch.W) == a[0] and list(ch.F) == a[2]
     assert np.array_equal(ch.W, a[3]) and np.array_equal(ch.last, a[4])
+
+
+def _device_arrays(dc, bits):
+    L_ = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    last = np.empty(dc.n, dtype=np.uint8)
+    assert L_.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n) == 0
+    assert L_.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n) == 0
+    wt = None
+    if bits:
+        wt = np.empty(dc.n, dtype=np.uint32)
+        assert L_.mtg_memcpy_d2h(wt.ctypes.data, dc.weights, dc.n * 4) == 0
+    return W, last, wt
+
+
+# configs[1] at its full size (10 M genome-sampled reads, 1.2e9 windows), bit for bit against the
+# oracle (~40 s of oracle time on the box's 16 threads per build)
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("canonical,bits", [(True, 0), (False, 0), (True, 8)])
+def test_full_bench_size_vs_oracle(canonical, bits):
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n_reads, L = 10_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=canonical, bits_per_count=bits)
+    dc = ctor.build_device(seq.data_ptr(), seq.numel())
+    t = ctor.timings()
+    assert t.n_extracted == n_reads * (L - 31 + 1) and t.n_batches == 1
+    W, last, wt = _device_arrays(dc, bits)
+    F = np.array([int(f) for f in dc.F], dtype=np.uint64)
+    n_real = dc.n_real
+    del ctor
+    host = seq.cpu().numpy()  # reads with their '$' separators: no window spans one
+    del seq
+    want = O.build_chunk_packed(30, host, np.arange(n_reads + 1, dtype=np.uint64) * (L + 1),
+                                canonical=canonical, bits_per_count=bits)
+    assert len(W) == len(want.W)
+    assert np.array_equal(W, want.W) and np.array_equal(last, want.last)
+    assert np.array_equal(F, want.F) and n_real == want.n_real
+    if bits:
+        assert np.array_equal(wt, want.weights)
+
+
+# configs[2]'s bounded-memory planner without overrides: a budget for which plan_ranges itself
+# picks 8 key ranges (k = 63, u128 keys, 4 M reads), bit for bit against the oracle
+@pytest.mark.timeout(900)
+def test_cfg3_planner_default_ranges_vs_oracle():
+    asc = bench.make_reads_host_codes(4_000_000, 150, 777, "genome", 10.0)
+    ctor = boss.IBOSSChunkConstructor.initialize(62, both_strands=True, bits_per_count=0,
+                                                 num_threads=8, memory_preallocated=1.2e10)
+    data, off = _packed(asc)
+    ctor.add_packed(data, off)
+    got = ctor.build_chunk()
+    t = ctor.timings()
+    assert t.n_batches >= 8, t.n_batches
+    want = O.build_chunk_packed(62, data, off, canonical=True)
+    _assert_same(got, want, "cfg3 planner, %d ranges" % t.n_batches)
+
+
+# configs[3]: one full 125 M-read share (1.5e10 windows) through the multi-GPU build on a
+# one-rank group: the batched collect plans its own rounds from the free HBM; size identities, and
+# the same reads through the single-GPU bounded build (key ranges) give the same arrays
+@pytest.mark.timeout(1200)
+def test_cfg4_share_dist_batched():
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n_reads, L = 125_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    comm = boss.Comm.local_group(1)[0]
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True)
+    dc = ctor.build_device(seq.data_ptr(), seq.numel(), comm=comm)
+    t = ctor.timings()
+    assert t.n_batches >= 2 and t.world == 1
+    assert t.n_extracted == n_reads * (L - 31 + 1)
+    assert dc.n == t.n_rows == 1 + dc.n_real + dc.n_dummy
+    W, last, _ = _device_arrays(dc, 0)
+    F = [int(f) for f in dc.F]
+    assert W[0] == 0 and last[0] == 0 and last[-1] == 1
+    assert F == sorted(F) and F[4] <= dc.n - 1
+    assert int(np.count_nonzero((W % 5) != 0)) >= dc.n_real
+    n_rows = dc.n
+    # the single-GPU build of the same reads (key ranges) on the same constructor
+    dc2 = ctor.build_device(seq.data_ptr(), seq.numel())
+    t2 = ctor.timings()
+    assert t2.n_batches >= 2 and dc2.n == n_rows
+    W2, last2, _ = _device_arrays(dc2, 0)
+    assert [int(f) for f in dc2.F] == F
+    assert np.array_equal(W, W2) and np.array_equal(last, last2)

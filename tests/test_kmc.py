@@ -132,3 +132,137 @@ def test_build_from_kmc_mixed_with_reads(transcripts_1000):
     want = O.build_chunk(10, list(reads) + [s for s, _ in recs], canonical=True, bits_per_count=8,
                          counts=[1] * len(reads) + [c for _, c in recs])
     assert np.array_equal(got.W, want.W) and np.array_equal(got.weights, want.weights)
+
+
+# ---------------------------------------------------------------- the builder's KMC1 writer
+#
+# BASELINE config 5 builds from a KMC database of k = 31 counts.  KMC itself is not in the image,
+# so the builder writes its own databases (mtg_kmc_write_device: GPU k-mer counting, KMC record
+# order and header); kmc_oracle -- pinned on the reference's fixtures above -- reads them back.
+
+def _device_reads(reads):
+    data = b"".join((r if isinstance(r, bytes) else r.encode()) + b"$" for r in reads)
+    L = boss.lib()
+    d = L.mtg_device_alloc(0, max(len(data), 1))
+    assert d
+    assert L.mtg_memcpy_h2d(d, data, len(data)) == 0
+    return d, len(data)
+
+
+def _lex_counts(reads, k, canonical):
+    c = collections.Counter()
+    for s in reads:
+        s = s if isinstance(s, bytes) else s.encode()
+        s = s.upper().replace(b"U", b"T")
+        for i in range(len(s) - k + 1):
+            w = s[i:i + k]
+            if w.strip(b"ACGT"):
+                continue
+            if canonical:
+                w = min(w, w[::-1].translate(RC))
+            c[w] += 1
+    return c
+
+
+def _write_db(tmp_path, reads, k, canonical, cs=1, name="db"):
+    d, n = _device_reads(reads)
+    try:
+        ctor = boss.IBOSSChunkConstructor.initialize(max(k - 1, 1))
+        base = str(tmp_path / name)
+        total = ctor.write_kmc(d, n, base, k, canonical=canonical, counter_size=cs)
+    finally:
+        boss.lib().mtg_device_free(d)
+    return base, total
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,canonical,cs", [(31, True, 1), (31, False, 2), (11, True, 1), (32, True, 4),
+                                            (15, False, 1), (3, True, 1)])
+def test_kmc_writer_roundtrip(tmp_path, k, canonical, cs):
+    from test_gpu_parity import _random_reads
+    reads = _random_reads(40 + k, 3000, 150, 30000, n_rate=0.002, lower=True)
+    reads += [b"ACGT" * 40, b"A" * 200]  # palindromes and a saturating count
+    base, total = _write_db(tmp_path, reads, k, canonical, cs)
+    want = _lex_counts(reads, k, canonical)
+    h = kmc_oracle.read_header(base)
+    assert (h["k"], h["counter_size"], h["total"], h["both_strands"]) == (k, cs, len(want), canonical)
+    assert (h["k"] - h["lut_len"]) % 4 == 0
+    got = kmc_oracle.read_kmers(base)
+    cmax = (1 << (8 * cs)) - 1
+    assert [w for w, _ in got] == sorted(want)  # KMC record order: lexicographic
+    assert all(c == min(want[w], cmax) for w, c in got)
+
+
+@pytest.mark.gpu
+def test_kmc_writer_empty_and_short(tmp_path):
+    base, total = _write_db(tmp_path, [b"ACGTN", b"NNNN"], 11, True)
+    assert total == 0 and kmc_oracle.read_kmers(base) == []
+    assert kmc_oracle.read_header(base)["total"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("canonical,bits", [(True, 8), (False, 16), (True, 0)])
+def test_build_from_written_kmc_k31(tmp_path, canonical, bits):
+    # configs[4]: k = 31 --count-kmers on a KMC database of the reads' canonical counts, through both
+    # inputs: add_kmc (the file, decoded at build time) and the device-resident decode
+    from test_gpu_parity import _random_reads
+    reads = _random_reads(77, 6000, 150, 60000, n_rate=0.0005)
+    base, total = _write_db(tmp_path, reads, 31, True)
+    got = _gpu_kmc(30, base, canonical, bits)
+    want = _oracle_kmc(30, base, canonical, bits)
+    for a in ("W", "last", "F") + (("weights",) if bits else ()):
+        assert np.array_equal(getattr(got, a), getattr(want, a)), a
+    dr = boss.DeviceReads(base, call_both_from_canonical=not canonical)
+    assert dr.n_reads == total * (1 if canonical else 2)
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=canonical, bits_per_count=bits)
+    dc = ctor.build_device(*dr.build_args())
+    L = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    L.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n)
+    assert np.array_equal(W, want.W) and list(dc.F) == list(want.F)
+    if bits:
+        wt = np.empty(dc.n, dtype=np.uint32)
+        L.mtg_memcpy_d2h(wt.ctypes.data, dc.weights, dc.n * 4)
+        assert np.array_equal(wt, want.weights)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,rounds", [(1, 0), (2, 0), (3, 0), (4, 0), (2, 3), (4, 5)])
+def test_dist_build_from_kmc_k31(tmp_path, monkeypatch, P, rounds):
+    # configs[4] across ranks: every rank counts its own reads into its own database; the ranks'
+    # records meet at their owners, where the counts add with saturation (the count-aggregating
+    # merge), and the concatenated rank chunks equal the oracle's build of all records
+    import threading
+    from test_gpu_parity import _random_reads
+    if rounds:
+        monkeypatch.setenv("MTG_RANGES", str(rounds))
+    reads = _random_reads(91, 4000, 150, 20000, n_rate=0.0005)
+    bases = [_write_db(tmp_path, reads[r::P], 31, True, name="r%d" % r)[0] for r in range(P)]
+    for canonical, bits in ((True, 8), (False, 16)):
+        comms = boss.Comm.local_group(P)
+        ctors = [boss.IBOSSChunkConstructor.initialize(30, both_strands=canonical, bits_per_count=bits)
+                 for _ in range(P)]
+        for r in range(P):
+            ctors[r].add_kmc(bases[r])
+        out, errs = [None] * P, []
+
+        def run(r):
+            try:
+                out[r] = ctors[r].build_chunk(comm=comms[r])
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errs.append((r, e))
+
+        ts = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=300)
+        assert not errs, errs
+        got = boss.concatenate(out)
+        recs = [rec for b in bases for rec in kmc_oracle.read_kmers(b, not canonical)]
+        want = O.build_chunk(30, [s for s, _ in recs], canonical=canonical, bits_per_count=bits,
+                             counts=[c for _, c in recs])
+        for a in ("W", "last", "F", "weights"):
+            assert np.array_equal(getattr(got, a), getattr(want, a)), (a, canonical, bits)
+        if rounds:
+            assert all(c.timings().n_batches == rounds for c in ctors)
