@@ -70,6 +70,8 @@ def parse():
                     help="reads of the FASTA-file leg (0 = skip)")
     ap.add_argument("--kmc", action="store_true",
                     help="build from a KMC1 database of the reads' canonical k-mer counts (configs[4])")
+    ap.add_argument("--parity-full-max", type=int, default=10_000_000,
+                    help="largest read count whose whole workload the bench checks against the oracle")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
     if args.config:
@@ -182,6 +184,35 @@ def cpu_baseline(args, kb, boss):
               "what": "GPU build (host C ABI) of the cpu_baseline sample vs the oracle: W, last, F, "
                       "weights bit for bit"}
     return base, parity
+
+
+def full_parity(args, kb, boss, dc, seq):
+    """The bench's own workload, whole: the device chunk of the last timed step against the oracle
+    built from all of this rank's reads (W, last, F, weights bit for bit).  Single-GPU lines only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle_ctypes
+    L = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    last = np.empty(dc.n, dtype=np.uint8)
+    L.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n)
+    L.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n)
+    wt = None
+    if args.count_width:
+        wt = np.empty(dc.n, dtype=np.uint32)
+        L.mtg_memcpy_d2h(wt.ctypes.data, dc.weights, dc.n * 4)
+    F = np.array([int(f) for f in dc.F], dtype=np.uint64)
+    host = seq.cpu().numpy()  # the reads with their '$' separators
+    stride = args.read_len + 1
+    t0 = time.perf_counter()
+    c = oracle_ctypes.build_chunk_packed(kb, host, np.arange(args.reads + 1, dtype=np.uint64) * stride,
+                                         canonical=args.mode == "canonical", bits_per_count=args.count_width)
+    dt = time.perf_counter() - t0
+    same = (len(W) == len(c.W) and np.array_equal(W, c.W) and np.array_equal(last, c.last)
+            and np.array_equal(F, c.F) and (wt is None or np.array_equal(wt, c.weights)))
+    return {"ok": bool(same), "rows": int(len(c.W)), "oracle_s": dt,
+            "what": "the timed step's device chunk (all %d reads of the workload) vs the oracle on the same "
+                    "reads: W, last, F, weights bit for bit" % args.reads}
 
 
 def cpu_baseline_kmc(args, kb, boss, kmc_base, n_records):
@@ -533,7 +564,12 @@ def main():
         if args.kmc:
             result["cpu_baseline"], result["parity"] = cpu_baseline_kmc(args, kb, boss, kmc_base, kmers_per_rank)
         else:
-            result["cpu_baseline"], result["parity"] = cpu_baseline(args, kb, boss)
+            result["cpu_baseline"], sample_parity = cpu_baseline(args, kb, boss)
+            if world == 1 and args.reads <= args.parity_full_max:
+                result["parity"] = full_parity(args, kb, boss, dc, seq)
+                result["parity"]["sample"] = sample_parity
+            else:
+                result["parity"] = sample_parity
     if kmc_dir:
         import shutil
         del dreads

@@ -240,6 +240,23 @@ void mtg_comm_destroy(mtg_comm *comm);
 int mtg_comm_rank(const mtg_comm *comm);
 int mtg_comm_size(const mtg_comm *comm);
 
+/*
+ * The same exchange over caller-supplied functions on HOST buffers (each returns 0 on success): the
+ * library stages every step's device data through host memory and calls them from the building
+ * thread.  Any transport carries the build this way (torch.distributed over gloo, MPI, sockets);
+ * RCCL over xGMI stays the fast path.  alltoallv: the bytes for rank j are send[sum scnt[0..j)]..
+ * (scnt[j] bytes), the bytes from rank i land at recv[sum rcnt[0..i)]...
+ */
+typedef struct mtg_comm_callbacks {
+    void *user;
+    int rank;
+    int world;
+    int (*allreduce_sum_u64)(void *user, uint64_t *buf, size_t n);
+    int (*allgather_u64)(void *user, const uint64_t *send, uint64_t *recv, size_t n);
+    int (*alltoallv)(void *user, const void *send, const uint64_t *scnt, void *recv, const uint64_t *rcnt);
+} mtg_comm_callbacks;
+mtg_comm *mtg_comm_create_callbacks(const mtg_comm_callbacks *callbacks);
+
 /* this rank's chunk of the global build (host input staged with mtg_boss_ctor_add_*) */
 int mtg_boss_ctor_build_chunk_dist(mtg_boss_ctor *ctor, mtg_comm *comm, mtg_boss_chunk *out);
 /* the same on device-resident reads */

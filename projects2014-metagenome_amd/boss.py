@@ -51,6 +51,19 @@ class _DeviceReads(ctypes.Structure):
                 ("counts", ctypes.c_void_p), ("n_reads", ctypes.c_uint64), ("device_id", ctypes.c_int)]
 
 
+_ALLREDUCE_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t)
+_ALLGATHER_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t)
+_ALLTOALLV_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
+class _CommCallbacks(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("rank", ctypes.c_int), ("world", ctypes.c_int),
+                ("allreduce_sum_u64", _ALLREDUCE_CB), ("allgather_u64", _ALLGATHER_CB),
+                ("alltoallv", _ALLTOALLV_CB)]
+
+
 class _DbgFile(ctypes.Structure):
     _fields_ = [(name, ctypes.c_uint64) for name in ("k", "n")] + \
                [("F", ctypes.c_uint64 * 5)] + \
@@ -91,7 +104,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free",
            "mtg_boss_ctor_add_fasta", "mtg_device_copy", "mtg_kmc_load_device",
            "mtg_device_reads_free", "mtg_kmc_write_device", "mtg_host_pool_bytes",
-           "mtg_host_pool_trim")
+           "mtg_host_pool_trim", "mtg_comm_create_callbacks")
 
 COMM_ID_BYTES = 128
 
@@ -162,6 +175,8 @@ def lib():
                                           ctypes.c_int, P(_DeviceReads)]
         L.mtg_device_reads_free.argtypes = [P(_DeviceReads)]
         L.mtg_host_pool_bytes.restype = ctypes.c_uint64
+        L.mtg_comm_create_callbacks.argtypes = [P(_CommCallbacks)]
+        L.mtg_comm_create_callbacks.restype = ctypes.c_void_p
         L.mtg_kmc_write_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint,
                                            ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_char_p,
                                            P(ctypes.c_uint64)]
@@ -515,11 +530,91 @@ class Comm:
         return Comm(h)
 
     @staticmethod
+    def callbacks(rank, world, allreduce_sum_u64, allgather_u64, alltoallv):
+        """One rank of a build whose exchanges run through Python functions on host numpy arrays
+        (mtg_comm_create_callbacks): allreduce_sum_u64(buf) in place; allgather_u64(send) -> array
+        of world * len(send); alltoallv(send_bytes, scounts) -> received bytes in rank order."""
+        def ar(_u, buf, n):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(n,)) if n else np.zeros(0, dtype=np.uint64)
+                a[:] = allreduce_sum_u64(a.copy())
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the library as a failed exchange
+                return 1
+
+        def ag(_u, send, recv, n):
+            try:
+                a = np.ctypeslib.as_array(send, shape=(n,)).copy() if n else np.zeros(0, dtype=np.uint64)
+                out = np.ctypeslib.as_array(recv, shape=(n * world,)) if n else None
+                got = allgather_u64(a)
+                if n:
+                    out[:] = got
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        def a2a(_u, send, scnt, recv, rcnt):
+            try:
+                sc = np.ctypeslib.as_array(scnt, shape=(world,)).copy()
+                rc = np.ctypeslib.as_array(rcnt, shape=(world,)).copy()
+                st, rt = int(sc.sum()), int(rc.sum())
+                sb = np.frombuffer((ctypes.c_uint8 * st).from_address(send), dtype=np.uint8) if st else \
+                    np.zeros(0, dtype=np.uint8)
+                got = alltoallv(sb.copy(), sc, rc)
+                if rt:
+                    np.frombuffer((ctypes.c_uint8 * rt).from_address(recv), dtype=np.uint8)[:] = got
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        cb = _CommCallbacks(None, rank, world, _ALLREDUCE_CB(ar), _ALLGATHER_CB(ag), _ALLTOALLV_CB(a2a))
+        h = lib().mtg_comm_create_callbacks(ctypes.byref(cb))
+        if not h:
+            raise RuntimeError(lib().mtg_last_error().decode())
+        c = Comm(h)
+        c._keep = cb  # the C function pointers must outlive the communicator
+        return c
+
+    @staticmethod
+    def torch_distributed(group=None):
+        """This process's rank of a build exchanging over an initialised torch.distributed group
+        (e.g. gloo between processes that share one GPU): host-staged, see callbacks()."""
+        f = torch_exchange_functions(group)
+        import torch.distributed as dist
+        return Comm.callbacks(dist.get_rank(group), dist.get_world_size(group), *f)
+
+    @staticmethod
     def local_group(world):
         """`world` ranks inside this process on one device (one host thread per rank)."""
         arr = (ctypes.c_void_p * world)()
         _check(lib().mtg_comm_create_local(world, arr))
         return [Comm(arr[r]) for r in range(world)]
+
+
+def torch_exchange_functions(group=None):
+    """The three exchange functions of Comm.callbacks over torch.distributed CPU tensors (gloo)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+
+    def allreduce(a):
+        t = torch.from_numpy(a.view(np.int64).copy())  # sums wrap like uint64
+        dist.all_reduce(t, group=group)
+        return t.numpy().view(np.uint64)
+
+    def allgather(a):
+        t = torch.from_numpy(a.view(np.int64).copy())
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return np.concatenate([o.numpy().view(np.uint64) for o in out])
+
+    def alltoallv(send, scounts, rcounts):
+        out = torch.empty(int(rcounts.sum()), dtype=torch.uint8)
+        dist.all_to_all_single(out, torch.from_numpy(send), [int(c) for c in rcounts],
+                               [int(c) for c in scounts], group=group)
+        return out.numpy()
+
+    return allreduce, allgather, alltoallv
 
 
 def dist_bounds(hist, world):

@@ -49,6 +49,7 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
                                                   unsigned K, int canonical,
                                                   const uint64_t *__restrict__ read_starts,
                                                   const uint32_t *__restrict__ read_counts, uint64_t n_reads,
+                                                  const uint64_t *__restrict__ rid_at,
                                                   uint32_t cmax, Key<L> (&kk)[PPT], uint32_t (&cc)[PPT]) {
     uint32_t valid_mask = 0;
     if (p0 >= npos) return 0;
@@ -63,14 +64,7 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
         R = R | shl(Key<L>::from(3 - c), 2 * (K - 1 - i));
     }
     uint64_t rid = 0;
-    if (KEYS && COUNTED && read_counts) {
-        uint64_t lo = 0, hi = n_reads;  // last read with start <= p0
-        while (hi - lo > 1) {
-            uint64_t mid = (lo + hi) / 2;
-            if (read_starts[mid] <= p0) lo = mid; else hi = mid;
-        }
-        rid = lo;
-    }
+    if (KEYS && COUNTED && read_counts) rid = read_of(read_starts, n_reads, rid_at, p0);  // last start <= p0
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const uint64_t p = p0 + j;
@@ -126,7 +120,7 @@ template <int L, bool COUNTED, bool COUNT_ONLY>
 __global__ __launch_bounds__(256) void extract_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts,
-    uint64_t n_reads, uint32_t cmax, Key<L> *__restrict__ out_keys,
+    uint64_t n_reads, const uint64_t *__restrict__ rid_at, uint32_t cmax, Key<L> *__restrict__ out_keys,
     uint32_t *__restrict__ out_counts, uint32_t *__restrict__ tcnt,
     const uint64_t *__restrict__ toff, uint32_t *__restrict__ hist, unsigned hist_bits) {
     // hist: when hist_bits > 0, counts of the top hist_bits (<= 9) bits of the 2K-bit keys
@@ -153,7 +147,7 @@ __global__ __launch_bounds__(256) void extract_kernel(
     Key<L> kk[PPT];
     uint32_t cc[PPT];
     const uint32_t valid_mask = slide_windows<L, COUNTED, PPT, !COUNT_ONLY>(
-        s_code, tid * PPT, p0, npos, K, canonical, read_starts, read_counts, n_reads, cmax, kk, cc);
+        s_code, tid * PPT, p0, npos, K, canonical, read_starts, read_counts, n_reads, rid_at, cmax, kk, cc);
     const uint32_t nvalid = __popc(valid_mask);
     uint32_t tile_total;
     const uint32_t off = block_exclusive_sum<BLOCK>(nvalid, s_scan, &tile_total);
@@ -1180,6 +1174,76 @@ __global__ __launch_bounds__(256) void emit_kernel(
             if (COUNTED) weights[o] = wt[j];
             ++o;
         }
+    }
+}
+
+
+// ------------------------------------------------------------------ dummy keys as dense ranks
+//
+// Every dummy edge of the construction (sinks boss_chunk_construct.cpp:54-98, sources of every
+// level :123-168, 286-306), read from its most significant char down, is r_1 .. r_m $^(k-m) c: m
+// real node chars, the $ run of a source of level k - m, then the label c (real for a source; $ for
+// a sink, where m = k).  In the lifted order ($ < A < C < G < T) these strings are the leaves of a
+// trie whose subtree below d real chars holds T(k) = 1, T(d) = 4 + 4 T(d + 1) = (7 4^(k-d) - 4) / 3
+// strings (the 4 sources that stop there, then the A, C, G, T subtrees), so a dummy's rank among
+// all of them is
+//     4 m + sum_p r_p T(p) + (m < k ? c : 0)  =  4 m + (7 W - 4 S) / 3 + (m < k ? c : 0),
+// W = the real chars as a left-aligned 2-bit word (r_1 highest, 4^(k-p) for r_p), S = their sum.
+// The rank is an order-preserving injection into [0, T(0)), 62 bits at k = 30, so the dummy sort runs
+// on u64 keys (8 LSD passes) instead of the 3(k+1)-bit lifted keys (k = 30: 93 bits, 12 passes over
+// 16-byte keys).  Valid for k <= 30 (7 4^k < 2^64).  A key outside that shape raises *bad (the
+// caller then sorts the lifted keys).
+
+__host__ __device__ inline uint64_t dummy_rank_space(unsigned k) {  // T(0)
+    return (7ull * (1ull << (2 * k)) - 4) / 3;
+}
+
+template <int L3>
+__global__ void dummy_encode_kernel(const Key<L3> *__restrict__ in, uint64_t n, unsigned k,
+                                    uint64_t *__restrict__ out, uint32_t *__restrict__ bad) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    bool err = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        const Key<L3> x = in[i];
+        uint64_t W = 0, S = 0;
+        unsigned m = 0, top_dollar = 0;  // highest node position holding $
+        for (unsigned j = 1; j <= k; ++j) {
+            const uint32_t v = char_at(x, j, 3);
+            if (v) {
+                W |= (uint64_t)(v - 1) << (2 * (j - 1));
+                S += v - 1;
+                ++m;
+            } else {
+                top_dollar = j;
+            }
+        }
+        const uint32_t c = char_at(x, 0, 3);
+        // the $ run must be exactly node positions 1 .. k - m, the label real iff m < k
+        err |= top_dollar != k - m || (m < k) != (c != 0) || c > 4 || shr(x, 3 * (k + 1)) != Key<L3>::zero();
+        out[i] = 4ull * m + (7 * W - 4 * S) / 3 + (m < k ? (uint64_t)(c - 1) : 0ull);
+    }
+    if (err) atomicOr(bad, 1u);
+}
+
+template <int L3>
+__global__ void dummy_decode_kernel(const uint64_t *__restrict__ in, uint64_t n, unsigned k, Key<L3> *__restrict__ out) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t T0 = dummy_rank_space(k);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+        uint64_t r = in[i], T = T0;
+        Key<L3> x = Key<L3>::zero();
+        for (unsigned p = 1; p <= k; ++p) {
+            if (r < 4) {  // a source of level k - (p - 1): its label
+                x = x | Key<L3>::from(r + 1);
+                break;
+            }
+            r -= 4;
+            T = (T - 4) / 4;  // T(p): strings below one real char at depth p
+            const uint64_t rp = (uint64_t)(r >= T) + (r >= 2 * T) + (r >= 3 * T);
+            r -= rp * T;
+            x = x | shl(Key<L3>::from(rp + 1), 3 * (k - p + 1));  // r_p sits at node position k - p + 1
+        }
+        out[i] = x;  // all k node chars real: a sink (label $)
     }
 }
 

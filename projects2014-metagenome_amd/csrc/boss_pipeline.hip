@@ -58,7 +58,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -103,6 +103,7 @@ struct Small {  // one device word block, zeroed per use
     uint32_t counter;
     uint32_t skip;
     uint32_t root_same;
+    uint32_t bad_dummy;
     uint32_t error;
 };
 
@@ -156,6 +157,8 @@ struct Ctx {
     double fused_ms = 0;           // device time of the last fused extract+partition launch
     bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it (the
                                    // redundant-sink path)
+    bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
+                                   // dense u64 ranks (dummy_encode_kernel)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
     const void *bidx_keys = nullptr;
     uint64_t bidx_n = 0;
@@ -177,6 +180,7 @@ static void load_knobs(Ctx &c) {
     c.emit_slow = is("MTG_EMIT", "slow");
     c.fused = !is("MTG_FUSED", "0");
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
+    c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
     c.debug = getenv("MTG_DEBUG") != nullptr;
     c.trace = getenv("MTG_TRACE") != nullptr;
     if (const char *e = getenv("MTG_FUSED_MIN")) c.fused_min = strtoull(e, nullptr, 10);
@@ -705,6 +709,7 @@ struct BuildInput {
     const uint64_t *read_starts;
     const uint32_t *read_counts;
     uint64_t n_reads;
+    const uint64_t *rid_at = nullptr;  // per-read counts: the read of every 4 K-position block
 };
 
 struct BuildOutput {
@@ -769,7 +774,7 @@ static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax,
         uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
         uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
         extract_kernel<L2, COUNTED, true><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax,
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
             nullptr, nullptr, tcnt, nullptr, nullptr, 0);
         HIP_CHECK(hipGetLastError());
         uint32_t ep;
@@ -781,7 +786,7 @@ static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax,
         HIP_CHECK(hipGetLastError());
         N = read_u64(c, (const unsigned long long *)(toff + tiles));
         extract_kernel<L2, COUNTED, false><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax,
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
             *ka, *ca, nullptr, toff, nullptr, 0);
         HIP_CHECK(hipGetLastError());
     }
@@ -892,7 +897,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
             constexpr int B = decltype(blk)::value;
             const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, B>::TILE);
             extract_partition_kernel<COUNTED, B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, cmax, b1,
+                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
                 per_stripe, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
         };
         if (fast_b) {
@@ -1053,7 +1058,7 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
                                                                           &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
         range_write_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, cmax, sel, toff, ka, ca);
+            in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, sel, toff, ka, ca);
         HIP_CHECK(hipGetLastError());
         const uint64_t N = read_u64(c, (const unsigned long long *)(toff + tiles));
         if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
@@ -1147,6 +1152,40 @@ static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db
                                     Key<L3> **dk) {
     uint64_t D = 0;
     uint32_t *nv = nullptr;
+    const unsigned kb = K - 1;
+    if (c.dummy_ranks && kb >= 1 && kb <= 30 && Draw) {
+        // as dense u64 ranks (boss_kernels.hpp: dummy_encode_kernel): ranks in db's memory, the
+        // sort's ping-pong in da's once encoded, the distinct keys decoded into the other one
+        Key<1> *ra = (Key<1> *)db, *rb = (Key<1> *)da;
+        HIP_CHECK(hipMemsetAsync(&c.small->bad_dummy, 0, 4, c.stream));
+        const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(Draw, 256), 16384);
+        dummy_encode_kernel<L3><<<dim3(g), dim3(256), 0, c.stream>>>(da, Draw, kb, (uint64_t *)ra, &c.small->bad_dummy);
+        HIP_CHECK(hipGetLastError());
+        uint32_t bad = 0;
+        HIP_CHECK(hipMemcpyAsync(&bad, &c.small->bad_dummy, 4, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (!bad) {
+            const uint64_t space = dummy_rank_space(kb);
+            const unsigned nbits = 64 - (unsigned)__builtin_clzll(space);
+            radix_sort<1, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
+            reset_small(c);
+            const uint64_t ut = ceil_div(Draw, 2048);
+            uint32_t udesc_ep;
+            uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
+            unique_kernel<1, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+                ra, nullptr, Draw, rb, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            D = read_u64(c, &c.small->total);
+            // the distinct ranks are in rb's memory: decode into the other buffer
+            Key<L3> *outk = (void *)rb == (void *)da ? db : da;
+            dummy_decode_kernel<L3><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
+                                      dim3(256), 0, c.stream>>>((const uint64_t *)rb, D, kb, outk);
+            HIP_CHECK(hipGetLastError());
+            *dk = outk;
+            return D;
+        }
+        if (c.debug) fprintf(stderr, "[mtg debug] dummy keys outside the rank shape: lifted sort\n");
+    }
     {
         radix_sort<L3, false>(c, &da, &db, &nv, &nv, Draw, 3 * K, false);
         reset_small(c);
@@ -1770,7 +1809,7 @@ static uint64_t collect_ranges_dist(Ctx &c, Dist &d, unsigned K, bool canonical,
                                                                               &c.small->counter, &c.small->error);
             HIP_CHECK(hipGetLastError());
             range_write_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-                in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, cmax, sel, toff, ka, ca);
+                in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, sel, toff, ka, ca);
             HIP_CHECK(hipGetLastError());
             const uint64_t N = read_u64(c, (const unsigned long long *)(toff + tiles));
             if (N != nj) throw std::runtime_error("range extraction count differs from its histogram");
@@ -2150,7 +2189,7 @@ static void run_suffix(Ctx &c, unsigned k, bool both, unsigned bits, const Suffi
     uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
     uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
     suffix_extract_kernel<L3, COUNTED, true><<<dim3((unsigned)tiles), dim3(T::BLOCK), 0, c.stream>>>(
-        in.seq, in.seq_len, K, both ? 1 : 0, suf, in.read_starts, in.read_counts, in.n_reads, cmax, tcnt,
+        in.seq, in.seq_len, K, both ? 1 : 0, suf, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, tcnt,
         nullptr, nullptr, nullptr);
     HIP_CHECK(hipGetLastError());
     {
@@ -2171,7 +2210,7 @@ static void run_suffix(Ctx &c, unsigned k, bool both, unsigned bits, const Suffi
     uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(cap, 1) * 4) : nullptr;
     if (N) {
         suffix_extract_kernel<L3, COUNTED, false><<<dim3((unsigned)tiles), dim3(T::BLOCK), 0, c.stream>>>(
-            in.seq, in.seq_len, K, both ? 1 : 0, suf, in.read_starts, in.read_counts, in.n_reads, cmax, nullptr,
+            in.seq, in.seq_len, K, both ? 1 : 0, suf, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, nullptr,
             toff, ka, ca);
         HIP_CHECK(hipGetLastError());
     }
@@ -2602,7 +2641,16 @@ static const char *kSuffixDist =
     "the suffix-filtered route builds one chunk per suffix on one GPU; it has no multi-GPU form";
 
 // the build on the device buffers: the suffix route or the full construction
-static void dispatch_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {
+static void dispatch_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in_, BuildOutput *out) {
+    BuildInput in = in_;
+    if (in.read_counts && in.n_reads > 1) {  // bracket the per-read count searches (device_common.hpp)
+        const uint64_t nq = (in.seq_len >> mtg::RID_SHIFT) + 2;
+        uint64_t *rid = (uint64_t *)c->ctx.ws.get(mtg::Workspace::RID_AT, nq * 8);
+        read_index_kernel<<<dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, c->ctx.stream>>>(in.read_starts,
+                                                                                          in.n_reads, nq, rid);
+        HIP_CHECK(hipGetLastError());
+        in.rid_at = rid;
+    }
     if (!c->suffix.empty()) {
         bool all_sentinel = false;
         const mtg::SuffixSpec spec = encode_suffix(c->suffix, &all_sentinel);
@@ -3029,6 +3077,22 @@ int mtg_comm_create_local(int world, mtg_comm **comms) {
         comms[r]->comm.reset(new mtg::LocalComm(group, r));
     }
     return MTG_OK;
+}
+
+mtg_comm *mtg_comm_create_callbacks(const mtg_comm_callbacks *cb) {
+    if (!cb || cb->world < 1 || cb->rank < 0 || cb->rank >= cb->world || cb->world > mtg::MAX_RANKS ||
+        !cb->allreduce_sum_u64 || !cb->allgather_u64 || !cb->alltoallv) {
+        set_error("bad arguments");
+        return nullptr;
+    }
+    mtg::CommCallbacks f;
+    f.user = cb->user;
+    f.allreduce_sum_u64 = cb->allreduce_sum_u64;
+    f.allgather_u64 = cb->allgather_u64;
+    f.alltoallv = cb->alltoallv;
+    auto *c = new mtg_comm();
+    c->comm.reset(new mtg::CallbackComm(f, cb->rank, cb->world));
+    return c;
 }
 
 void mtg_comm_destroy(mtg_comm *comm) { delete comm; }

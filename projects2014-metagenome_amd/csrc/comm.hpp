@@ -152,6 +152,78 @@ class RcclComm : public Comm {
     ncclComm_t comm_ = nullptr;
 };
 
+// ------------------------------------------------------------------- host-staged callbacks
+//
+// The exchange over caller-supplied functions on host buffers (mtg_comm_create_callbacks): every
+// step stages its device data through host memory, calls the function, and copies the result back.
+// Any transport a caller has can carry the build this way -- torch.distributed over gloo (the
+// two-process GPU test), MPI, a socket -- at PCIe + network speed instead of xGMI.
+struct CommCallbacks {
+    void *user = nullptr;
+    // in place, n u64
+    int (*allreduce_sum_u64)(void *user, uint64_t *buf, size_t n) = nullptr;
+    // recv[r * n + i] = rank r's send[i]
+    int (*allgather_u64)(void *user, const uint64_t *send, uint64_t *recv, size_t n) = nullptr;
+    // byte all-to-all-v: the bytes for rank j are send[sum(scnt[0..j)) ..) (scnt[j] bytes), those
+    // from rank i land at recv[sum(rcnt[0..i)) ..)
+    int (*alltoallv)(void *user, const void *send, const uint64_t *scnt, void *recv, const uint64_t *rcnt) = nullptr;
+};
+
+class CallbackComm : public Comm {
+  public:
+    CallbackComm(const CommCallbacks &cb, int rank, int size) : Comm(rank, size), cb_(cb) {}
+    void allreduce_sum_u64(uint64_t *d, size_t n, hipStream_t s) override {
+        std::vector<uint64_t> h(n);
+        COMM_HIP(hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, s));
+        COMM_HIP(hipStreamSynchronize(s));
+        check(cb_.allreduce_sum_u64(cb_.user, h.data(), n), "all-reduce");
+        COMM_HIP(hipMemcpyAsync(d, h.data(), n * 8, hipMemcpyHostToDevice, s));
+        COMM_HIP(hipStreamSynchronize(s));
+    }
+    void allgather_u64(const uint64_t *d_send, uint64_t *d_recv, size_t n, hipStream_t s) override {
+        std::vector<uint64_t> h(n), all(n * size_);
+        COMM_HIP(hipMemcpyAsync(h.data(), d_send, n * 8, hipMemcpyDeviceToHost, s));
+        COMM_HIP(hipStreamSynchronize(s));
+        check(cb_.allgather_u64(cb_.user, h.data(), all.data(), n), "all-gather");
+        COMM_HIP(hipMemcpyAsync(d_recv, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+        COMM_HIP(hipStreamSynchronize(s));
+    }
+    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                   const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
+        std::vector<uint64_t> sb(size_), rb(size_);
+        uint64_t st = 0, rt = 0;
+        for (int p = 0; p < size_; ++p) {
+            sb[p] = scnt[p] * esz;
+            rb[p] = rcnt[p] * esz;
+            st += sb[p];
+            rt += rb[p];
+        }
+        std::vector<char> hs(std::max<uint64_t>(st, 1)), hr(std::max<uint64_t>(rt, 1));
+        uint64_t o = 0;
+        for (int p = 0; p < size_; ++p) {  // the slices, packed in rank order
+            if (sb[p])
+                COMM_HIP(hipMemcpyAsync(hs.data() + o, (const char *)d_send + soff[p] * esz, sb[p],
+                                        hipMemcpyDeviceToHost, s));
+            o += sb[p];
+        }
+        COMM_HIP(hipStreamSynchronize(s));
+        check(cb_.alltoallv(cb_.user, hs.data(), sb.data(), hr.data(), rb.data()), "all-to-all");
+        o = 0;
+        for (int p = 0; p < size_; ++p) {
+            if (rb[p])
+                COMM_HIP(hipMemcpyAsync((char *)d_recv + roff[p] * esz, hr.data() + o, rb[p], hipMemcpyHostToDevice, s));
+            o += rb[p];
+        }
+        COMM_HIP(hipStreamSynchronize(s));  // hr is a local
+    }
+
+  private:
+    static void check(int rc, const char *what) {
+        if (rc != 0) throw std::runtime_error(std::string("exchange callback failed: ") + what);
+    }
+    CommCallbacks cb_;
+};
+
 // ------------------------------------------------------------------- in-process rank threads
 struct LocalGroup {
     explicit LocalGroup(int n) : size(n), slots(n), host(n) {}

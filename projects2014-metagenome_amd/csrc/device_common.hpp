@@ -217,4 +217,33 @@ __device__ __forceinline__ void tile_base_lookback(uint64_t *desc, uint32_t tile
     __syncthreads();
 }
 
+// ---------------------------------------------------------------- per-read counts lookup
+//
+// The read holding buffer position p (the last r with read_starts[r] <= p), for per-read counts.
+// rid_at (optional, read_index_kernel) brackets the search: rid_at[q] = that read for position
+// q << RID_SHIFT, so a window searches the few reads of its 4 K-position block instead of all of
+// them (KMC input: one read per k + 1 bytes, 1.9e8 reads at configs[4]).
+constexpr unsigned RID_SHIFT = 12;
+
+__device__ __forceinline__ uint64_t read_of(const uint64_t *__restrict__ read_starts, uint64_t n_reads,
+                                            const uint64_t *__restrict__ rid_at, uint64_t p) {
+    uint64_t lo = 0, hi = n_reads;
+    if (rid_at) {
+        const uint64_t q = p >> RID_SHIFT;
+        lo = rid_at[q];
+        hi = min(n_reads, rid_at[q + 1] + 1);
+    }
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (read_starts[mid] <= p) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void read_index_kernel(const uint64_t *__restrict__ read_starts, uint64_t n_reads, uint64_t nq,
+                                  uint64_t *__restrict__ rid_at) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) rid_at[q] = read_of(read_starts, n_reads, nullptr, q << RID_SHIFT);
+}
+
 }  // namespace mtg

@@ -171,7 +171,7 @@ template <bool COUNTED, int BLOCK_>
 __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
-    uint32_t cmax, unsigned b, uint64_t per_stripe, unsigned long long *__restrict__ cursor,
+    const uint64_t *__restrict__ rid_at, uint32_t cmax, unsigned b, uint64_t per_stripe, unsigned long long *__restrict__ cursor,
     const unsigned long long *__restrict__ bend, Key<1> *__restrict__ kout, uint32_t *__restrict__ vout,
     uint32_t *__restrict__ error) {
     using F = FusedTraits<COUNTED, BLOCK_>;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     Key<1> kk[PPT];
     uint32_t cc[PPT];
     const uint32_t m = slide_windows<1, COUNTED, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos, K,
-                                                            canonical, read_starts, read_counts, n_reads, cmax, kk, cc);
+                                                            canonical, read_starts, read_counts, n_reads, rid_at, cmax, kk, cc);
     uint32_t r[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j)

@@ -162,7 +162,7 @@ template <int L, bool COUNTED>
 __global__ __launch_bounds__(256) void range_write_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int both,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
-    uint32_t cmax, BinSet sel, const uint64_t *__restrict__ toff, Key<L> *__restrict__ out,
+    const uint64_t *__restrict__ rid_at, uint32_t cmax, BinSet sel, const uint64_t *__restrict__ toff, Key<L> *__restrict__ out,
     uint32_t *__restrict__ out_counts) {
     using T = RangeTraits<L>;
     constexpr int BLOCK = T::BLOCK, PPT = T::PPT, TILE = T::TILE;
@@ -229,15 +229,7 @@ __global__ __launch_bounds__(256) void range_write_kernel(
         out[gb + i] = (it & 1u) ? revcomp2(f, K) : f;
         if (COUNTED) {
             uint32_t c = 1;
-            if (read_counts) {  // the read holding window base + w: last start <= it
-                const uint64_t p = base + w;
-                uint64_t lo = 0, hi = n_reads;
-                while (hi - lo > 1) {
-                    const uint64_t mid = (lo + hi) / 2;
-                    if (read_starts[mid] <= p) lo = mid; else hi = mid;
-                }
-                c = read_counts[lo];
-            }
+            if (read_counts) c = read_counts[read_of(read_starts, n_reads, rid_at, base + w)];  // window base + w
             out_counts[gb + i] = c < cmax ? c : cmax;
         }
     }

@@ -99,6 +99,7 @@ template <int L3, bool COUNTED, bool COUNT_ONLY>
 __global__ __launch_bounds__(256) void suffix_extract_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int both, SuffixSpec suf,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
+    const uint64_t *__restrict__ rid_at,
     uint32_t cmax, uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out,
     uint32_t *__restrict__ out_counts) {
     using T = SuffixTraits;
@@ -131,15 +132,8 @@ __global__ __launch_bounds__(256) void suffix_extract_kernel(
     for (int j = 0; j < T::PPT; ++j) {
         if (!ms[j]) continue;
         uint32_t c = 1;
-        if (COUNTED && read_counts) {  // the read holding position p: last start <= p
-            const uint64_t p = base + (uint64_t)tid * T::PPT + j;
-            uint64_t lo = 0, hi = n_reads;
-            while (hi - lo > 1) {
-                const uint64_t mid = (lo + hi) / 2;
-                if (read_starts[mid] <= p) lo = mid; else hi = mid;
-            }
-            c = read_counts[lo];
-        }
+        if (COUNTED && read_counts)  // the read holding position p: last start <= p
+            c = read_counts[read_of(read_starts, n_reads, rid_at, base + (uint64_t)tid * T::PPT + j)];
         c = c < cmax ? c : cmax;
         if (ms[j] & 1u) {
             out[o] = fw[j];

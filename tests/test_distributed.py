@@ -112,3 +112,46 @@ def test_comm_id_broadcast_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got[0] == got[1] == bytes(range(128))
+
+
+def _exchange_rank(rank, world, port, q):
+    # the host-staged exchange functions the library calls through mtg_comm_create_callbacks
+    import importlib
+    import numpy as np
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    boss = importlib.import_module("projects2014-metagenome_amd.boss")
+    ar, ag, a2a = boss.torch_exchange_functions()
+    s = ar(np.array([rank + 1, 2**63 + rank, 7], dtype=np.uint64))
+    g = ag(np.array([10 * rank, 10 * rank + 1], dtype=np.uint64))
+    # uneven byte all-to-all-v: rank r sends j + 1 + r bytes of value 16 r + j to rank j (none to itself
+    # on rank 1), in rank order
+    scnt = np.array([0 if (rank == 1 and j == 1) else j + 1 + rank for j in range(world)], dtype=np.uint64)
+    send = np.concatenate([np.full(int(scnt[j]), 16 * rank + j, dtype=np.uint8) for j in range(world)])
+    rcnt = np.array([0 if (i == 1 and rank == 1) else rank + 1 + i for i in range(world)], dtype=np.uint64)
+    got = a2a(send, scnt, rcnt)
+    q.put((rank, s.tolist(), g.tolist(), got.tolist()))
+    dist.destroy_process_group()
+
+
+def test_host_staged_exchange_functions_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: (s, g, a) for r, s, g, a in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        s, g, a = got[r]
+        assert s == [3, (2 * 2**63 + 1) % 2**64, 14]  # uint64 sums wrap
+        assert g == [0, 1, 10, 11]
+        want = []
+        for i in range(world):
+            n = 0 if (i == 1 and r == 1) else r + 1 + i
+            want += [16 * i + r] * n
+        assert a == want

@@ -166,7 +166,7 @@ def test_device_build_matches_host_build():
         L.mtg_device_free(d)
 
 
-@pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"},
+@pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_DUMMY_SORT": "lifted"},
                                  {"MTG_FUSED": "0"}, {"MTG_FUSED_EMIT": "0"}])
 def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
     # the unfused merge + emit, the compacting emit kernel, the unfused K1 and the LSD sorts
