@@ -63,8 +63,7 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
         P = P | shl(Key<L>::from(c), 2 * i);
         R = R | shl(Key<L>::from(3 - c), 2 * (K - 1 - i));
     }
-    uint64_t rid = 0;
-    if (KEYS && COUNTED && read_counts) rid = read_of(read_starts, n_reads, rid_at, p0);  // last start <= p0
+    uint64_t rid = ~0ull;  // the read of the thread's first valid window, searched when it comes
 #pragma unroll
     for (int j = 0; j < PPT; ++j) {
         const uint64_t p = p0 + j;
@@ -80,6 +79,7 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
                     if (COUNTED) {
                         uint32_t c = 1;
                         if (read_counts) {
+                            if (rid == ~0ull) rid = read_of(read_starts, n_reads, rid_at, p);  // last start <= p
                             while (rid + 1 < n_reads && read_starts[rid + 1] <= p) ++rid;
                             c = read_counts[rid];
                         }
@@ -599,11 +599,53 @@ __device__ __forceinline__ Key<LO> lift_fast(const Key<LI> &x, unsigned K) {
  * with char 1 cleared to $ (:165); level 1 + j is its j-fold to_prev(., $) (:286-303), in closed
  * form (node chars shifted up j places, label = the level-1 word's char K - j).
  */
-template <int L2, int L3>
+// ------------------------------------------------------------------ dummy keys as dense ranks
+//
+// Every dummy edge of the construction (sinks boss_chunk_construct.cpp:54-98, sources of every
+// level :123-168, 286-306), read from its most significant char down, is r_1 .. r_m $^(k-m) c: m
+// real node chars, the $ run of a source of level k - m, then the label c (real for a source; $ for
+// a sink, where m = k).  In the lifted order ($ < A < C < G < T) these strings are the leaves of a
+// trie whose subtree below d real chars holds T(k) = 1, T(d) = 4 + 4 T(d + 1) = (7 4^(k-d) - 4) / 3
+// strings (the 4 sources that stop there, then the A, C, G, T subtrees), so a dummy's rank among
+// all of them is
+//     4 m + sum_p r_p T(p) + (m < k ? c : 0)  =  4 m + (7 W - 4 S) / 3 + (m < k ? c : 0),
+// W = the real chars as a left-aligned 2-bit word (r_1 highest, 4^(k-p) for r_p), S = their sum.
+// The rank is an order-preserving injection into [0, T(0)), 62 bits at k = 30, so the dummy sort runs
+// on u64 keys (8 LSD passes) instead of the 3(k+1)-bit lifted keys (k = 30: 93 bits, 12 passes over
+// 16-byte keys).  Valid for k <= 30 (7 4^k < 2^64).  A key outside that shape raises *bad (the
+// caller then sorts the lifted keys).
+
+__host__ __device__ inline uint64_t dummy_rank_space(unsigned k) {  // T(0)
+    return (7ull * (1ull << (2 * k)) - 4) / 3;
+}
+
+// the lifted key as one 128-bit integer (k <= 30: 3 (k + 1) <= 93 bits)
+template <int L3>
+__device__ __forceinline__ unsigned __int128 lifted128(const Key<L3> &x) {
+    if constexpr (L3 == 1) return x.w[0];
+    else return ((unsigned __int128)x.w[1] << 64) | x.w[0];
+}
+
+// sum of the 2-bit chars of a word
+__device__ __forceinline__ uint64_t char_sum2(uint64_t w) {
+    return (uint64_t)__popcll(w & 0x5555555555555555ull) + 2ull * (uint64_t)__popcll(w & 0xAAAAAAAAAAAAAAAAull);
+}
+
+// rank of the dummy with m real node chars forming the 2-bit word W (r_1 highest, $ run below) and
+// label c (0..3; ignored for a sink, m = k)
+__device__ __forceinline__ uint64_t dummy_rank(uint64_t W, unsigned m, unsigned k, uint32_t c) {
+    return 4ull * m + (7 * W - 4 * char_sum2(W)) / 3 + (m < k ? (uint64_t)c : 0ull);
+}
+
+// RANKS (k <= 30): the dummies as their dense u64 ranks (dummy_rank, below) straight from the 2-bit
+// edge -- a sink's real chars are the edge's target node (x >> 2 with the label moved on top), a
+// level-l source's are the edge's first k - l node chars shifted up l places -- instead of lifted keys
+template <int L2, int L3, bool RANKS = false>
 __global__ __launch_bounds__(256) void dummy_write_kernel(
     const Key<L2> *__restrict__ keys, const uint8_t *__restrict__ flags,
     const uint8_t *__restrict__ in_flag, uint64_t n, unsigned K,
     const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out) {
+    uint64_t *rout = reinterpret_cast<uint64_t *>(out);
     __shared__ uint32_t s_scan[256 / 64 + 1];
     __shared__ uint16_t s_src[4096];  // tile-relative edge index of each source
     const uint32_t tid = threadIdx.x;
@@ -627,11 +669,22 @@ __global__ __launch_bounds__(256) void dummy_write_kernel(
             const Key<L2> x = keys[i0 + j];
             const Key<L2> t = (shr(x, 2) | shl(Key<L2>::from(x.w[0] & 3), 2 * (K - 1))) &
                               ~Key<L2>::from(3);
-            out[base + so++] = lift_fast<L3>(t, K) & ~Key<L3>::from(7);
+            if constexpr (RANKS) rout[base + so++] = dummy_rank(t.w[0] >> 2, k, k, 0);
+            else out[base + so++] = lift_fast<L3>(t, K) & ~Key<L3>::from(7);
         }
         if ((m >> (16 + j)) & 1u) s_src[qo++] = (uint16_t)(tid * 16 + j);
     }
     __syncthreads();
+    if constexpr (RANKS) {
+        uint64_t *o = rout + base + nsink;
+        for (uint32_t it = tid; it < nsrc * k; it += 256) {
+            const uint32_t q = it / k, lev = it - q * k + 1;  // level 1 .. k
+            const uint64_t node = keys[t0 + s_src[q]].w[0] >> 2;  // a_1 .. a_k, a_1 lowest
+            const uint64_t low = node & ((1ull << (2 * (k - lev))) - 1);  // a_1 .. a_(k - lev)
+            o[it] = dummy_rank(low << (2 * lev), k - lev, k, (uint32_t)(node >> (2 * (k - lev))) & 3u);
+        }
+        return;
+    }
     Key<L3> *o = out + base + nsink;
     for (uint32_t it = tid; it < nsrc * k; it += 256) {
         const uint32_t q = it / k, lev = it - q * k;
@@ -1178,49 +1231,28 @@ __global__ __launch_bounds__(256) void emit_kernel(
 }
 
 
-// ------------------------------------------------------------------ dummy keys as dense ranks
-//
-// Every dummy edge of the construction (sinks boss_chunk_construct.cpp:54-98, sources of every
-// level :123-168, 286-306), read from its most significant char down, is r_1 .. r_m $^(k-m) c: m
-// real node chars, the $ run of a source of level k - m, then the label c (real for a source; $ for
-// a sink, where m = k).  In the lifted order ($ < A < C < G < T) these strings are the leaves of a
-// trie whose subtree below d real chars holds T(k) = 1, T(d) = 4 + 4 T(d + 1) = (7 4^(k-d) - 4) / 3
-// strings (the 4 sources that stop there, then the A, C, G, T subtrees), so a dummy's rank among
-// all of them is
-//     4 m + sum_p r_p T(p) + (m < k ? c : 0)  =  4 m + (7 W - 4 S) / 3 + (m < k ? c : 0),
-// W = the real chars as a left-aligned 2-bit word (r_1 highest, 4^(k-p) for r_p), S = their sum.
-// The rank is an order-preserving injection into [0, T(0)), 62 bits at k = 30, so the dummy sort runs
-// on u64 keys (8 LSD passes) instead of the 3(k+1)-bit lifted keys (k = 30: 93 bits, 12 passes over
-// 16-byte keys).  Valid for k <= 30 (7 4^k < 2^64).  A key outside that shape raises *bad (the
-// caller then sorts the lifted keys).
-
-__host__ __device__ inline uint64_t dummy_rank_space(unsigned k) {  // T(0)
-    return (7ull * (1ull << (2 * k)) - 4) / 3;
-}
-
 template <int L3>
 __global__ void dummy_encode_kernel(const Key<L3> *__restrict__ in, uint64_t n, unsigned k,
                                     uint64_t *__restrict__ out, uint32_t *__restrict__ bad) {
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     bool err = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-        const Key<L3> x = in[i];
-        uint64_t W = 0, S = 0;
+        const unsigned __int128 v = lifted128(in[i]);
+        uint64_t W = 0;
         unsigned m = 0, top_dollar = 0;  // highest node position holding $
         for (unsigned j = 1; j <= k; ++j) {
-            const uint32_t v = char_at(x, j, 3);
-            if (v) {
-                W |= (uint64_t)(v - 1) << (2 * (j - 1));
-                S += v - 1;
+            const uint32_t ch = (uint32_t)(v >> (3 * j)) & 7u;
+            if (ch) {
+                W |= (uint64_t)(ch - 1) << (2 * (j - 1));
                 ++m;
             } else {
                 top_dollar = j;
             }
         }
-        const uint32_t c = char_at(x, 0, 3);
+        const uint32_t c = (uint32_t)v & 7u;
         // the $ run must be exactly node positions 1 .. k - m, the label real iff m < k
-        err |= top_dollar != k - m || (m < k) != (c != 0) || c > 4 || shr(x, 3 * (k + 1)) != Key<L3>::zero();
-        out[i] = 4ull * m + (7 * W - 4 * S) / 3 + (m < k ? (uint64_t)(c - 1) : 0ull);
+        err |= top_dollar != k - m || (m < k) != (c != 0) || c > 4 || (v >> (3 * (k + 1))) != 0;
+        out[i] = dummy_rank(W, m, k, c - 1);
     }
     if (err) atomicOr(bad, 1u);
 }
@@ -1231,19 +1263,24 @@ __global__ void dummy_decode_kernel(const uint64_t *__restrict__ in, uint64_t n,
     const uint64_t T0 = dummy_rank_space(k);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         uint64_t r = in[i], T = T0;
-        Key<L3> x = Key<L3>::zero();
+        unsigned __int128 x = 0;
         for (unsigned p = 1; p <= k; ++p) {
             if (r < 4) {  // a source of level k - (p - 1): its label
-                x = x | Key<L3>::from(r + 1);
+                x |= r + 1;
                 break;
             }
             r -= 4;
-            T = (T - 4) / 4;  // T(p): strings below one real char at depth p
+            T = (T - 4) >> 2;  // T(p): strings below one real char at depth p
             const uint64_t rp = (uint64_t)(r >= T) + (r >= 2 * T) + (r >= 3 * T);
             r -= rp * T;
-            x = x | shl(Key<L3>::from(rp + 1), 3 * (k - p + 1));  // r_p sits at node position k - p + 1
+            x |= (unsigned __int128)(rp + 1) << (3 * (k - p + 1));  // r_p sits at node position k - p + 1
         }
-        out[i] = x;  // all k node chars real: a sink (label $)
+        Key<L3> o;  // all k node chars real and no label: a sink ($)
+        o.w[0] = (uint64_t)x;
+        if constexpr (L3 > 1) o.w[1] = (uint64_t)(x >> 64);
+#pragma unroll
+        for (int q = 2; q < L3; ++q) o.w[q] = 0;
+        out[i] = o;
     }
 }
 

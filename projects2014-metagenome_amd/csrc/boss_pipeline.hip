@@ -588,9 +588,10 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 constexpr bool KC = decltype(keycas)::value;
                 constexpr int SL = decltype(sl)::value;
                 constexpr bool ND = decltype(nodup)::value;
-                local_unique_kernel<L, COUNTED, KC, 512, SL, ND><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
-                    *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt,
-                    COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax);
+                constexpr int WPE = (L == 1 && KC && !ND && !COUNTED) ? 8 : 1;
+                local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
+                    *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt, COUNTED ? *valt : nullptr,
+                    ucount, ovf, &c.small->counter, cmax);
             };
             using T_ = std::true_type;
             using F_ = std::false_type;
@@ -1147,6 +1148,39 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
 // value density of lifted chars and with a read-before-CAS hash for their repeated keys, measured
 // 24.5 vs 7.5 ms per cfg2 step and 24.9 vs 0.51 s per cfg3 step: groups of the $-padded source
 // levels overflow the LDS tables and fall back.)
+// the dense-rank dummy sort (boss_kernels.hpp: dummy_rank): `ranks` (u64 view of one of the two
+// Draw-key buffers xa / xb) sorted + deduplicated, the distinct ranks decoded to lifted keys in
+// whichever buffer does not hold them (both hold Draw lifted keys); returns D, *dk = the keys
+template <int L3>
+static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3> *xb, Key<1> *ranks, uint64_t Draw,
+                                        Key<L3> **dk) {
+    Key<1> *ra = ranks, *rb = (void *)ranks == (void *)xa ? (Key<1> *)xb : (Key<1> *)xa;
+    uint32_t *nv = nullptr;
+    const unsigned nbits = 64 - (unsigned)__builtin_clzll(dummy_rank_space(kb));
+    radix_sort<1, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
+    reset_small(c);
+    const uint64_t ut = ceil_div(Draw, 2048);
+    uint32_t udesc_ep;
+    uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
+    unique_kernel<1, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+        ra, nullptr, Draw, rb, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total, &c.small->error);
+    HIP_CHECK(hipGetLastError());
+    const uint64_t D = read_u64(c, &c.small->total);
+    Key<L3> *outk = (void *)rb == (void *)xa ? xb : xa;
+    dummy_decode_kernel<L3><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
+                              dim3(256), 0, c.stream>>>((const uint64_t *)rb, D, kb, outk);
+    HIP_CHECK(hipGetLastError());
+    *dk = outk;
+    return D;
+}
+
+// sort + unique of the lifted dummy keys da[0..Draw) (db is the ping-pong buffer); returns D and
+// leaves the distinct dummies in *dk.  For k <= 30 they are sorted as dense u64 ranks (8 LSD passes
+// of 8-byte keys instead of 12 of 16-byte ones); otherwise, or when a key is not of the dummy shape,
+// by an LSD sort of the lifted keys.  (An MSD sort of the dummies, planned for the 5-of-8 value
+// density of lifted chars and with a read-before-CAS hash for their repeated keys, measured 24.5 vs
+// 7.5 ms per cfg2 step and 24.9 vs 0.51 s per cfg3 step: groups of the $-padded source levels
+// overflow the LDS tables and fall back.)
 template <int L3>
 static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db, uint64_t Draw,
                                     Key<L3> **dk) {
@@ -1154,36 +1188,14 @@ static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db
     uint32_t *nv = nullptr;
     const unsigned kb = K - 1;
     if (c.dummy_ranks && kb >= 1 && kb <= 30 && Draw) {
-        // as dense u64 ranks (boss_kernels.hpp: dummy_encode_kernel): ranks in db's memory, the
-        // sort's ping-pong in da's once encoded, the distinct keys decoded into the other one
-        Key<1> *ra = (Key<1> *)db, *rb = (Key<1> *)da;
         HIP_CHECK(hipMemsetAsync(&c.small->bad_dummy, 0, 4, c.stream));
         const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(Draw, 256), 16384);
-        dummy_encode_kernel<L3><<<dim3(g), dim3(256), 0, c.stream>>>(da, Draw, kb, (uint64_t *)ra, &c.small->bad_dummy);
+        dummy_encode_kernel<L3><<<dim3(g), dim3(256), 0, c.stream>>>(da, Draw, kb, (uint64_t *)db, &c.small->bad_dummy);
         HIP_CHECK(hipGetLastError());
         uint32_t bad = 0;
         HIP_CHECK(hipMemcpyAsync(&bad, &c.small->bad_dummy, 4, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
-        if (!bad) {
-            const uint64_t space = dummy_rank_space(kb);
-            const unsigned nbits = 64 - (unsigned)__builtin_clzll(space);
-            radix_sort<1, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
-            reset_small(c);
-            const uint64_t ut = ceil_div(Draw, 2048);
-            uint32_t udesc_ep;
-            uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
-            unique_kernel<1, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
-                ra, nullptr, Draw, rb, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total, &c.small->error);
-            HIP_CHECK(hipGetLastError());
-            D = read_u64(c, &c.small->total);
-            // the distinct ranks are in rb's memory: decode into the other buffer
-            Key<L3> *outk = (void *)rb == (void *)da ? db : da;
-            dummy_decode_kernel<L3><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
-                                      dim3(256), 0, c.stream>>>((const uint64_t *)rb, D, kb, outk);
-            HIP_CHECK(hipGetLastError());
-            *dk = outk;
-            return D;
-        }
+        if (!bad) return sort_unique_dummy_ranks<L3>(c, kb, da, db, (Key<1> *)db, Draw, dk);
         if (c.debug) fprintf(stderr, "[mtg debug] dummy keys outside the rank shape: lifted sort\n");
     }
     {
@@ -1252,6 +1264,14 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
     if (!Draw) return 0;
     K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
     K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
+    if constexpr (L2 == 1) {
+        if (c.dummy_ranks && k <= 30) {  // written as dense ranks: no lifted keys until the decode
+            dummy_write_kernel<L2, L3, true><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(ka, flags, in_flag,
+                                                                                                  R, K, toff, da);
+            HIP_CHECK(hipGetLastError());
+            return sort_unique_dummy_ranks<L3>(c, k, da, db, (Key<1> *)da, Draw, dk);
+        }
+    }
     dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(ka, flags, in_flag, R, K,
                                                                                     toff, da);
     HIP_CHECK(hipGetLastError());

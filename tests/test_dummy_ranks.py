@@ -74,3 +74,33 @@ def test_rank_fits_u64_up_to_k30():
     assert space(30) < 2 ** 64 and 7 * 4 ** 30 < 2 ** 64
     assert (space(30)).bit_length() == 62  # 8 LSD passes of 8 bits
     assert 7 * 4 ** 31 >= 2 ** 64  # k = 31 would overflow: the lifted sort takes over
+
+
+def char_sum2(w):
+    return sum((w >> (2 * i)) & 3 for i in range(32))
+
+
+def rank_direct(W, m, k, c):
+    return 4 * m + (7 * W - 4 * char_sum2(W)) // 3 + (c if m < k else 0)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 12, 30])
+def test_ranks_straight_from_the_edge(k):
+    # dummy_write_kernel<RANKS>: a sink's and every source level's rank from the 2-bit edge x
+    # (node a_1..a_k at bits 2i, label a_K in the low bits) equal the rank of the lifted dummy the
+    # reference builds (to_next + $ label, :54-98; to_prev + $ in char 1 and its levels, :123-168)
+    import random
+    rnd = random.Random(k)
+    K = k + 1
+    for _ in range(200):
+        a = [rnd.randrange(4) for _ in range(K)]  # a[0] = a_1 ... a[K-1] = a_K
+        node = sum(a[i] << (2 * i) for i in range(k))
+        # sink: node a_2 .. a_K, label $
+        sink = lifted([v + 1 for v in reversed(a[1:K])], 0, k)
+        assert encode(sink, k) == rank_direct(sum(a[i + 1] << (2 * i) for i in range(k)), k, k, 0)
+        for lev in range(1, k + 1):
+            # level lev: node $^lev a_1 .. a_(k-lev) (a_1 at position lev + 1), label a_(k-lev+1)
+            top_down = [v + 1 for v in reversed(a[:k - lev])] + [0] * lev
+            src = lifted(top_down, a[k - lev] + 1, k)
+            low = node & ((1 << (2 * (k - lev))) - 1)
+            assert encode(src, k) == rank_direct(low << (2 * lev), k - lev, k, (node >> (2 * (k - lev))) & 3)
