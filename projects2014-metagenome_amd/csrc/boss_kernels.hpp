@@ -413,8 +413,7 @@ struct DummyTraits {
     static constexpr int BLOCK = 256;
     static constexpr int PER = L == 1 ? 4 : 2;   // consecutive edges per thread
     static constexpr int TILE = BLOCK * PER;
-    static constexpr int CAP = 2 * TILE;         // staged real edges (the 4 sink ranges)
-    static constexpr int BCAP = TILE;            // staged bucket starts
+    static constexpr int CAP = TILE * 5 / 4;     // staged real edges (the 4 sink ranges hold ~TILE)
     static constexpr int WTILE = 4096;           // edges per tile of the count / write passes
 };
 
@@ -433,8 +432,11 @@ struct DummyTraits {
  * This is the GPU form of the reference's per-character merge iterators.  A workgroup takes
  * TILE consecutive edges, PER consecutive ones per thread.  The sink probes of label c are
  * sorted (to_next is monotone on the edges of one label), so all edges they can hit lie in one
- * contiguous key range.  The 4 ranges and their slices of the bucket index are staged in LDS;
- * a probe reads its bucket's slice bounds from LDS and binary-searches the bucket (a few keys).
+ * contiguous key range, found from the bucket index.  The 4 ranges (about TILE edges together)
+ * are staged in LDS and every probe binary-searches its range there.  The kernel is bound by the
+ * edges in flight per CU, which LDS caps: 10 bytes per edge (CAP = 1.25 TILE keys, no staged
+ * bucket slices) instead of 20 (2 TILE keys + a bucket-start slice): 2.66 -> 2.21 ms at configs[1]
+ * (8 edges per thread instead of 4: 2.59 ms).
  * A range that does not fit falls back to bucketed searches in global memory.
  */
 template <int L>
@@ -444,9 +446,8 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     using T = DummyTraits<L>;
     constexpr int PER = T::PER;
     __shared__ Key<L> s_r[T::CAP];
-    __shared__ uint32_t s_b[T::BCAP];
-    __shared__ uint64_t s_lo[4], s_blo[4];
-    __shared__ uint32_t s_cnt[4], s_nb[4], s_off[4], s_boff[4];
+    __shared__ uint64_t s_lo[4];
+    __shared__ uint32_t s_cnt[4], s_off[4];
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * T::TILE;
     const uint32_t tn = (uint32_t)min((uint64_t)T::TILE, n - base);
@@ -460,9 +461,7 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         const uint64_t blo = bits_at(shr(lo, bshift), 0, 32), bhi = bits_at(shr(hi, bshift), 0, 32);
         const uint64_t a = start[blo], b = start[bhi + 1];
         s_lo[tid] = a;
-        s_blo[tid] = blo;
         s_cnt[tid] = (uint32_t)min(b - a, (uint64_t)0xFFFFFFFFu);
-        s_nb[tid] = (uint32_t)min(bhi - blo + 2, (uint64_t)0xFFFFFFFFu);
     }
     const uint32_t j0 = tid * PER;
     Key<L> x[PER];
@@ -481,15 +480,12 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     }
     __syncthreads();
     if (tid == 0) {
-        uint32_t cum = 0, bcum = 0;
+        uint32_t cum = 0;
         for (int c = 0; c < 4; ++c) {
             s_off[c] = ~0u;  // ~0 = global fallback
-            if ((uint64_t)cum + s_cnt[c] <= (uint64_t)T::CAP &&
-                (uint64_t)bcum + s_nb[c] <= (uint64_t)T::BCAP) {
+            if ((uint64_t)cum + s_cnt[c] <= (uint64_t)T::CAP) {
                 s_off[c] = cum;
-                s_boff[c] = bcum;
                 cum += s_cnt[c];
-                bcum += s_nb[c];
             }
         }
     }
@@ -498,9 +494,8 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     for (int c = 0; c < 4; ++c) {
         if (s_off[c] == ~0u) continue;
         const uint64_t a = s_lo[c];
-        const uint32_t off = s_off[c], boff = s_boff[c];
+        const uint32_t off = s_off[c];
         for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = keys[a + j];
-        for (uint32_t j = tid; j < s_nb[c]; j += 256) s_b[boff + j] = (uint32_t)(start[s_blo[c] + j] - a);
     }
     __syncthreads();
 #pragma unroll
@@ -512,13 +507,13 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         uint64_t hit = ~0ull;
         const uint32_t off = s_off[c];
         if (off != ~0u) {
-            const uint32_t bo = s_boff[c] + (uint32_t)(bits_at(shr(p, bshift), 0, 32) - s_blo[c]);
-            uint32_t lo = s_b[bo], hi = s_b[bo + 1];
+            const uint32_t cnt = s_cnt[c];
+            uint32_t lo = 0, hi = cnt;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
                 if (s_r[off + mid] < p) lo = mid + 1; else hi = mid;
             }
-            if (lo < s_cnt[c] && shr(s_r[off + lo], 2) == shr(p, 2)) hit = s_lo[c] + lo;
+            if (lo < cnt && shr(s_r[off + lo], 2) == shr(p, 2)) hit = s_lo[c] + lo;
         } else {
             const uint64_t i = lower_bound_bucketed(keys, start, bshift, p);
             if (i < n && shr(keys[i], 2) == shr(p, 2)) hit = i;

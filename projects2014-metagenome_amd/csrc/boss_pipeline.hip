@@ -385,7 +385,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
                                 double dup, const uint32_t *hist1 = nullptr, bool distinct = false,
                                 const std::vector<uint64_t> *runs = nullptr, bool level1_done = false,
-                                RcMerge<L> *rm = nullptr) {
+                                RcMerge<L> *rm = nullptr, const MsdPlan *force_plan = nullptr) {
     // level1_done: the producer already scattered the keys by the plan's level-1 digit
     // (extract_partition_kernel); hist1 holds that level's counts
     // hist1: counts of the top plan.digit_end[1] bits of the input, when its producer made them;
@@ -396,7 +396,8 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
     constexpr int TILE = MsdTraits<L>::TILE;
     const uint64_t tiles = ceil_div(n, TILE);
-    const MsdPlan plan = msd_plan<L>(c, n, nbits, dup);
+    // force_plan: the caller fixed the digits (the routed multi-GPU collect: level 1 is the routing digit)
+    const MsdPlan plan = force_plan ? *force_plan : msd_plan<L>(c, n, nbits, dup);
     unsigned levels = plan.levels;
     unsigned digit_end[4] = {plan.digit_end[0], plan.digit_end[1], plan.digit_end[2], plan.digit_end[3]};
     unsigned b = 0;
@@ -1895,6 +1896,193 @@ static uint64_t collect_ranges_dist(Ctx &c, Dist &d, unsigned K, bool canonical,
     return off;
 }
 
+// ------------------------------------------ multi-GPU: the extraction routed straight to the owners
+//
+// The single build's fused K1 (extract_partition.hpp) already scatters every rank's k-mers by the
+// top 9 bits of their key.  With the owner ranges drawn at 4-char (8-bit) boundaries -- unions of
+// those buckets, balanced on the global histogram of pass A -- every owner's keys are one contiguous
+// slice of the rank's scattered array: they go to the owner as extracted (exchange 1 moves every
+// k-mer occurrence once), and the owner runs the single build's level-2 partition + LDS unique over
+// the P received runs (the partition reads its input in any order), so each k-mer is sorted exactly
+// once in the whole job.  The earlier design sorted and deduplicated each rank's k-mers locally,
+// exchanged the distinct runs and deduplicated them again at the owner: at 1.25x local coverage
+// (8 GPUs) the local dedupe keeps ~2/3 of the k-mers, so nearly every k-mer was sorted twice
+// (DESIGN.md section 8).  Returns false when the fused extraction does not apply (the caller runs
+// the local-collect path).
+template <bool COUNTED>
+static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                                Key<1> **xa_out, uint32_t **xac_out, uint64_t *U_out, std::vector<uint64_t> *bounds,
+                                Tracer &tr, EventTimer &tm, int *ev_extract, int *ev_sort) {
+    using K2 = Key<1>;
+    // the same on every rank (no input-size test: a rank may hold no reads)
+    if (!c.fused || c.use_lsd || K - 1 < FUSED_HB / 2 || K > 32 || c.force_ranges) return false;
+    constexpr unsigned OB = 8;   // owner-range prefix bits (4 node chars: whole chars for the lifted bounds)
+    constexpr unsigned B1 = 9;   // pass B's scatter digit
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    c.timings.n_positions = npos;
+    constexpr int TILE = ExtractTraits<1>::TILE;
+    const uint64_t tiles = ceil_div(npos, TILE);
+    const int fbk = 512;
+    const uint32_t rps = (uint32_t)(16 * fbk / TILE);
+    uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
+    if (nrows >= rps) nrows -= nrows % rps;
+    constexpr uint32_t NBH = 1u << FUSED_HB;
+    // pass A: per-row histograms of the canonical keys' top 12 bits (and of the other strand's)
+    uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, std::max<uint64_t>((uint64_t)nrows * NBH, 1) * 4);
+    uint32_t *rows_o = (uint32_t *)c.ws.get(Workspace::RC_COMB, std::max<uint64_t>((uint64_t)nrows * NBH, 1) * 4);
+    uint64_t *hg = (uint64_t *)c.ws.get(Workspace::XHIST, 2 * NBH * 8);
+    HIP_CHECK(hipMemsetAsync(hg, 0, 2 * NBH * 8, c.stream));
+    const uint64_t tiles_b = ceil_div(npos, (uint64_t)16 * fbk);
+    const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
+    const uint64_t per_stripe = std::max<uint64_t>(1, ceil_div(tiles_b, stripes));
+    const uint64_t per_row = stripes == 1 && nrows ? ceil_div(tiles_b * rps, nrows) : per_stripe;
+    uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, 2 * NBH * 4);
+    HIP_CHECK(hipMemsetAsync(h12, 0, 2 * NBH * 4, c.stream));
+    if (nrows) {
+        extract_hist_fast_kernel<true><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                             tiles, per_row, rows, rows_o);
+        HIP_CHECK(hipGetLastError());
+        hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(NBH, 256)), dim3(256), 0,
+                                  c.stream>>>(rows, nrows, NBH, h12);
+        HIP_CHECK(hipGetLastError());
+        hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(NBH, 256)), dim3(256), 0,
+                                  c.stream>>>(rows_o, nrows, NBH, h12 + NBH);
+        HIP_CHECK(hipGetLastError());
+    }
+    std::vector<uint32_t> hl(2 * NBH);
+    HIP_CHECK(hipMemcpyAsync(hl.data(), h12, 2 * NBH * 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<uint64_t> hloc(2 * NBH);
+    for (uint32_t i = 0; i < 2 * NBH; ++i) hloc[i] = hl[i];
+    HIP_CHECK(hipMemcpyAsync(hg, hloc.data(), 2 * NBH * 8, hipMemcpyHostToDevice, c.stream));
+    const int e0 = d.tm->mark();
+    d.comm.allreduce_sum_u64(hg, 2 * NBH, c.stream);
+    d.xev.push_back({e0, d.tm->mark()});
+    std::vector<uint64_t> H(2 * NBH);
+    HIP_CHECK(hipMemcpyAsync(H.data(), hg, 2 * NBH * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // hloc is a host local
+    uint64_t N = 0, Nall = 0;
+    for (uint32_t i = 0; i < NBH; ++i) {
+        N += hl[i];
+        Nall += H[i];
+    }
+    // owner ranges over the 256 4-char prefixes, balanced on the build's work: the collect and the rc
+    // stage follow the canonical k-mers (2/3 of a step), the dummy and emit stages the real edges,
+    // i.e. both strands (canonical mode; basic mode: the k-mers themselves)
+    constexpr uint32_t NOB = 1u << OB;
+    std::vector<uint64_t> wgt(NOB, 0);
+    {
+        uint64_t tc = 0, tr2 = 0;
+        for (uint32_t i = 0; i < NBH; ++i) {
+            tc += H[i];
+            tr2 += H[i] + (canonical ? H[NBH + i] : H[i]);
+        }
+        for (uint32_t i = 0; i < NBH; ++i) {
+            const double wc = tc ? (double)H[i] / (double)tc : 0.0;
+            const double wr = tr2 ? (double)(H[i] + (canonical ? H[NBH + i] : H[i])) / (double)tr2 : 0.0;
+            wgt[i >> (FUSED_HB - OB)] += (uint64_t)((2.0 * wc + wr) * 1e12);
+        }
+    }
+    *bounds = balanced_bounds(wgt.data(), NOB, d.P);
+    d.m = OB / 2;
+    d.shift2 = 2 * K - OB;
+    d.nb = NOB;
+    tr("route plan", N, Nall);
+    // pass B: this rank's k-mers scattered by their top B1 bits (the single build's fused pass)
+    const uint32_t nb1 = 1u << B1;
+    std::vector<uint32_t> h1(nb1, 0);
+    for (uint32_t i = 0; i < NBH; ++i) h1[i >> (FUSED_HB - B1)] += hl[i];
+    std::vector<unsigned long long> cur(2 * nb1);
+    unsigned long long acc = 0;
+    for (uint32_t i = 0; i < nb1; ++i) {
+        cur[i] = acc;
+        acc += h1[i];
+    }
+    for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
+    K2 *ka = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(N, 1) * 8);
+    uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
+    if (nrows) {
+        unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
+        HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
+        auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
+        unsigned long long *send = scur + (size_t)stripes * nb1;
+        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, FUSED_HB, B1, stripes, rps, dcur, scur,
+                                                                     send);
+        HIP_CHECK(hipGetLastError());
+        if (!COUNTED) {
+            extract_partition_fast_kernel<512><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), 0,
+                                                  c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, B1, per_stripe,
+                                                              scur, send, ka, &c.small->error);
+        } else {
+            const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
+            extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
+                B1, per_stripe, scur, send, ka, ca, &c.small->error);
+        }
+        HIP_CHECK(hipGetLastError());
+        cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
+            scur, send, stripes * nb1, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // cur is a host local
+    }
+    c.timings.n_extracted = N;
+    *ev_extract = tm.mark();
+    tr("extract + scatter", N);
+    // exchange 1: owner o gets the rank's buckets of its prefixes [bounds[o], bounds[o + 1])
+    std::vector<std::vector<uint64_t>> soff(1, std::vector<uint64_t>(d.P + 1));
+    for (int j = 0; j <= d.P; ++j) {
+        const uint64_t b = (*bounds)[j] << (B1 - OB);  // first level-1 bucket of the prefix
+        soff[0][j] = b >= nb1 ? N : cur[b];
+    }
+    K2 *xa;
+    uint32_t *xac = nullptr;
+    const K2 *arrs[1] = {ka};
+    const uint32_t *cnts[1] = {ca};
+    const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA, Workspace::XAC,
+                                          &xa, &xac);
+    tr("exchange 1", n1);
+    // the owner's level-1 counts: the global pass-A histogram over its buckets
+    const uint64_t ob0 = (*bounds)[d.me] << (B1 - OB), ob1 = std::min<uint64_t>((*bounds)[d.me + 1] << (B1 - OB), nb1);
+    std::vector<uint32_t> hown(nb1, 0);
+    uint64_t nown = 0;
+    for (uint32_t i = 0; i < NBH; ++i) {
+        const uint32_t b = i >> (FUSED_HB - B1);
+        if (b >= ob0 && b < ob1) {
+            hown[b] += (uint32_t)H[i];
+            nown += H[i];
+        }
+    }
+    if (nown != n1) throw std::runtime_error("received k-mers differ from the global histogram of the owned range");
+    uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
+    HIP_CHECK(hipMemcpyAsync(dh1, hown.data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
+    // plan: the keys fill (ob1 - ob0) of the nb1 level-1 buckets; level 1 is "done" (the buckets are
+    // known from the histogram), level 2 partitions the P runs in one pass (any input order)
+    uint64_t U = 0;
+    if (n1) {
+        K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
+        uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
+        const double spread = (double)nb1 / (double)std::max<uint64_t>(1, ob1 - ob0);
+        const double dup = estimate_dup<1>(c, xa, n1, 8.0) / spread;
+        MsdPlan plan = msd_plan<1>(c, n1, 2 * K, dup);
+        unsigned T = plan.levels ? plan.digit_end[plan.levels] : 0;
+        T = std::min(2 * K, std::max(T, B1 + 1));  // at least one partition pass after the routing digit
+        MsdPlan fp{};
+        fp.levels = 1 + (T - B1 + MSD_DBITS - 1) / MSD_DBITS;
+        fp.digit_end[1] = B1;
+        for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
+        c.track_partition = true;
+        U = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup, dh1, false, nullptr, true,
+                                        nullptr, &fp);
+        c.track_partition = false;
+    }
+    *ev_sort = tm.mark();
+    tr("owner sort", U);
+    *xa_out = xa;
+    *xac_out = xac;
+    *U_out = U;
+    return true;
+}
+
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, unsigned bits,
                               const BuildInput &in, BuildOutput *out) {
@@ -1938,6 +2126,14 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         ev_sort = ev_unique = tm.mark();
         T.n_unique = R;
     } else {
+        K2 *xa = nullptr;
+        uint32_t *xac = nullptr;
+        std::vector<uint64_t> b1;
+        bool routed = false;
+        if constexpr (L2 == 1)  // the fused extraction routes every k-mer to its owner
+            routed = dist_collect_routed<COUNTED>(c, d, K, canonical, cmax, in, &xa, &xac, &T.n_unique, &b1, tr, tm,
+                                                  &ev_extract, &ev_sort);
+        if (!routed) {
         // ---- K1-K3 on this rank's reads
         K2 *ka, *kb;
         uint32_t *ca, *cb;
@@ -1954,7 +2150,6 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
 
         // ---- exchange 1: the distinct k-mers by range of their own prefix, merged at the owner
         std::vector<std::vector<uint64_t>> soff;
-        std::vector<uint64_t> b1;
         {
             // canonical mode: the ranges balance both strands (the canonical keys and their rc keys)
             // and are final, so exchange 2 moves only the rc keys
@@ -1963,8 +2158,6 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
             b1 = dist_ranges<L2>(c, d, 1, arrs, ns, &soff, canonical ? K : 0);
         }
         tr("ranges 1");
-        K2 *xa;
-        uint32_t *xac = nullptr;
         {
             const K2 *arrs[1] = {ka};
             const uint32_t *cnts[1] = {ca};
@@ -1984,6 +2177,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
                 T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
                                                           false, &runs);
             }
+        }
         }
         const uint64_t U = T.n_unique;
         tr("owner dedupe", U);

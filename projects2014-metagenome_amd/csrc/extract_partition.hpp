@@ -87,17 +87,26 @@ __device__ __forceinline__ uint32_t rc_word(uint32_t w) {
 // validity a field of the invalid-char mask (round 2: 1.85 -> ~1.2 ms, VALU-bound before).
 // Row r counts the per_row consecutive tiles [r * per_row, (r + 1) * per_row): rps consecutive rows
 // then cover one stripe of pass B's tiles (stripe_cursor_kernel).
+// OTHER (the multi-GPU build): also rows_other, the histogram of the top bits of the other strand's
+// key of every canonical window (its reverse complement: max(fwd, rc)), so the owner ranges can be
+// balanced on the real edges (both strands) as well as on the canonical k-mers.
+template <bool OTHER = false>
 __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
                                                                 unsigned K, int canonical, uint64_t ntiles,
-                                                                uint64_t per_row, uint32_t *__restrict__ rows) {
+                                                                uint64_t per_row, uint32_t *__restrict__ rows,
+                                                                uint32_t *__restrict__ rows_other = nullptr) {
     constexpr int BLOCK = 256, PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;
     constexpr uint32_t NB = 1u << FUSED_HB;
     static_assert(FUSED_HB == 12, "6-char tops");
     __shared__ uint32_t s_pack[NW];
     __shared__ uint32_t s_inv[NW];
     __shared__ uint32_t s_h[NB];
+    __shared__ uint32_t s_o[OTHER ? NB : 1];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
+    for (uint32_t i = tid; i < NB; i += BLOCK) {
+        s_h[i] = 0;
+        if (OTHER) s_o[i] = 0;
+    }
     const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
     const uint64_t maskK = (1ull << K) - 1;
     const unsigned fs = 2 * (K - 7);  // K >= 7 (callers check K - 1 >= 6)
@@ -151,11 +160,17 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
             const int sr = 2 * (41 - j);  // 52 .. 82
             const uint32_t r = (sr >= 64 ? (q2 >> (sr - 64)) : __builtin_amdgcn_alignbit(q2, q1, sr - 32)) & (NB - 1);
             const bool ok = (uint32_t)j < nwin && ((inv >> j) & maskK) == 0;
-            if (ok) atomicAdd(&s_h[canonical && r < f ? r : f], 1u);
+            if (ok) {
+                atomicAdd(&s_h[canonical && r < f ? r : f], 1u);
+                if (OTHER) atomicAdd(&s_o[canonical && r < f ? f : r], 1u);
+            }
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < NB; i += BLOCK) rows[(uint64_t)blockIdx.x * NB + i] = s_h[i];
+    for (uint32_t i = tid; i < NB; i += BLOCK) {
+        rows[(uint64_t)blockIdx.x * NB + i] = s_h[i];
+        if (OTHER) rows_other[(uint64_t)blockIdx.x * NB + i] = s_o[i];
+    }
 }
 
 template <bool COUNTED, int BLOCK_ = COUNTED ? 512 : 1024>
