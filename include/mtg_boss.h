@@ -71,10 +71,11 @@ typedef struct mtg_boss_params {
     double memory_preallocated;  /* bytes of device memory the build may use (0 = all free HBM);
                                     larger inputs are built in key-range batches */
     int container_type;          /* MTG_CONTAINER_VECTOR, or MTG_CONTAINER_VECTOR_DISK (--disk-swap):
-                                    the bounded-memory build, in key-range batches (nothing spills:
-                                    the real edges stay in HBM) */
-    const char *swap_dir;        /* unused: no spill files */
-    uint64_t disk_cap_bytes;     /* unused: no spill files */
+                                    the bounded-memory build, in key-range batches; when even the real
+                                    edges would not fit memory_preallocated, build_chunk spills: one
+                                    range's edges in HBM at a time, the rest in host memory / swap_dir */
+    const char *swap_dir;        /* the disk container's spill files go here (copied at create) */
+    uint64_t disk_cap_bytes;     /* at most this many bytes of spill files; further blocks stay in RAM */
     int device_id;               /* HIP device ordinal */
 } mtg_boss_params;
 
@@ -138,6 +139,7 @@ typedef struct mtg_boss_timings {
     uint64_t n_batches;          /* key-range batches of the build (1 = the input fit at once) */
     uint64_t peak_bytes;         /* device workspace held at the end of the build */
     double input_ms;             /* host-buffer builds: KMC decode + FASTA split on the device (incl. their copies) */
+    uint64_t spilled_bytes;      /* bytes the build kept outside HBM (the disk container's spill; 0 = none) */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);
@@ -239,6 +241,13 @@ int mtg_comm_create_local(int world, mtg_comm **comms /* world entries */);
 void mtg_comm_destroy(mtg_comm *comm);
 int mtg_comm_rank(const mtg_comm *comm);
 int mtg_comm_size(const mtg_comm *comm);
+/*
+ * Local groups created with MTG_LOCAL_SERIAL=1 in the environment hand the device to one rank at a
+ * time (from build start to its next exchange, and between exchanges): a step's wall time is then
+ * the sum of the ranks' work.  Returns this rank's accumulated device time in ms (reset != 0 zeroes
+ * it), -1 for other communicators.  A measurement aid (tools/dist_sim.py), not a build mode.
+ */
+double mtg_comm_local_held_ms(mtg_comm *comm, int reset);
 
 /*
  * The same exchange over caller-supplied functions on HOST buffers (each returns 0 on success): the

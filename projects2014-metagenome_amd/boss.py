@@ -85,7 +85,7 @@ class Timings(ctypes.Structure):
                [(name, ctypes.c_double) for name in
                 ("stage_ms", "h2d_ms", "d2h_ms", "host_total_ms")] + \
                [("n_batches", ctypes.c_uint64), ("peak_bytes", ctypes.c_uint64),
-                ("input_ms", ctypes.c_double)]
+                ("input_ms", ctypes.c_double), ("spilled_bytes", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -104,7 +104,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free",
            "mtg_boss_ctor_add_fasta", "mtg_device_copy", "mtg_kmc_load_device",
            "mtg_device_reads_free", "mtg_kmc_write_device", "mtg_host_pool_bytes",
-           "mtg_host_pool_trim", "mtg_comm_create_callbacks")
+           "mtg_host_pool_trim", "mtg_comm_create_callbacks", "mtg_comm_local_held_ms")
 
 COMM_ID_BYTES = 128
 
@@ -156,6 +156,8 @@ def lib():
         L.mtg_comm_destroy.argtypes = [ctypes.c_void_p]
         L.mtg_comm_rank.argtypes = [ctypes.c_void_p]
         L.mtg_comm_size.argtypes = [ctypes.c_void_p]
+        L.mtg_comm_local_held_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.mtg_comm_local_held_ms.restype = ctypes.c_double
         L.mtg_boss_ctor_build_chunk_dist.argtypes = [ctypes.c_void_p, ctypes.c_void_p, P(_Chunk)]
         L.mtg_boss_build_device_dist.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_uint64, ctypes.c_void_p,
@@ -513,6 +515,10 @@ class Comm:
     @property
     def size(self):
         return lib().mtg_comm_size(self.handle)
+
+    def held_ms(self, reset=False):
+        """Serial local groups (MTG_LOCAL_SERIAL=1): this rank's device time in ms; -1 otherwise."""
+        return lib().mtg_comm_local_held_ms(self.handle, 1 if reset else 0)
 
     @staticmethod
     def unique_id():

@@ -20,6 +20,9 @@
 #include <type_traits>
 #include <vector>
 
+#include <sys/types.h>
+#include <unistd.h>
+
 #include "../../include/mtg_boss.h"
 #include "boss_kernels.hpp"
 #include "comm.hpp"
@@ -58,7 +61,7 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -104,6 +107,7 @@ struct Small {  // one device word block, zeroed per use
     uint32_t skip;
     uint32_t root_same;
     uint32_t bad_dummy;
+    uint32_t bruns;  // bucket_index: listed long runs
     uint32_t error;
 };
 
@@ -152,6 +156,13 @@ struct Ctx {
     uint32_t force_ranges = 0;     // MTG_RANGES=P: collect in P key ranges (tests; else planned from memory)
     double mem_budget = 0;         // memory_preallocated (bytes; 0 = free HBM)
     bool disk = false;             // MTG_CONTAINER_VECTOR_DISK: the bounded-memory (range-batched) build
+    bool host_output = false;      // the build's arrays go to the host (build_chunk): it may spill
+    bool force_spill = false;      // MTG_SPILL=1: spill whenever the build runs in key ranges (tests)
+    std::string swap_dir;          // spill files of the disk container (swap_dir of initialize)
+    uint64_t disk_cap = 0;         // at most this many bytes of spill files (disk_cap_bytes); the rest in RAM
+    std::vector<uint8_t> spill_W, spill_last;  // the spilled build's output rows (host)
+    std::vector<uint32_t> spill_weights;
+    uint64_t spilled_bytes = 0;    // bytes the last build kept outside HBM
     uint32_t hist_rows = 2048;     // MTG_HIST_ROWS: workgroups of the fused K1 histogram pass (tests
                                    // lower it so the grid-stride + prefetch loop runs on small inputs)
     double fused_ms = 0;           // device time of the last fused extract+partition launch
@@ -181,6 +192,7 @@ static void load_knobs(Ctx &c) {
     c.fused = !is("MTG_FUSED", "0");
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
+    c.force_spill = is("MTG_SPILL", "1");
     c.debug = getenv("MTG_DEBUG") != nullptr;
     c.trace = getenv("MTG_TRACE") != nullptr;
     if (const char *e = getenv("MTG_FUSED_MIN")) c.fused_min = strtoull(e, nullptr, 10);
@@ -222,6 +234,21 @@ static uint64_t *acquire_desc(Ctx &c, uint64_t words, uint32_t *epoch) {
     }
     *epoch = ++c.epoch;
     return d;
+}
+
+// bucket index of a sorted key array (boss_kernels.hpp: bucket_index_kernel + the grid-wide fill of
+// its long empty runs)
+constexpr uint32_t kBucketRuns = 4096;
+template <int L>
+static void bucket_index(Ctx &c, const Key<L> *keys, uint64_t n, unsigned shift, uint64_t nb, uint64_t *start) {
+    uint64_t *runs = (uint64_t *)c.ws.get(Workspace::BRUNS, kBucketRuns * 24);
+    HIP_CHECK(hipMemsetAsync(&c.small->bruns, 0, 4, c.stream));
+    const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n + 1, 256), 8192));
+    bucket_index_kernel<L><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(keys, n, shift, nb, start, runs,
+                                                                         &c.small->bruns, kBucketRuns);
+    HIP_CHECK(hipGetLastError());
+    bucket_fill_kernel<<<dim3(1024), dim3(256), 0, c.stream>>>(runs, &c.small->bruns, kBucketRuns, start);
+    HIP_CHECK(hipGetLastError());
 }
 
 // LSD radix sort of keys[0..n) (and vals) over the low nbits; result left in *keys / *vals
@@ -467,10 +494,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         int64_t *delta = (int64_t *)c.ws.get(Workspace::RUN_DELTA, (uint64_t)P * nbuckets * 8);
         for (uint32_t j = 0; j < P; ++j) {
             const uint64_t r0 = (*runs)[j], rn = (*runs)[j + 1] - r0;
-            const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(rn + 1, 256), 8192));
-            bucket_index_kernel<L><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(
-                *keys + r0, rn, nbits - T, nbuckets, idx + (uint64_t)j * (nbuckets + 1));
-            HIP_CHECK(hipGetLastError());
+            bucket_index<L>(c, *keys + r0, rn, nbits - T, nbuckets, idx + (uint64_t)j * (nbuckets + 1));
         }
         bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nbuckets + 1) * 8);
         runs_delta_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(nbuckets + 1, 256), 16384)), dim3(256), 0,
@@ -508,10 +532,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 // fused rc merge: the canonical keys of every bucket (bucket index of the sorted
                 // set), and groups sized by rc + canonical keys together
                 cstart = (uint64_t *)c.ws.get(Workspace::RC_CSTART, (nbuckets + 2) * 8);
-                const uint64_t gi = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(rm->nc + 1, 256), 8192));
-                bucket_index_kernel<L><<<dim3((unsigned)gi), dim3(256), 0, c.stream>>>(rm->ck, rm->nc, nbits - b,
-                                                                                       nbuckets, cstart);
-                HIP_CHECK(hipGetLastError());
+                bucket_index<L>(c, rm->ck, rm->nc, nbits - b, nbuckets, cstart);
                 uint64_t *comb = (uint64_t *)c.ws.get(Workspace::RC_COMB, (nbuckets + 1) * 8);
                 add_starts_kernel<<<dim3((unsigned)ceil_div(nbuckets + 1, 256)), dim3(256), 0, c.stream>>>(
                     bstart, cstart, nbuckets + 1, comb);
@@ -722,6 +743,7 @@ struct BuildOutput {
     uint64_t F[5];
     uint64_t n_real;
     uint64_t n_dummy;
+    bool host = false;  // the spilled build (run_pipeline_spill): W / last / weights are host arrays
 };
 
 // MTG_DEBUG=1: host-side check that a device key array is strictly increasing
@@ -1404,6 +1426,12 @@ static void emit_stream(Ctx &c, unsigned k, uint32_t wmax, const Key<L3> *sk, co
     out->n_dummy = rows - R;
 }
 
+template <int L2, bool COUNTED>
+static bool want_spill(Ctx &c, unsigned K, bool canonical, const BuildInput &in, uint32_t P);
+template <int L2, int L3, bool COUNTED>
+static void run_pipeline_spill(Ctx &c, unsigned k, bool canonical, unsigned bits, const BuildInput &in, uint32_t P,
+                               BuildOutput *out);
+
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
                          const BuildInput &in, BuildOutput *out) {
@@ -1430,6 +1458,10 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     c.radix_bytes = 0;
     c.radix_launches = 0;
     const uint32_t P = plan_ranges<L2, COUNTED>(c, K, canonical, in);
+    if (want_spill<L2, COUNTED>(c, K, canonical, in, P)) {  // not even the real edges fit: spill
+        run_pipeline_spill<L2, L3, COUNTED>(c, k, canonical, bits, in, P, out);
+        return;
+    }
     uint64_t U = 0, R = 0;
     int ev_extract, ev_sort, ev_unique;
     if (P > 1) {
@@ -1680,6 +1712,7 @@ static std::vector<uint64_t> route(Ctx &c, const Dist &d, const Key<L> *in, uint
                                    unsigned pshift, unsigned pbits, const std::vector<uint64_t> &bounds,
                                    Key<L> *out, const uint32_t *in_v = nullptr, uint32_t *out_v = nullptr) {
     const int P = d.P;
+    if (P > MAX_ROUTE) throw std::runtime_error("more destinations than the routing kernels support");
     std::vector<uint64_t> soff(P + 1, 0);
     if (!n) return soff;
     const uint64_t ntiles = ceil_div(n, RT_TILE);
@@ -1701,7 +1734,7 @@ static std::vector<uint64_t> route(Ctx &c, const Dist &d, const Key<L> *in, uint
         in, n, K, pshift, pbits, db, (uint32_t)P, toff, ntiles, out, in_v, out_v);
     HIP_CHECK(hipGetLastError());
     uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, (P + 1) * 8);
-    gather_strided_kernel<<<1, 256, 0, c.stream>>>(toff, ntiles, (uint32_t)P + 1, g);
+    gather_strided_kernel<<<dim3((unsigned)ceil_div(P + 1, 256)), 256, 0, c.stream>>>(toff, ntiles, (uint32_t)P + 1, g);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(soff.data(), g, (P + 1) * 8, hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -2034,12 +2067,17 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
         const uint64_t b = (*bounds)[j] << (B1 - OB);  // first level-1 bucket of the prefix
         soff[0][j] = b >= nb1 ? N : cur[b];
     }
-    K2 *xa;
-    uint32_t *xac = nullptr;
-    const K2 *arrs[1] = {ka};
-    const uint32_t *cnts[1] = {ca};
-    const uint64_t n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA, Workspace::XAC,
-                                          &xa, &xac);
+    K2 *xa = ka;
+    uint32_t *xac = ca;
+    uint64_t n1 = N;
+    if (d.P == 1) {  // one rank: its keys stay where they are (the buffers change slots instead of a copy)
+        c.ws.swap(Workspace::KA, Workspace::XA);
+        if (COUNTED) c.ws.swap(Workspace::CA, Workspace::XAC);
+    } else {
+        const K2 *arrs[1] = {ka};
+        const uint32_t *cnts[1] = {ca};
+        n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA, Workspace::XAC, &xa, &xac);
+    }
     tr("exchange 1", n1);
     // the owner's level-1 counts: the global pass-A histogram over its buckets
     const uint64_t ob0 = (*bounds)[d.me] << (B1 - OB), ob1 = std::min<uint64_t>((*bounds)[d.me + 1] << (B1 - OB), nb1);
@@ -2242,14 +2280,15 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     const unsigned k_b = K - 1;
     uint64_t D = 0;
     K3 *dk = nullptr;
-    {
+    if (d.P == 1) {  // one rank owns every target node: the single build's local join
+        D = stage_dummies_local<L2, L3>(c, K, E, R, &dk);
+        tr("dummies (local)", D);
+    } else {
         const unsigned B = bucket_bits<L2>(R, 2 * K);
         const unsigned bshift = 2 * K - B;
         const uint64_t nbk = 1ull << B;
         uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nbk + 2) * 8);
-        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
-        bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(E, R, bshift, nbk, bstart);
-        HIP_CHECK(hipGetLastError());
+        bucket_index<L2>(c, E, R, bshift, nbk, bstart);
         note_bucket_index(c, E, R, bstart, bshift);
         uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
         uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, R + 1);
@@ -2259,21 +2298,56 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
                                     c.stream>>>(E, R, flags);
             HIP_CHECK(hipGetLastError());
         }
-        // queries t = to_next(x, 0) of every owned edge, routed by the prefix of t
+        // queries t = to_next(x, 0) of every owned edge, as 4 sorted arrays (one per label of the
+        // querying edge, dist_kernels.hpp: target_split_kernel); every owner's share is a slice of each
         K2 *qs = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(R, 1) * sizeof(K2));
-        std::vector<std::vector<uint64_t>> qoff(1);
-        qoff[0] = route<L2, 0>(c, d, E, R, K, d.shift2, 2 * d.m, bounds, qs);
-        tr("first flags + route q", R);
+        std::vector<std::vector<uint64_t>> qoff(4, std::vector<uint64_t>(d.P + 1, 0));
+        std::vector<uint64_t> cstart(5, 0);
+        if (R) {
+            const uint64_t stiles = ceil_div(R, SplitTraits<L2>::TILE);
+            uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::RTCNT, (4 * stiles + 1) * 4);
+            uint64_t *toff = (uint64_t *)c.ws.get(Workspace::RTOFF, (4 * stiles + 1) * 8);
+            target_split_kernel<L2, true><<<dim3((unsigned)stiles), dim3(256), 0, c.stream>>>(E, R, K, stiles, tcnt,
+                                                                                               nullptr, nullptr);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t st = ceil_div(4 * stiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, 4 * stiles, toff, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            target_split_kernel<L2, false><<<dim3((unsigned)stiles), dim3(256), 0, c.stream>>>(E, R, K, stiles, nullptr,
+                                                                                                toff, qs);
+            HIP_CHECK(hipGetLastError());
+            uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, (5 + 4 * (d.P + 1)) * 8);
+            gather_strided_kernel<<<1, 256, 0, c.stream>>>(toff, stiles, 5, g);
+            HIP_CHECK(hipGetLastError());
+            uint64_t *db = (uint64_t *)c.ws.get(Workspace::BOUNDS, (d.P + 1) * 8);
+            HIP_CHECK(hipMemcpyAsync(db, bounds.data(), (d.P + 1) * 8, hipMemcpyHostToDevice, c.stream));
+            class_bounds_kernel<L2><<<dim3((unsigned)ceil_div(4 * (d.P + 1), 256)), dim3(256), 0, c.stream>>>(
+                qs, g, db, (uint32_t)d.P, d.shift2, g + 5);
+            HIP_CHECK(hipGetLastError());
+            std::vector<uint64_t> pos(4 * (d.P + 1));
+            HIP_CHECK(hipMemcpyAsync(cstart.data(), g, 5 * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipMemcpyAsync(pos.data(), g + 5, pos.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));  // bounds / pos are host locals
+            for (int cl = 0; cl < 4; ++cl)
+                for (int j = 0; j <= d.P; ++j) qoff[cl][j] = pos[cl * (d.P + 1) + j] - cstart[cl];
+            // the last owner ends at its class end
+            for (int cl = 0; cl < 4; ++cl) qoff[cl][d.P] = cstart[cl + 1] - cstart[cl];
+        }
+        tr("first flags + split q", R);
         K2 *qr;
         uint32_t *unused_c = nullptr;
-        const K2 *qarr[1] = {qs};
-        const uint64_t nq = exchange_runs<K2>(c, d, 1, qarr, nullptr, qoff, Workspace::QRECV, Workspace::XAC,
+        const K2 *qarr[4] = {qs + cstart[0], qs + cstart[1], qs + cstart[2], qs + cstart[3]};
+        const uint64_t nq = exchange_runs<K2>(c, d, 4, qarr, nullptr, qoff, Workspace::QRECV, Workspace::XAC,
                                          &qr, &unused_c);
         tr("exchange q", nq);
         uint8_t *qflag = (uint8_t *)c.ws.get(Workspace::QFLAG, nq + 1);
         if (nq) {
-            query_answer_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(nq, 256), 65536)), dim3(256), 0,
-                                      c.stream>>>(E, R, bstart, bshift, qr, nq, in_flag, qflag);
+            query_join_kernel<L2><<<dim3((unsigned)ceil_div(nq, JoinTraits<L2>::TILE)), dim3(256), 0, c.stream>>>(
+                E, R, bstart, bshift, qr, nq, in_flag, qflag);
             HIP_CHECK(hipGetLastError());
         }
         tr("answer q", nq);
@@ -2369,6 +2443,403 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     T.radix_launches = c.radix_launches;
     T.radix_pass_ms = c.radix_launches ? c.radix_ms / c.radix_launches : 0;
     T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
+    T.peak_bytes = c.ws.held();
+}
+
+// ------------------------------------------------------------- spilled build (out of HBM, f3)
+//
+// The disk container's role (SortedSetDisk + construct_boss_chunk_disk, boss_chunk_construct.cpp:
+// 664-933; sorted_set_disk_base.cpp:36-278) when even the real edges do not fit the budget: the
+// distributed algorithm with the key ranges as its "ranks", run one range at a time, every exchange
+// going through host memory (or files under swap_dir) instead of a peer GPU.  HBM holds one range's
+// edges and buffers at a time:
+//   1. per range: collect its real edges (collect_ranges' extraction, both strands in canonical
+//      mode) -> host; split their sink queries by label into 4 sorted arrays -> host;
+//   2. per range r: its edges and every range's queries that target r -> sinks of r (misses) and
+//      in-edge marks -> the dummy sources of r's nodes, routed by their lifted prefix -> host;
+//   3. per range: its edges, sinks and the sources routed to it -> sort + unique -> split emit ->
+//      the chunk rows appended on the host (BOSS::Chunk::extend, boss_chunk.cpp:230-270).
+class SpillStore {
+  public:
+    SpillStore(std::string dir, uint64_t disk_cap) : dir_(std::move(dir)), cap_(disk_cap) {}
+    ~SpillStore() {
+        for (auto &b : blocks_)
+            if (!b.path.empty()) std::remove(b.path.c_str());
+    }
+    // bytes of device memory d -> a new block (stream-ordered, synchronous)
+    uint32_t put(const void *d, uint64_t bytes, hipStream_t s) {
+        Block b;
+        b.bytes = bytes;
+        std::vector<uint8_t> h(bytes);
+        if (bytes) {
+            HIP_CHECK(hipMemcpyAsync(h.data(), d, bytes, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+        }
+        if (!dir_.empty() && on_disk_ + bytes <= cap_ && bytes) {
+            b.path = dir_ + "/mtg_spill_" + std::to_string((unsigned long)getpid()) + "_" +
+                     std::to_string((unsigned long)(uintptr_t)this) + "_" + std::to_string(blocks_.size()) + ".bin";
+            FILE *f = fopen(b.path.c_str(), "wb");
+            const bool ok = f && fwrite(h.data(), 1, bytes, f) == bytes;
+            if (f) fclose(f);
+            if (ok) {
+                on_disk_ += bytes;
+            } else {  // swap_dir unusable: keep the block in RAM
+                std::remove(b.path.c_str());
+                b.path.clear();
+                b.ram = std::move(h);
+            }
+        } else {
+            b.ram = std::move(h);
+        }
+        total_ += bytes;
+        blocks_.push_back(std::move(b));
+        return (uint32_t)blocks_.size() - 1;
+    }
+    // bytes [off, off + n) of block id -> device memory d
+    void get(uint32_t id, uint64_t off, uint64_t n, void *d, hipStream_t s) {
+        if (!n) return;
+        const Block &b = blocks_[id];
+        if (off + n > b.bytes) throw std::runtime_error("spill block read past its end");
+        if (b.path.empty()) {
+            HIP_CHECK(hipMemcpyAsync(d, b.ram.data() + off, n, hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            return;
+        }
+        std::vector<uint8_t> h(n);
+        FILE *f = fopen(b.path.c_str(), "rb");
+        const bool ok = f && fseeko(f, (off_t)off, SEEK_SET) == 0 && fread(h.data(), 1, n, f) == n;
+        if (f) fclose(f);
+        if (!ok) throw std::runtime_error("cannot read spill file " + b.path);
+        HIP_CHECK(hipMemcpyAsync(d, h.data(), n, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    uint64_t bytes(uint32_t id) const { return blocks_[id].bytes; }
+    uint64_t total() const { return total_; }
+    uint64_t on_disk() const { return on_disk_; }
+
+  private:
+    struct Block {
+        uint64_t bytes = 0;
+        std::vector<uint8_t> ram;
+        std::string path;
+    };
+    std::string dir_;
+    uint64_t cap_;
+    uint64_t total_ = 0, on_disk_ = 0;
+    std::vector<Block> blocks_;
+};
+
+// the exchange layer of a spilled build has no peers: the routing helpers only read P from it
+class NoComm : public Comm {
+  public:
+    explicit NoComm(int P) : Comm(0, P) {}
+    void allreduce_sum_u64(uint64_t *, size_t, hipStream_t) override { fail(); }
+    void allgather_u64(const uint64_t *, uint64_t *, size_t, hipStream_t) override { fail(); }
+    void alltoallv(const void *, const uint64_t *, const uint64_t *, void *, const uint64_t *, const uint64_t *,
+                   size_t, hipStream_t) override {
+        fail();
+    }
+
+  private:
+    static void fail() { throw std::runtime_error("a spilled build has no exchange"); }
+};
+
+// spill when the build runs in key ranges, its arrays go to the host, and the real edges (at most
+// the windows of both strands) may not fit the budget -- or always with MTG_SPILL=1
+template <int L2, bool COUNTED>
+static bool want_spill(Ctx &c, unsigned K, bool canonical, const BuildInput &in, uint32_t P) {
+    if (P < 2 || !c.host_output || K < RB_CHARS + 2) return false;
+    if (c.force_spill) return true;
+    if (!c.disk) return false;
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    double budget = c.mem_budget;
+    if (budget <= 0) {
+        size_t fr = 0, tot = 0;
+        HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        budget = 0.9 * ((double)fr + (double)c.ws.held());
+    }
+    const double per_key = (double)sizeof(Key<L2>) + (COUNTED ? 4.0 : 0.0);
+    // the in-HBM tail holds the real edges, their flags, the dummies and the output rows
+    return (double)npos * (canonical ? 2.0 : 1.0) * (per_key + 4.0) > budget;
+}
+
+template <int L2, int L3, bool COUNTED>
+static void run_pipeline_spill(Ctx &c, unsigned k, bool canonical, unsigned bits, const BuildInput &in, uint32_t P,
+                               BuildOutput *out) {
+    using K2 = Key<L2>;
+    using K3 = Key<L3>;
+    const unsigned K = k + 1;
+    const unsigned cbits = bits <= 8 ? 8 : bits <= 16 ? 16 : 32;
+    const uint32_t cmax = cbits == 8 ? 0xFFu : cbits == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+    mtg_boss_timings &T = c.timings;
+    EventTimer tm(c.stream);
+    const int ev_start = tm.mark();
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    T.n_positions = npos;
+    const int both = canonical ? 1 : 0;
+    constexpr int TILE = RangeTraits<L2>::TILE;
+    const uint64_t tiles = ceil_div(npos, TILE);
+    // the ranges: count pass, bins balanced (collect_ranges)
+    std::vector<uint64_t> hist(RB_BINS, 0);
+    uint16_t *tbins = (uint16_t *)c.ws.get(Workspace::RANGE_BINS, std::max<uint64_t>(tiles, 1) * RB_BINS * 2);
+    if (tiles) {
+        auto *dh = (unsigned long long *)c.ws.get(Workspace::XHIST, RB_BINS * 8);
+        HIP_CHECK(hipMemsetAsync(dh, 0, RB_BINS * 8, c.stream));
+        range_count_kernel<L2><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, both, tbins);
+        HIP_CHECK(hipGetLastError());
+        range_bins_reduce_kernel<<<dim3((unsigned)std::min<uint64_t>(tiles, 2048)), dim3(RB_BINS), 0, c.stream>>>(
+            tbins, tiles, dh);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(hist.data(), dh, RB_BINS * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+    uint64_t total = 0;
+    for (uint64_t v : hist) total += v;
+    P = std::min<uint32_t>(P, RB_BINS);
+    const std::vector<uint64_t> bounds = balanced_bounds(hist.data(), RB_BINS, (int)P);
+    NoComm nocomm((int)P);
+    Dist d{nocomm, (int)P, 0, RB_CHARS, 2 * K - 2 * RB_CHARS, RB_BINS, &tm, {}};
+    SpillStore st(c.disk ? c.swap_dir : std::string(), c.disk_cap);
+    uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
+    uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
+    std::vector<uint32_t> eid(P), ecid(P), qid(P);
+    std::vector<uint64_t> rn(P, 0);
+    std::vector<std::vector<uint64_t>> qpos(P), qcs(P);  // per range: query slices [4][P + 1], class starts [5]
+    // ---- 1. the real edges of every range, and their sink queries split by label
+    for (uint32_t j = 0; j < P; ++j) {
+        const uint32_t lo = (uint32_t)bounds[j], hi = (uint32_t)bounds[j + 1];
+        uint64_t nj = 0;
+        for (uint32_t b = lo; b < hi; ++b) nj += hist[b];
+        K2 *ka = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(nj, 1) * sizeof(K2));
+        K2 *kb = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nj, 1) * sizeof(K2));
+        uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(nj, 1) * 4) : nullptr;
+        uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nj, 1) * 4) : nullptr;
+        uint64_t U = 0;
+        if (nj) {
+            BinSet sel{};
+            sel.add(lo, hi);
+            range_tile_counts_kernel<<<dim3((unsigned)ceil_div(tiles, 4)), dim3(256), 0, c.stream>>>(tbins, tiles, sel,
+                                                                                                     tcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t sct = ceil_div(tiles, 4096);
+            uint64_t *desc = acquire_desc(c, sct, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)sct), dim3(512), 0, c.stream>>>(tcnt, tiles, toff, desc, ep,
+                                                                               &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            range_write_kernel<L2, COUNTED><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
+                in.seq, in.seq_len, K, both, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, sel, toff, ka,
+                ca);
+            HIP_CHECK(hipGetLastError());
+            if (read_u64(c, (const unsigned long long *)(toff + tiles)) != nj)
+                throw std::runtime_error("range extraction count differs from its histogram");
+            const double spread = (double)RB_BINS / (double)(hi - lo);
+            const double dup = estimate_dup<L2>(c, ka, nj, 8.0) / spread;
+            U = msd_sort_unique<L2, COUNTED>(c, &ka, &kb, &ca, &cb, nj, 2 * K, cmax, dup);
+        }
+        rn[j] = U;
+        eid[j] = st.put(ka, U * sizeof(K2), c.stream);
+        if (COUNTED) ecid[j] = st.put(ca, U * 4, c.stream);
+        // the queries of the range's edges, 4 sorted arrays, sliced by target range
+        qcs[j].assign(5, 0);
+        qpos[j].assign(4 * (P + 1), 0);
+        K2 *qs = (K2 *)c.ws.get(Workspace::QSEND, std::max<uint64_t>(U, 1) * sizeof(K2));
+        if (U) {
+            const uint64_t stiles = ceil_div(U, SplitTraits<L2>::TILE);
+            uint32_t *qtc = (uint32_t *)c.ws.get(Workspace::RTCNT, (4 * stiles + 1) * 4);
+            uint64_t *qto = (uint64_t *)c.ws.get(Workspace::RTOFF, (4 * stiles + 1) * 8);
+            target_split_kernel<L2, true><<<dim3((unsigned)stiles), dim3(256), 0, c.stream>>>(ka, U, K, stiles, qtc,
+                                                                                               nullptr, nullptr);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t sct = ceil_div(4 * stiles, 4096);
+            uint64_t *desc = acquire_desc(c, sct, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)sct), dim3(512), 0, c.stream>>>(qtc, 4 * stiles, qto, desc, ep,
+                                                                               &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            target_split_kernel<L2, false><<<dim3((unsigned)stiles), dim3(256), 0, c.stream>>>(ka, U, K, stiles, nullptr,
+                                                                                                qto, qs);
+            HIP_CHECK(hipGetLastError());
+            uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, (5 + 4 * (P + 1)) * 8);
+            gather_strided_kernel<<<1, 256, 0, c.stream>>>(qto, stiles, 5, g);
+            HIP_CHECK(hipGetLastError());
+            uint64_t *db = (uint64_t *)c.ws.get(Workspace::BOUNDS, (P + 1) * 8);
+            HIP_CHECK(hipMemcpyAsync(db, bounds.data(), (P + 1) * 8, hipMemcpyHostToDevice, c.stream));
+            class_bounds_kernel<L2><<<dim3((unsigned)ceil_div(4 * (P + 1), 256)), dim3(256), 0, c.stream>>>(
+                qs, g, db, P, d.shift2, g + 5);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(qcs[j].data(), g, 5 * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipMemcpyAsync(qpos[j].data(), g + 5, qpos[j].size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            for (int cl = 0; cl < 4; ++cl) qpos[j][cl * (P + 1) + P] = qcs[j][cl + 1];
+        }
+        qid[j] = st.put(qs, U * sizeof(K2), c.stream);
+    }
+    T.n_extracted = total / (canonical ? 2 : 1);
+    uint64_t R = 0;
+    for (uint64_t v : rn) R += v;
+    T.n_unique = T.n_real = R;
+    const int ev_collect = tm.mark();
+    // ---- 2. sinks and in-edge marks at every range, then the sources of its nodes, routed
+    std::vector<uint32_t> skid(P), srcid(P);
+    std::vector<uint64_t> nsk(P, 0);
+    std::vector<std::vector<uint64_t>> soffs(P);
+    const std::vector<uint64_t> b3 = lifted_bounds(bounds, RB_CHARS);
+    for (uint32_t r = 0; r < P; ++r) {
+        const uint64_t Rr = rn[r];
+        K2 *E = (K2 *)c.ws.get(Workspace::REAL, std::max<uint64_t>(Rr, 1) * sizeof(K2));
+        st.get(eid[r], 0, Rr * sizeof(K2), E, c.stream);
+        const unsigned B = bucket_bits<L2>(Rr, 2 * K);
+        const unsigned bshift = 2 * K - B;
+        uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << B) + 2) * 8);
+        bucket_index<L2>(c, E, Rr, bshift, 1ull << B, bstart);
+        // every range's queries that target r: 4 sorted runs per range, in class order
+        uint64_t nq = 0;
+        for (uint32_t j = 0; j < P; ++j)
+            for (int cl = 0; cl < 4; ++cl) nq += qpos[j][cl * (P + 1) + r + 1] - qpos[j][cl * (P + 1) + r];
+        K2 *qr = (K2 *)c.ws.get(Workspace::QRECV, std::max<uint64_t>(nq, 1) * sizeof(K2));
+        uint64_t o = 0;
+        for (uint32_t j = 0; j < P; ++j)
+            for (int cl = 0; cl < 4; ++cl) {
+                const uint64_t a = qpos[j][cl * (P + 1) + r], b = qpos[j][cl * (P + 1) + r + 1];
+                st.get(qid[j], a * sizeof(K2), (b - a) * sizeof(K2), qr + o, c.stream);
+                o += b - a;
+            }
+        uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, Rr + 1);
+        uint8_t *in_flag = (uint8_t *)c.ws.get(Workspace::INFLAG, Rr + 1);
+        uint8_t *qflag = (uint8_t *)c.ws.get(Workspace::QFLAG, nq + 1);
+        if (Rr) {
+            HIP_CHECK(hipMemsetAsync(in_flag, 0, Rr, c.stream));
+            first_flag_kernel<L2><<<dim3((unsigned)std::min<uint64_t>(ceil_div(Rr, 256), 16384)), dim3(256), 0,
+                                    c.stream>>>(E, Rr, flags);
+            HIP_CHECK(hipGetLastError());
+        }
+        if (nq) {
+            query_join_kernel<L2><<<dim3((unsigned)ceil_div(nq, JoinTraits<L2>::TILE)), dim3(256), 0, c.stream>>>(
+                E, Rr, bstart, bshift, qr, nq, in_flag, qflag);
+            HIP_CHECK(hipGetLastError());
+        }
+        // the sinks of r: the queries that missed
+        const uint64_t qtiles = ceil_div(nq, RT_TILE);
+        uint32_t *qtcnt = (uint32_t *)c.ws.get(Workspace::QTCNT, (qtiles + 1) * 4);
+        uint64_t *qtoff = (uint64_t *)c.ws.get(Workspace::QTOFF, (qtiles + 1) * 8);
+        uint64_t nsink = 0;
+        K3 *sk = nullptr;
+        if (nq) {
+            sink_count_kernel<<<dim3((unsigned)qtiles), dim3(RT_BLOCK), 0, c.stream>>>(qflag, nq, qtcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t sct = ceil_div(qtiles, 4096);
+            uint64_t *desc = acquire_desc(c, sct, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)sct), dim3(512), 0, c.stream>>>(qtcnt, qtiles, qtoff, desc, ep,
+                                                                               &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            nsink = read_u64(c, (const unsigned long long *)(qtoff + qtiles));
+            sk = (K3 *)c.ws.get(Workspace::DA, std::max<uint64_t>(nsink, 1) * sizeof(K3));
+            if (nsink) {
+                sink_write_kernel<L2, L3><<<dim3((unsigned)qtiles), dim3(RT_BLOCK), 0, c.stream>>>(qr, qflag, nq, K,
+                                                                                                  qtoff, sk);
+                HIP_CHECK(hipGetLastError());
+            }
+        }
+        nsk[r] = nsink;
+        skid[r] = st.put(sk, nsink * sizeof(K3), c.stream);
+        // the sources of r's nodes (first edges no query hit), every level, routed by lifted prefix
+        const uint64_t wtiles = ceil_div(Rr, DummyTraits<L2>::WTILE);
+        uint32_t *wc = (uint32_t *)c.ws.get(Workspace::DTCNT, (std::max(wtiles, tiles) + 1) * 4);
+        uint64_t *wo = (uint64_t *)c.ws.get(Workspace::DTOFF, (std::max(wtiles, tiles) + 1) * 8);
+        uint64_t nsrc = 0;
+        if (Rr) {
+            dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, Rr, k, wc);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t sct = ceil_div(wtiles, 4096);
+            uint64_t *desc = acquire_desc(c, sct, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)sct), dim3(512), 0, c.stream>>>(wc, wtiles, wo, desc, ep,
+                                                                               &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            nsrc = read_u64(c, (const unsigned long long *)(wo + wtiles));
+        }
+        K3 *src = (K3 *)c.ws.get(Workspace::DSRC, std::max<uint64_t>(nsrc, 1) * sizeof(K3));
+        if (nsrc) {
+            dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(E, flags, in_flag, Rr, K, wo,
+                                                                                            src);
+            HIP_CHECK(hipGetLastError());
+        }
+        K3 *ssend = (K3 *)c.ws.get(Workspace::DSEND, std::max<uint64_t>(nsrc, 1) * sizeof(K3));
+        soffs[r] = route<L3, 1>(c, d, src, nsrc, K, 3 * K - 3 * RB_CHARS, 3 * RB_CHARS, b3, ssend);
+        srcid[r] = st.put(ssend, nsrc * sizeof(K3), c.stream);
+    }
+    const int ev_dummy_route = tm.mark();
+    // ---- 3. per range: dummies sorted, rows emitted, appended on the host
+    c.spill_W.clear();
+    c.spill_last.clear();
+    c.spill_weights.clear();
+    uint64_t F[5] = {0, 0, 0, 0, 0}, ndummy = 0;
+    for (uint32_t r = 0; r < P; ++r) {
+        const uint64_t Rr = rn[r];
+        K2 *E = (K2 *)c.ws.get(Workspace::REAL, std::max<uint64_t>(Rr, 1) * sizeof(K2));
+        uint32_t *Ec = COUNTED ? (uint32_t *)c.ws.get(Workspace::REALC, std::max<uint64_t>(Rr, 1) * 4) : nullptr;
+        st.get(eid[r], 0, Rr * sizeof(K2), E, c.stream);
+        if (COUNTED) st.get(ecid[r], 0, Rr * 4, Ec, c.stream);
+        uint64_t Draw = nsk[r];
+        for (uint32_t j = 0; j < P; ++j) Draw += soffs[j][r + 1] - soffs[j][r];
+        K3 *da = (K3 *)c.ws.get(Workspace::DA, std::max<uint64_t>(Draw, 1) * sizeof(K3));
+        K3 *db = (K3 *)c.ws.get(Workspace::DB, std::max<uint64_t>(Draw, 1) * sizeof(K3));
+        st.get(skid[r], 0, nsk[r] * sizeof(K3), da, c.stream);
+        uint64_t o = nsk[r];
+        for (uint32_t j = 0; j < P; ++j) {
+            const uint64_t a = soffs[j][r], b = soffs[j][r + 1];
+            st.get(srcid[j], a * sizeof(K3), (b - a) * sizeof(K3), da + o, c.stream);
+            o += b - a;
+        }
+        K3 *dk = nullptr;
+        uint64_t D = 0;
+        if (Draw) D = sort_unique_dummies<L3>(c, K, da, db, Draw, &dk);
+        note_bucket_index(c, nullptr, 0, nullptr, 0);
+        BuildOutput o2{};
+        int ev_m;
+        stage_merge_emit<L2, L3, COUNTED>(c, tm, &ev_m, k, bits, E, Ec, Rr, dk, D, r == 0, &o2);
+        check_error_word(c);
+        // extend: range 0 keeps its leading row 0, the others append the rows after it
+        const uint64_t from = r == 0 ? 0 : 1, rows = o2.n - from;
+        const uint64_t at = c.spill_W.size();
+        c.spill_W.resize(at + rows);
+        c.spill_last.resize(at + rows);
+        HIP_CHECK(hipMemcpyAsync(c.spill_W.data() + at, o2.W + from, rows, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(c.spill_last.data() + at, o2.last + from, rows, hipMemcpyDeviceToHost, c.stream));
+        if (COUNTED) {
+            c.spill_weights.resize(at + rows);
+            HIP_CHECK(hipMemcpyAsync(c.spill_weights.data() + at, o2.weights + from, rows * 4, hipMemcpyDeviceToHost,
+                                     c.stream));
+        }
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        for (int ch = 0; ch < 5; ++ch) F[ch] += o2.F[ch];
+        ndummy += o2.n_dummy;
+    }
+    const int ev_emit = tm.mark();
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    out->host = true;
+    out->W = c.spill_W.data();
+    out->last = c.spill_last.data();
+    out->weights = COUNTED ? c.spill_weights.data() : nullptr;
+    out->n = c.spill_W.size();
+    std::memcpy(out->F, F, sizeof(F));
+    out->n_real = R;
+    out->n_dummy = ndummy;
+    c.spilled_bytes = st.total();
+    T.spilled_bytes = st.total();
+    T.n_dummy = ndummy;
+    T.n_rows = out->n;
+    T.n_batches = P;
+    T.extract_ms = tm.ms(ev_start, ev_collect);
+    T.dummy_ms = tm.ms(ev_collect, ev_dummy_route);
+    T.emit_ms = tm.ms(ev_dummy_route, ev_emit);
+    T.total_ms = tm.ms(ev_start, ev_emit);
     T.peak_bytes = c.ws.held();
 }
 
@@ -2657,7 +3128,8 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
     }
     auto *c = new mtg_boss_ctor();
     c->params = *p;
-    c->params.filter_suffix = nullptr;  // the caller's string need not outlive the call
+    c->params.filter_suffix = nullptr;  // the caller's strings need not outlive the call
+    c->params.swap_dir = nullptr;
     c->suffix = suffix;
     c->device = p->device_id;
     c->stage.enable_mirror(c->device);
@@ -2667,6 +3139,8 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
         load_knobs(c->ctx);
         c->ctx.mem_budget = p->memory_preallocated;
+        c->ctx.swap_dir = p->swap_dir ? p->swap_dir : "";
+        c->ctx.disk_cap = p->disk_cap_bytes;
         // the disk container bounds memory: always collect in key ranges (boss_chunk_construct.cpp:664-933)
         if (p->container_type == MTG_CONTAINER_VECTOR_DISK && !c->ctx.force_ranges) c->ctx.disk = true;
     } catch (const std::exception &e) {
@@ -2883,6 +3357,15 @@ static int run_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, Bu
     }
     try {
         HIP_CHECK(hipSetDevice(c->device));
+        // the build's device work, bracketed for the exchange layer (LocalComm's serial mode)
+        struct Scope {
+            mtg::Comm *comm;
+            hipStream_t s;
+            ~Scope() {
+                if (comm) comm->end_build(s);
+            }
+        } scope{comm, c->ctx.stream};
+        if (comm) comm->begin_build(c->ctx.stream);
         dispatch_build(c, comm, in, out);
         return MTG_OK;
     } catch (const std::exception &e) {
@@ -3117,8 +3600,45 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         const double input_ms = ms_since(t_input);
         BuildInput in{dseq, seq_base, dstarts, dcounts, per_read ? total_reads : 0};
         BuildOutput o{};
+        c->ctx.host_output = comm == nullptr;  // a single build with host arrays may spill
         dispatch_build(c, comm, in, &o);
+        c->ctx.host_output = false;
         const auto t_d2h = std::chrono::steady_clock::now();
+        if (o.host) {  // the spilled build: its rows are already on the host
+            PinnedPool &pool = PinnedPool::get();
+            const uint64_t nwords = ceil_div(o.n, 64);
+            out->k = c->params.k;
+            out->alph_size = 5;
+            out->n = o.n;
+            out->bits_per_count = c->params.bits_per_count;
+            out->n_real = o.n_real;
+            out->n_dummy = o.n_dummy;
+            std::memcpy(out->F, o.F, sizeof(o.F));
+            out->W = (uint8_t *)pool.take(std::max<uint64_t>(o.n, 1));
+            std::memcpy(out->W, o.W, o.n);
+            out->last = (uint64_t *)pool.take(std::max<uint64_t>(nwords, 1) * 8);
+            std::memset(out->last, 0, std::max<uint64_t>(nwords, 1) * 8);
+            for (uint64_t i = 0; i < o.n; ++i) out->last[i >> 6] |= (uint64_t)(o.last[i] & 1) << (i & 63);
+            if (o.weights) {
+                out->weights = (uint32_t *)pool.take(std::max<uint64_t>(o.n, 1) * 4);
+                std::memcpy(out->weights, o.weights, o.n * 4);
+            }
+            c->ctx.spill_W = std::vector<uint8_t>();
+            c->ctx.spill_last = std::vector<uint8_t>();
+            c->ctx.spill_weights = std::vector<uint32_t>();
+            mtg_boss_timings &T = c->ctx.timings;
+            T.d2h_ms = ms_since(t_d2h);
+            T.h2d_ms = h2d_ms;
+            T.input_ms = input_ms;
+            T.stage_ms = (double)c->stage_ns.exchange(0) * 1e-6;
+            c->stage.clear_locked();
+            stage_lock.unlock();
+            c->kmc.clear();
+            for (auto &f : c->fasta) free_fasta(f);
+            c->fasta.clear();
+            T.host_total_ms = ms_since(t_start);
+            return MTG_OK;
+        }
         const uint64_t nwords = ceil_div(o.n, 64);
         uint64_t *dbits = (uint64_t *)c->ctx.ws.get(Workspace::LAST_BITS, std::max<uint64_t>(nwords, 1) * 8);
         if (nwords) {
@@ -3286,6 +3806,8 @@ int mtg_comm_create_local(int world, mtg_comm **comms) {
         return MTG_ERR_ARGUMENT;
     }
     auto group = std::make_shared<mtg::LocalGroup>(world);
+    const char *ser = getenv("MTG_LOCAL_SERIAL");
+    group->serial = ser && ser[0] == '1';
     for (int r = 0; r < world; ++r) {
         comms[r] = new mtg_comm();
         comms[r]->comm.reset(new mtg::LocalComm(group, r));
@@ -3310,6 +3832,11 @@ mtg_comm *mtg_comm_create_callbacks(const mtg_comm_callbacks *cb) {
 }
 
 void mtg_comm_destroy(mtg_comm *comm) { delete comm; }
+
+double mtg_comm_local_held_ms(mtg_comm *comm, int reset) {
+    auto *lc = comm ? dynamic_cast<mtg::LocalComm *>(comm->comm.get()) : nullptr;
+    return lc ? lc->held_ms(reset != 0) : -1.0;
+}
 
 int mtg_comm_rank(const mtg_comm *comm) { return comm ? comm->comm->rank() : -1; }
 

@@ -48,6 +48,9 @@ class Comm {
     virtual void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff,
                            void *d_recv, const uint64_t *rcnt, const uint64_t *roff, size_t esz,
                            hipStream_t s) = 0;
+    // a build's device work starts / ends on stream s (LocalComm's serial mode hands the device over)
+    virtual void begin_build(hipStream_t) {}
+    virtual void end_build(hipStream_t) {}
 
   protected:
     int rank_, size_;
@@ -226,7 +229,7 @@ class CallbackComm : public Comm {
 
 // ------------------------------------------------------------------- in-process rank threads
 struct LocalGroup {
-    explicit LocalGroup(int n) : size(n), slots(n), host(n) {}
+    explicit LocalGroup(int n) : size(n), slots(n), host(n), held_ms(n, 0.0) {}
     int size;
     std::mutex mu;
     std::condition_variable cv;
@@ -240,6 +243,13 @@ struct LocalGroup {
     std::vector<std::vector<uint64_t>> host;
 
     std::string failure;  // first error any rank reported: every barrier then throws it
+
+    // serial mode (MTG_LOCAL_SERIAL=1, tools/dist_sim.py): one rank at a time owns the device, from
+    // build start to its next exchange and from there to the next, so every rank's device time is
+    // its own work (held_ms) and the step's wall time is the SUM of the ranks' work
+    bool serial = false;
+    std::mutex gpu;
+    std::vector<double> held_ms;
 
     // a rank that failed says so (fail), and peers waiting in a barrier throw its message at once;
     // a rank that dies without failing never arrives, and the others give up after a minute
@@ -269,16 +279,30 @@ struct LocalGroup {
 class LocalComm : public Comm {
   public:
     LocalComm(std::shared_ptr<LocalGroup> g, int rank) : Comm(rank, g->size), g_(std::move(g)) {}
+    void begin_build(hipStream_t) override { hold(); }
+    void end_build(hipStream_t s) override {
+        if (!held_) return;
+        (void)hipStreamSynchronize(s);
+        drop();
+    }
+    // this rank's device time in serial mode (ms), optionally reset
+    double held_ms(bool reset) {
+        std::lock_guard<std::mutex> lk(g_->mu);
+        const double v = g_->held_ms[rank_];
+        if (reset) g_->held_ms[rank_] = 0;
+        return v;
+    }
     void allreduce_sum_u64(uint64_t *d, size_t n, hipStream_t s) override {
         auto &mine = g_->host[rank_];
         mine.resize(n);
         COMM_HIP(hipMemcpyAsync(mine.data(), d, n * 8, hipMemcpyDeviceToHost, s));
         COMM_HIP(hipStreamSynchronize(s));
-        g_->barrier();
+        wait();
         std::vector<uint64_t> sum(n, 0);
         for (int r = 0; r < size_; ++r)
             for (size_t i = 0; i < n; ++i) sum[i] += g_->host[r][i];
-        g_->barrier();
+        wait();
+        hold();
         COMM_HIP(hipMemcpyAsync(d, sum.data(), n * 8, hipMemcpyHostToDevice, s));
         COMM_HIP(hipStreamSynchronize(s));
     }
@@ -287,10 +311,11 @@ class LocalComm : public Comm {
         mine.resize(n);
         COMM_HIP(hipMemcpyAsync(mine.data(), d_send, n * 8, hipMemcpyDeviceToHost, s));
         COMM_HIP(hipStreamSynchronize(s));
-        g_->barrier();
+        wait();
         std::vector<uint64_t> all(n * size_);
         for (int r = 0; r < size_; ++r) std::copy(g_->host[r].begin(), g_->host[r].end(), all.begin() + r * n);
-        g_->barrier();
+        wait();
+        hold();
         COMM_HIP(hipMemcpyAsync(d_recv, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
         COMM_HIP(hipStreamSynchronize(s));
     }
@@ -301,7 +326,7 @@ class LocalComm : public Comm {
         slot.ptr = d_send;
         slot.soff.assign(soff, soff + size_);
         slot.scnt.assign(scnt, scnt + size_);
-        g_->barrier();
+        wait();
         for (int i = 0; i < size_; ++i)
             if (g_->slots[i].scnt[rank_] != rcnt[i]) {
                 const std::string msg = "local all-to-all: rank " + std::to_string(rank_) + " expects " +
@@ -310,6 +335,7 @@ class LocalComm : public Comm {
                 g_->fail(msg);  // peers in the next barrier throw this too, without waiting
                 throw std::runtime_error(msg);
             }
+        hold();
         for (int i = 0; i < size_; ++i) {
             const auto &src = g_->slots[i];
             if (rcnt[i])
@@ -318,11 +344,35 @@ class LocalComm : public Comm {
                                         hipMemcpyDeviceToDevice, s));
         }
         COMM_HIP(hipStreamSynchronize(s));
-        g_->barrier();  // nobody reuses its send buffer while a peer still copies from it
+        wait();  // nobody reuses its send buffer while a peer still copies from it
+        hold();
     }
 
   private:
+    // serial mode: take / hand over the device (the stream is drained before every hand-over)
+    void hold() {
+        if (!g_->serial || held_) return;
+        g_->gpu.lock();
+        held_ = true;
+        t0_ = std::chrono::steady_clock::now();
+    }
+    void drop() {
+        if (!held_) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0_).count();
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            g_->held_ms[rank_] += ms;
+        }
+        held_ = false;
+        g_->gpu.unlock();
+    }
+    void wait() {
+        drop();
+        g_->barrier();
+    }
     std::shared_ptr<LocalGroup> g_;
+    bool held_ = false;
+    std::chrono::steady_clock::time_point t0_;
 };
 
 }  // namespace mtg

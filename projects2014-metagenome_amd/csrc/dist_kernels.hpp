@@ -26,15 +26,20 @@
 namespace mtg {
 
 constexpr int MAX_RANKS = 64;
+// destinations of one routing launch: ranks, or the key ranges of a spilled build (<= RB_BINS)
+constexpr int MAX_ROUTE = 256;
 constexpr int RT_BLOCK = 256;
 constexpr int RT_TILE = 4096;
 constexpr int RT_PER = RT_TILE / RT_BLOCK;
 
-// rank of a prefix: #{j in 1..P-1 : bounds[j] <= v}
+// rank of a prefix: #{j in 1..P-1 : bounds[j] <= v} (bounds ascending)
 __device__ __forceinline__ uint32_t owner_of(uint64_t v, const uint64_t *s_bounds, uint32_t P) {
-    uint32_t o = 0;
-    for (uint32_t j = 1; j < P; ++j) o += s_bounds[j] <= v ? 1u : 0u;
-    return o;
+    uint32_t a = 1, b = P;
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (s_bounds[mid] <= v) a = mid + 1; else b = mid;
+    }
+    return a - 1;
 }
 
 // MODE 0: the routed key is t = to_next(x, K, 0) of a 2-bit edge x (node a_2..a_K, label $);
@@ -53,8 +58,8 @@ template <int L, int MODE>
 __global__ __launch_bounds__(RT_BLOCK) void route_count_kernel(
     const Key<L> *__restrict__ in, uint64_t n, unsigned K, unsigned pshift, unsigned pbits,
     const uint64_t *__restrict__ bounds, uint32_t P, uint32_t *__restrict__ tcnt, uint64_t ntiles) {
-    __shared__ uint64_t s_b[MAX_RANKS + 1];
-    __shared__ uint32_t s_c[MAX_RANKS];
+    __shared__ uint64_t s_b[MAX_ROUTE + 1];
+    __shared__ uint32_t s_c[MAX_ROUTE];
     const uint32_t tid = threadIdx.x;
     for (uint32_t j = tid; j <= P; j += RT_BLOCK) s_b[j] = bounds[j];
     for (uint32_t j = tid; j < P; j += RT_BLOCK) s_c[j] = 0;
@@ -88,9 +93,9 @@ __global__ __launch_bounds__(RT_BLOCK) void route_write_kernel(
     uint64_t ntiles, Key<L> *__restrict__ out, const uint32_t *__restrict__ in_v = nullptr,
     uint32_t *__restrict__ out_v = nullptr) {
     // in_v / out_v (optional): a count per key, moved with it
-    __shared__ uint64_t s_b[MAX_RANKS + 1];
-    __shared__ uint64_t s_base[MAX_RANKS];
-    __shared__ uint32_t s_c[MAX_RANKS];
+    __shared__ uint64_t s_b[MAX_ROUTE + 1];
+    __shared__ uint64_t s_base[MAX_ROUTE];
+    __shared__ uint32_t s_c[MAX_ROUTE];
     const uint32_t tid = threadIdx.x;
     for (uint32_t j = tid; j <= P; j += RT_BLOCK) s_b[j] = bounds[j];
     for (uint32_t j = tid; j < P; j += RT_BLOCK) {
@@ -163,37 +168,6 @@ __global__ void first_flag_kernel(const Key<L> *__restrict__ keys, uint64_t n,
     }
 }
 
-/*
- * Owner side of the sink join: query p = node (a_2..a_K) with label $ of some edge x anywhere.
- * The first edge of node p (lower bound of p among the owner's sorted edges) gets its in-edge
- * mark -- x targets that node, so it needs no dummy source (:148-166); a miss means x's target
- * node has no out-edge and needs a dummy sink (:80-95): qflag = 1.
- */
-template <int L>
-__global__ void query_answer_kernel(const Key<L> *__restrict__ keys, uint64_t n,
-                                    const uint64_t *__restrict__ start, unsigned bshift,
-                                    const Key<L> *__restrict__ q, uint64_t nq,
-                                    uint8_t *__restrict__ in_flag, uint8_t *__restrict__ qflag) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += stride) {
-        const Key<L> p = q[i];
-        bool hit = false;
-        if (n) {
-            const uint64_t b = bits_at(shr(p, bshift), 0, 32);
-            uint64_t lo = start[b], hi = start[b + 1];
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                if (keys[mid] < p) lo = mid + 1; else hi = mid;
-            }
-            if (lo < n && shr(keys[lo], 2) == shr(p, 2)) {
-                hit = true;
-                in_flag[lo] = 1;
-            }
-        }
-        qflag[i] = hit ? 0 : 1;
-    }
-}
-
 // sink compaction over the answered queries: per-tile miss counts ...
 __global__ __launch_bounds__(RT_BLOCK) void sink_count_kernel(const uint8_t *__restrict__ qflag,
                                                              uint64_t nq, uint32_t *__restrict__ tcnt) {
@@ -235,6 +209,258 @@ __global__ __launch_bounds__(RT_BLOCK) void sink_write_kernel(const Key<L2> *__r
             out[base + pos] = lift_fast<L3>(q[i], K) & ~Key<L3>::from(7);
         }
     }
+}
+
+/*
+ * The sink / in-edge queries as 4 sorted arrays (one per label c of the querying edge).  The query of
+ * edge x is t = to_next(x, 0) (node a_2..a_K, label $), whose top char is x's label, and on the edges
+ * of one label to_next is monotone -- so the queries of label c, in edge order, are sorted, and the 4
+ * label classes occupy disjoint key ranges.  A stable split of the owned edges by label therefore
+ * yields the queries sorted, every owner's share is a contiguous slice of each class (found by
+ * binary search), and the owner receives 4 P sorted runs: its answering probes (query_join_kernel)
+ * join tiles of sorted queries against the edge range they span.
+ * One tile = SplitTraits::TILE edges.  The count pass reads the labels coalesced; the write pass
+ * loads the tile coalesced, ranks every edge inside its class (PER consecutive edges per thread, one
+ * block scan), permutes the queries in LDS and writes each class's run of the tile contiguously to
+ * toff[c * ntiles + tile] (class-major: the 4 sorted arrays back to back).  Per-thread scattered
+ * 8-byte stores instead (round 3, first cut): 16.6 ms for the write pass at configs[1]/2.
+ */
+template <int L>
+struct SplitTraits {
+    static constexpr int PER = L == 1 ? 16 : L == 2 ? 8 : 4;
+    static constexpr int TILE = 256 * PER;
+};
+
+template <int L, bool COUNT_ONLY>
+__global__ __launch_bounds__(256) void target_split_kernel(const Key<L> *__restrict__ E, uint64_t n, unsigned K,
+                                                          uint64_t ntiles, uint32_t *__restrict__ tcnt,
+                                                          const uint64_t *__restrict__ toff, Key<L> *__restrict__ out) {
+    constexpr int PER = SplitTraits<L>::PER, TILE = SplitTraits<L>::TILE;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)TILE, n - base);
+    if constexpr (COUNT_ONLY) {
+        __shared__ uint32_t s_t[4];
+        if (tid < 4) s_t[tid] = 0;
+        uint32_t cnt01 = 0, cnt23 = 0;  // 16-bit fields
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t i = j * 256 + tid;
+            if (i < tn) {
+                const uint32_t c = (uint32_t)(E[base + i].w[0] & 3);
+                if (c < 2) cnt01 += 1u << (16 * c); else cnt23 += 1u << (16 * (c - 2));
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            cnt01 += __shfl_xor(cnt01, off, 64);
+            cnt23 += __shfl_xor(cnt23, off, 64);
+        }
+        __syncthreads();
+        if (__lane_id() == 0) {
+            atomicAdd(&s_t[0], cnt01 & 0xFFFFu);
+            atomicAdd(&s_t[1], cnt01 >> 16);
+            atomicAdd(&s_t[2], cnt23 & 0xFFFFu);
+            atomicAdd(&s_t[3], cnt23 >> 16);
+        }
+        __syncthreads();
+        if (tid < 4) tcnt[(uint64_t)tid * ntiles + blockIdx.x] = s_t[tid];
+        return;
+    } else {
+        __shared__ Key<L> s_k[TILE];
+        __shared__ uint16_t s_dst[TILE];
+        __shared__ uint8_t s_lab[TILE];
+        __shared__ uint32_t s_scan[256 / 64 + 1];
+        Key<L> x[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t i = j * 256 + tid;
+            if (i < tn) {
+                x[j] = E[base + i];
+                s_lab[i] = (uint8_t)(x[j].w[0] & 3);
+            }
+        }
+        __syncthreads();
+        // thread tid ranks edges tid * PER .. + PER inside their classes
+        uint32_t lab = 0, cnt01 = 0, cnt23 = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t i = tid * PER + q;
+            const uint32_t c = i < tn ? s_lab[i] : 4u;
+            lab |= (c & 3u) << (2 * q);
+            if (c < 2) cnt01 += 1u << (16 * c); else if (c < 4) cnt23 += 1u << (16 * (c - 2));
+        }
+        uint32_t t01, t23;
+        const uint32_t o01 = block_exclusive_sum<256>(cnt01, s_scan, &t01);
+        const uint32_t o23 = block_exclusive_sum<256>(cnt23, s_scan, &t23);
+        // class starts inside the tile
+        const uint32_t cs1 = t01 & 0xFFFFu, cs2 = cs1 + (t01 >> 16), cs3 = cs2 + (t23 & 0xFFFFu);
+        uint32_t pos[4] = {o01 & 0xFFFFu, cs1 + (o01 >> 16), cs2 + (o23 & 0xFFFFu), cs3 + (o23 >> 16)};
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t i = tid * PER + q;
+            if (i < tn) {
+                const uint32_t c = (lab >> (2 * q)) & 3u;
+                const uint32_t p = c == 0 ? pos[0]++ : c == 1 ? pos[1]++ : c == 2 ? pos[2]++ : pos[3]++;
+                s_dst[i] = (uint16_t)p;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t i = j * 256 + tid;
+            if (i < tn) s_k[s_dst[i]] = routed_key<L, 0>(x[j], K);
+        }
+        __syncthreads();
+        const uint64_t g0 = toff[blockIdx.x], g1 = toff[ntiles + blockIdx.x] - cs1,
+                       g2 = toff[2 * ntiles + blockIdx.x] - cs2, g3 = toff[3 * ntiles + blockIdx.x] - cs3;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t sl = j * 256 + tid;
+            if (sl < tn) {
+                const uint64_t g = sl >= cs3 ? g3 : sl >= cs2 ? g2 : sl >= cs1 ? g1 : g0;
+                out[g + sl] = s_k[sl];
+            }
+        }
+    }
+}
+
+/*
+ * Owner side of the sink join over sorted query runs: query p = node (a_2..a_K) with label $ of
+ * some edge x anywhere.  The first edge of node p (lower bound of p among the owner's sorted
+ * edges) gets its in-edge mark -- x targets that node, so it needs no dummy source (:148-166); a
+ * miss means x's target node has no out-edge and needs a dummy sink (:80-95): qflag = 1.
+ * A workgroup takes JoinTraits::TILE consecutive queries.  Inside one sorted run they span a short
+ * key range [min, max]; the edges of its buckets are staged in LDS (coalesced) and every probe
+ * binary-searches them there.  A tile whose range does not fit (it straddles two runs, or the
+ * edges are dense there) binary-searches the bucketed global array instead.
+ */
+template <int L>
+struct JoinTraits {
+    static constexpr int PER = L == 1 ? 4 : 2;
+    static constexpr int TILE = 256 * PER;
+    static constexpr int CAP = TILE * 5 / 4;
+};
+
+template <int L>
+__device__ __forceinline__ Key<L> wave_min_key(Key<L> v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        Key<L> o;
+#pragma unroll
+        for (int w = 0; w < L; ++w) o.w[w] = __shfl_xor(v.w[w], off, 64);
+        if (o < v) v = o;
+    }
+    return v;
+}
+
+template <int L>
+__device__ __forceinline__ Key<L> wave_max_key(Key<L> v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        Key<L> o;
+#pragma unroll
+        for (int w = 0; w < L; ++w) o.w[w] = __shfl_xor(v.w[w], off, 64);
+        if (v < o) v = o;
+    }
+    return v;
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void query_join_kernel(const Key<L> *__restrict__ keys, uint64_t n,
+                                                         const uint64_t *__restrict__ start, unsigned bshift,
+                                                         const Key<L> *__restrict__ q, uint64_t nq,
+                                                         uint8_t *__restrict__ in_flag, uint8_t *__restrict__ qflag) {
+    using T = JoinTraits<L>;
+    constexpr int PER = T::PER;
+    __shared__ Key<L> s_r[T::CAP];
+    __shared__ Key<L> s_mm[8];
+    __shared__ uint64_t s_a;
+    __shared__ uint32_t s_cnt;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * T::TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)T::TILE, nq - base);
+    const uint32_t j0 = tid * PER;
+    Key<L> x[PER];
+    Key<L> mn = ~Key<L>::zero(), mx = Key<L>::zero();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        x[k] = Key<L>::zero();
+        if (j0 + k < tn) {
+            x[k] = q[base + j0 + k];
+            if (x[k] < mn) mn = x[k];
+            if (mx < x[k]) mx = x[k];
+        }
+    }
+    mn = wave_min_key<L>(mn);
+    mx = wave_max_key<L>(mx);
+    if (__lane_id() == 0) {
+        s_mm[tid / 64] = mn;
+        s_mm[4 + tid / 64] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        Key<L> a = s_mm[0], b = s_mm[4];
+        for (int w = 1; w < 4; ++w) {
+            if (s_mm[w] < a) a = s_mm[w];
+            if (b < s_mm[4 + w]) b = s_mm[4 + w];
+        }
+        uint32_t cnt = ~0u;
+        uint64_t lo = 0;
+        if (n) {
+            const uint64_t blo = bits_at(shr(a, bshift), 0, 32), bhi = bits_at(shr(b | Key<L>::from(3), bshift), 0, 32);
+            lo = start[blo];
+            const uint64_t hi = start[bhi + 1];
+            if (hi - lo <= (uint64_t)T::CAP) cnt = (uint32_t)(hi - lo);
+        }
+        s_a = lo;
+        s_cnt = cnt;
+    }
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    const uint64_t a = s_a;
+    if (cnt != ~0u) {
+        for (uint32_t j = tid; j < cnt; j += 256) s_r[j] = keys[a + j];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (j0 + k >= tn) continue;
+        const Key<L> p = x[k];
+        uint64_t hit = ~0ull;
+        if (!n) {
+        } else if (cnt != ~0u) {
+            uint32_t lo = 0, hi = cnt;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_r[mid] < p) lo = mid + 1; else hi = mid;
+            }
+            if (lo < cnt && shr(s_r[lo], 2) == shr(p, 2)) hit = a + lo;
+        } else {
+            const uint64_t i = lower_bound_bucketed(keys, start, bshift, p);
+            if (i < n && shr(keys[i], 2) == shr(p, 2)) hit = i;
+        }
+        if (hit != ~0ull) in_flag[hit] = 1;
+        qflag[base + j0 + k] = hit == ~0ull ? 1 : 0;
+    }
+}
+
+// first query index of every owner in every class: out[c * (P + 1) + j] = lower bound of the prefix
+// bounds[j] in the sorted class array [cstart[c], cstart[c + 1])
+template <int L>
+__global__ void class_bounds_kernel(const Key<L> *__restrict__ q, const uint64_t *__restrict__ cstart,
+                                    const uint64_t *__restrict__ bounds, uint32_t P, unsigned pshift,
+                                    uint64_t *__restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 4 * (P + 1)) return;
+    const uint32_t c = t / (P + 1), j = t % (P + 1);
+    uint64_t lo = cstart[c], hi = cstart[c + 1];
+    const uint64_t b = bounds[j];
+    while (lo < hi) {  // first query whose owner prefix is >= b
+        const uint64_t mid = (lo + hi) >> 1;
+        if (bits_at(shr(q[mid], pshift), 0, 32) < b) lo = mid + 1; else hi = mid;
+    }
+    out[t] = lo;
 }
 
 }  // namespace mtg

@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--k", type=int, default=31)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--no-single", action="store_true", help="skip the single build (profiling the ranks only)")
+    ap.add_argument("--serial", action="store_true",
+                    help="one rank owns the device at a time (MTG_LOCAL_SERIAL): the step is the SUM of the "
+                         "ranks' work, and each rank's device time is measured alone")
+    ap.add_argument("--only-single", action="store_true", help="the single build only (its kernel profile)")
     args = ap.parse_args()
     import torch
     boss = importlib.import_module("projects2014-metagenome_amd.boss")
@@ -49,7 +53,12 @@ def main():
         t_single = (time.perf_counter() - t0) / args.steps
         ts = single.timings().as_dict()
         rows_single = dc.n
+    if args.only_single:
+        print(json.dumps({"single_ms": t_single * 1e3, "rows": rows_single}))
+        return
 
+    if args.serial:
+        os.environ["MTG_LOCAL_SERIAL"] = "1"
     comms = boss.Comm.local_group(P)
     ctors = [boss.IBOSSChunkConstructor.initialize(kb, both_strands=True) for _ in range(P)]
     res = [None] * P
@@ -66,6 +75,8 @@ def main():
 
     step()
     step()
+    for cm in comms:
+        cm.held_ms(reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -73,11 +84,17 @@ def main():
     rows_dist = sum(c.n for c in res) - (P - 1)
     assert rows_single is None or rows_dist == rows_single, (rows_dist, rows_single)
     per_rank = [c.timings().as_dict() for c in ctors]
+    held = [cm.held_ms() / args.steps for cm in comms]
     keys = ("extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms", "merge_ms", "emit_ms",
             "total_ms", "exchange_ms")
     print(json.dumps({
         "ranks": P, "reads_per_rank": args.reads, "rows": rows_single,
-        "single_ms": t_single * 1e3, "dist_wall_ms": t_dist * 1e3,
+        "single_ms": t_single * 1e3, "dist_wall_ms": t_dist * 1e3, "serial": args.serial,
+        # serial mode: each rank's device time alone; work ratio = their sum / the single build, and
+        # the weak-scaling estimate P * single(P reads) / (P * max rank) = P / (P * max / single)
+        "rank_held_ms": [round(h, 2) for h in held] if args.serial else None,
+        "work_ratio": round(sum(held) / (t_single * 1e3), 3) if args.serial and t_single else None,
+        "max_rank_ratio": round(P * max(held) / (t_single * 1e3), 3) if args.serial and t_single else None,
         "single_stages": {k: round(ts[k], 2) for k in keys if k in ts},
         "rank_stages": [{k: round(t[k], 2) for k in keys} for t in per_rank],
         "n_sent": [t["n_sent"] for t in per_rank],
