@@ -22,6 +22,32 @@ __host__ __device__ __forceinline__ uint32_t encode_dna(uint32_t c) {
     return idx > 20u ? 4u : (uint32_t)(TAB >> (3u * idx)) & 7u;
 }
 
+// Which strand a canonical window keeps.  canonical == 1: the smaller key (kmer_extractor.cpp:165-196).
+// canonical == 2 (the routed multi-GPU collect, boss_pipeline.hip: dist_collect_routed): the strand
+// whose top 12 key bits hash smaller, the smaller key when the tops tie.  Every {x, rc(x)} pair still
+// has one representative and the chunk is the same (the real edges are both strands, counts follow
+// the pair), but the representatives spread over the key space like the real edges instead of
+// piling into the low prefixes, so one range partition balances the collect and the later stages.
+// A tie keeps the top either way, so the 12-bit histograms of pass A need only the tops.
+__host__ __device__ __forceinline__ uint32_t top_hash12(uint32_t t) {
+    t = (t + 0x9e3779b9u) * 0x85ebca6bu;
+    t ^= t >> 13;
+    t *= 0xc2b2ae35u;
+    return t ^ (t >> 16);
+}
+__host__ __device__ __forceinline__ bool take_rc_top(int canonical, uint32_t ftop, uint32_t rtop) {
+    if (canonical == 2) return ftop != rtop && top_hash12(rtop) < top_hash12(ftop);
+    return canonical && rtop < ftop;
+}
+template <int L>
+__device__ __forceinline__ bool take_rc(int canonical, const Key<L> &f, const Key<L> &r, unsigned K) {
+    if (canonical == 2) {
+        const uint32_t tf = (uint32_t)bits_at(shr(f, 2 * K - 12), 0, 12), tr = (uint32_t)bits_at(shr(r, 2 * K - 12), 0, 12);
+        if (tf != tr) return top_hash12(tr) < top_hash12(tf);
+    }
+    return canonical && r < f;
+}
+
 template <int L>
 struct ExtractTraits {
     static constexpr int PPT = L == 4 ? 8 : 16;  // positions per thread
@@ -73,7 +99,7 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
                     Key<L> f = plain_to_boss(P, K, low);
                     if (canonical) {
                         Key<L> r = plain_to_boss(R, K, low);
-                        if (r < f) f = r;
+                        if (take_rc(canonical, f, r, K)) f = r;
                     }
                     kk[j] = f;
                     if (COUNTED) {

@@ -28,6 +28,7 @@
 #include "comm.hpp"
 #include "dbg_io.hpp"
 #include "dist_kernels.hpp"
+#include "superkmer.hpp"
 #include "extract_partition.hpp"
 #include "fasta.hpp"
 #include "range_extract.hpp"
@@ -61,7 +62,9 @@ class Workspace {
         // multi-GPU build: exchange buffers, routing and the query join
         XA, XAC, XB, XBC, XHIST, XSTART_A, XSTART_B, XMAT, BOUNDS, RTCNT, RTOFF, XGATHER, QSEND, QRECV,
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
-        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS, NSLOTS
+        LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
+        SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
+        SK_STARTS, SK_RID, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -168,6 +171,9 @@ struct Ctx {
     double fused_ms = 0;           // device time of the last fused extract+partition launch
     bool fused_emit = true;        // MTG_FUSED_EMIT=0: K7 writes the lifted stream, K8 reads it (the
                                    // redundant-sink path)
+    bool routed_min = false;       // MTG_ROUTED_CANON=min: the routed collect keeps min(fwd, rc)
+    int dist_collect = 1;          // MTG_DIST_COLLECT: 1 routed keys (default), 0 super-k-mers
+                                   // (=superkmer), 2 local collect + exchange of sorted runs (=local)
     bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
                                    // dense u64 ranks (dummy_encode_kernel)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
@@ -192,6 +198,8 @@ static void load_knobs(Ctx &c) {
     c.fused = !is("MTG_FUSED", "0");
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
+    c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
+    c.routed_min = is("MTG_ROUTED_CANON", "min");
     c.force_spill = is("MTG_SPILL", "1");
     c.debug = getenv("MTG_DEBUG") != nullptr;
     c.trace = getenv("MTG_TRACE") != nullptr;
@@ -1950,6 +1958,9 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     // the same on every rank (no input-size test: a rank may hold no reads)
     if (!c.fused || c.use_lsd || K - 1 < FUSED_HB / 2 || K > 32 || c.force_ranges) return false;
     constexpr unsigned OB = 8;   // owner-range prefix bits (4 node chars: whole chars for the lifted bounds)
+    // canonical windows keep the strand whose key top hashes smaller (boss_kernels.hpp: take_rc): the
+    // owners' canonical keys then follow the real edges, and one set of ranges balances both
+    const int cmode = canonical ? (c.routed_min || d.P == 1 ? 1 : 2) : 0;
     constexpr unsigned B1 = 9;   // pass B's scatter digit
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     c.timings.n_positions = npos;
@@ -1972,7 +1983,7 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, 2 * NBH * 4);
     HIP_CHECK(hipMemsetAsync(h12, 0, 2 * NBH * 4, c.stream));
     if (nrows) {
-        extract_hist_fast_kernel<true><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+        extract_hist_fast_kernel<true><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, cmode,
                                                                              tiles, per_row, rows, rows_o);
         HIP_CHECK(hipGetLastError());
         hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(NBH, 256)), dim3(256), 0,
@@ -2044,12 +2055,12 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
         HIP_CHECK(hipGetLastError());
         if (!COUNTED) {
             extract_partition_fast_kernel<512><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), 0,
-                                                  c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, B1, per_stripe,
+                                                  c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
                                                               scur, send, ka, &c.small->error);
         } else {
             const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
             extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
+                in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
                 B1, per_stripe, scur, send, ka, ca, &c.small->error);
         }
         HIP_CHECK(hipGetLastError());
@@ -2121,6 +2132,115 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     return true;
 }
 
+// ------------------------------------------------ multi-GPU: exchange 0, super-k-mers (superkmer.hpp)
+//
+// Every rank's windows go to their collect owner (a hash of the window's canonical minimizer) as
+// 2-bit packed runs; *out becomes the owner's input: the received runs unpacked into a read buffer
+// (each run one read, carrying its read's count).  The owner's collect then extracts, sorts and
+// dedupes each k-mer exactly once in the whole job, and its distinct keys are disjoint from every
+// other owner's.  Returns false where the path does not apply (the caller collects its own reads).
+static bool dist_superkmers(Ctx &c, Dist &d, unsigned K, bool canonical, const BuildInput &in, BuildInput *out,
+                            Tracer &tr) {
+    if (c.dist_collect != 0 || d.P < 2 || d.P > SK_MAX_OWNERS || K < 20 || K + 16 > (unsigned)SK_KMAX) return false;
+    const unsigned M = std::min(11u, K - 12);
+    const uint32_t P = (uint32_t)d.P;
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    const uint64_t ntiles = ceil_div(npos, SK_TILE);
+    const bool per_read = in.read_counts != nullptr;
+    std::vector<std::vector<uint64_t>> soff_r(1, std::vector<uint64_t>(P + 1, 0)), soff_w(1, std::vector<uint64_t>(P + 1, 0));
+    uint64_t *words = nullptr;
+    uint32_t *nwords = nullptr, *cnt = nullptr;
+    if (npos) {
+        uint8_t *own = (uint8_t *)c.ws.get(Workspace::SK_OWN, npos + 16);
+        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::SK_TCNT, (2 * P * ntiles + 1) * 4);
+        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::SK_TOFF, (2 * P * ntiles + 2) * 8);
+        uint64_t *toffw = toff + P * ntiles + 1;
+        sk_owner_kernel<<<dim3((unsigned)ntiles), dim3(SK_BLOCK), 0, c.stream>>>(in.seq, in.seq_len, K, M,
+                                                                               canonical ? 1 : 0, P, own);
+        HIP_CHECK(hipGetLastError());
+        sk_runs_kernel<true><<<dim3((unsigned)ntiles), dim3(SK_BLOCK), 0, c.stream>>>(
+            own, npos, in.seq, K, P, ntiles, tcnt, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+            nullptr);
+        HIP_CHECK(hipGetLastError());
+        for (int half = 0; half < 2; ++half) {
+            uint32_t ep;
+            const uint64_t st = ceil_div(P * ntiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(
+                tcnt + half * P * ntiles, P * ntiles, half ? toffw : toff, desc, ep, &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+        }
+        uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, 2 * (P + 1) * 8);
+        gather_strided_kernel<<<1, 256, 0, c.stream>>>(toff, ntiles, P + 1, g);
+        gather_strided_kernel<<<1, 256, 0, c.stream>>>(toffw, ntiles, P + 1, g + P + 1);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(soff_r[0].data(), g, (P + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(soff_w[0].data(), g + P + 1, (P + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        const uint64_t nruns = soff_r[0][P], nwtot = soff_w[0][P];
+        words = (uint64_t *)c.ws.get(Workspace::SK_WORDS, std::max<uint64_t>(nwtot, 1) * 8);
+        if (per_read) {
+            nwords = (uint32_t *)c.ws.get(Workspace::SK_LENS, std::max<uint64_t>(nruns, 1) * 4);
+            cnt = (uint32_t *)c.ws.get(Workspace::SK_CNT, std::max<uint64_t>(nruns, 1) * 4);
+        }
+        sk_runs_kernel<false><<<dim3((unsigned)ntiles), dim3(SK_BLOCK), 0, c.stream>>>(
+            own, npos, in.seq, K, P, ntiles, nullptr, toff, toffw, in.read_starts, in.read_counts, in.n_reads,
+            in.rid_at, words, nwords, cnt);
+        HIP_CHECK(hipGetLastError());
+    }
+    tr("super-k-mers", soff_r[0][P], soff_w[0][P]);
+    uint64_t *rwords = nullptr;
+    uint32_t *rnw = nullptr, *rcnt = nullptr, *unused = nullptr;
+    const uint64_t *wa[1] = {words};
+    const uint64_t nw = exchange_runs<uint64_t>(c, d, 1, wa, nullptr, soff_w, Workspace::SK_RWORDS, Workspace::SK_RCNT,
+                                                &rwords, &unused);
+    uint64_t nr = 0;
+    if (per_read) {
+        const uint32_t *la[1] = {nwords};
+        const uint32_t *ca[1] = {cnt};
+        nr = exchange_runs<uint32_t>(c, d, 1, la, ca, soff_r, Workspace::SK_RLENS, Workspace::SK_RCNT, &rnw, &rcnt);
+    }
+    tr("exchange 0", nr, nw);
+    // the received words -> a read buffer of 28 bytes per word (every run ends in a separator)
+    *out = BuildInput{};
+    uint8_t *seq = (uint8_t *)c.ws.get(Workspace::SK_SEQ, std::max<uint64_t>(SK_WCH * nw, 4));
+    if (nw) {
+        sk_unpack_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(nw, 256), 65536)), dim3(256), 0, c.stream>>>(
+            rwords, nw, (uint32_t *)seq);
+        HIP_CHECK(hipGetLastError());
+    }
+    out->seq = seq;
+    out->seq_len = SK_WCH * nw;
+    if (per_read && nr) {
+        uint64_t *wstart = (uint64_t *)c.ws.get(Workspace::SK_WOFF, (nr + 1) * 8);
+        uint64_t *starts = (uint64_t *)c.ws.get(Workspace::SK_STARTS, nr * 8);
+        uint32_t ep;
+        const uint64_t st = ceil_div(nr, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(rnw, nr, wstart, desc, ep, &c.small->counter,
+                                                                          &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        if (read_u64(c, (const unsigned long long *)(wstart + nr)) != nw)
+            throw std::runtime_error("received super-k-mer words differ from their runs' word counts");
+        const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(nr, 256), 16384);
+        sk_starts_kernel<<<dim3(g), dim3(256), 0, c.stream>>>(wstart, nr, starts);
+        HIP_CHECK(hipGetLastError());
+        out->read_starts = starts;
+        out->read_counts = rcnt;
+        out->n_reads = nr;
+        if (nr > 1) {
+            const uint64_t nq = (out->seq_len >> RID_SHIFT) + 2;
+            uint64_t *rid = (uint64_t *)c.ws.get(Workspace::SK_RID, nq * 8);
+            read_index_kernel<<<dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, c.stream>>>(starts, nr, nq, rid);
+            HIP_CHECK(hipGetLastError());
+            out->rid_at = rid;
+        }
+    }
+    return true;
+}
+
 template <int L2, int L3, bool COUNTED>
 static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, unsigned bits,
                               const BuildInput &in, BuildOutput *out) {
@@ -2168,18 +2288,27 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         uint32_t *xac = nullptr;
         std::vector<uint64_t> b1;
         bool routed = false;
+        // exchange 0: the windows to their collect owners as super-k-mers (the collect below then runs
+        // on the received runs); else the routed collect, else every rank collects its own reads
+        BuildInput sk_in{};
+        const bool sk = dist_superkmers(c, d, K, canonical, in, &sk_in, tr);
         if constexpr (L2 == 1)  // the fused extraction routes every k-mer to its owner
-            routed = dist_collect_routed<COUNTED>(c, d, K, canonical, cmax, in, &xa, &xac, &T.n_unique, &b1, tr, tm,
-                                                  &ev_extract, &ev_sort);
+            if (!sk && c.dist_collect != 2)
+                routed = dist_collect_routed<COUNTED>(c, d, K, canonical, cmax, in, &xa, &xac, &T.n_unique, &b1, tr, tm,
+                                                      &ev_extract, &ev_sort);
         if (!routed) {
+        const BuildInput &cin = sk ? sk_in : in;
         // ---- K1-K3 on this rank's reads
         K2 *ka, *kb;
         uint32_t *ca, *cb;
         uint64_t N = 0;
         double dup = 0;
         const uint32_t *hist1 = nullptr;
-        if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
-            N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
+        if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+            N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb);
+        if (sk) {  // the windows of this rank's reads, not of the received runs
+            T.n_positions = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+        }
         ev_extract = tm.mark();
         tr("extract", N);
         const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);

@@ -161,8 +161,9 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
             const uint32_t r = (sr >= 64 ? (q2 >> (sr - 64)) : __builtin_amdgcn_alignbit(q2, q1, sr - 32)) & (NB - 1);
             const bool ok = (uint32_t)j < nwin && ((inv >> j) & maskK) == 0;
             if (ok) {
-                atomicAdd(&s_h[canonical && r < f ? r : f], 1u);
-                if (OTHER) atomicAdd(&s_o[canonical && r < f ? f : r], 1u);
+                const bool rc = take_rc_top(canonical, f, r);
+                atomicAdd(&s_h[rc ? r : f], 1u);
+                if (OTHER) atomicAdd(&s_o[rc ? f : r], 1u);
             }
         }
     }
@@ -351,7 +352,10 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
         if (j) R = ((R << 2) | (3u - ((E >> (2 * (j - 1))) & 3u))) & maskP;
         const uint64_t f = ((P & lowNode) << 2) | (P >> sh);
         const uint64_t r = ((R & lowNode) << 2) | (R >> sh);
-        kk[j] = canonical && r < f ? r : f;
+        const bool rc = canonical == 2 ? take_rc_top(2, (uint32_t)(f >> (2 * K - 12)), (uint32_t)(r >> (2 * K - 12))) ||
+                                             ((f >> (2 * K - 12)) == (r >> (2 * K - 12)) && r < f)
+                                       : canonical && r < f;
+        kk[j] = rc ? r : f;
         m |= (uint32_t)((uint32_t)j < nwin && ((inv >> j) & maskK) == 0) << j;
     }
     const unsigned bshift = 2 * K - b;

@@ -100,6 +100,28 @@ def test_dist_counts_saturate_across_ranks():
             check_dist(11, seqs, 4, canonical, bits, counts)
 
 
+def test_dist_superkmer_read_counts(monkeypatch):
+    # exchange 0 carries every run's read count: per-read counts of k >= 19 builds go through it
+    monkeypatch.setenv("MTG_DIST_COLLECT", "superkmer")
+    rng = np.random.default_rng(12)
+    seqs = _random_reads(13, 1500, 150, 9000, n_rate=0.003, lower=True)
+    counts = rng.integers(1, 90, size=len(seqs)).tolist()
+    for k, P, canonical, bits in ((25, 4, True, 8), (40, 3, False, 16), (19, 8, True, 4)):
+        check_dist(k, seqs, P, canonical, bits, counts)
+
+
+@pytest.mark.parametrize("env", [{"MTG_DIST_COLLECT": "superkmer"}, {"MTG_DIST_COLLECT": "local"},
+                                 {"MTG_ROUTED_CANON": "min"}])
+def test_dist_collect_modes(monkeypatch, env):
+    # every collect of the multi-GPU build (MTG_DIST_COLLECT; the routed default with min(fwd, rc)
+    # canonical keys instead of the hashed-top choice) is exact
+    for name, v in env.items():
+        monkeypatch.setenv(name, v)
+    reads = _random_reads(21, 2000, 150, 20000, n_rate=0.005, lower=True)
+    for k, P, canonical, bits in ((30, 3, True, 8), (31, 2, False, 0), (19, 4, True, 16)):
+        check_dist(k, reads, P, canonical, bits)
+
+
 def test_dist_empty_and_lopsided_ranks():
     reads = _random_reads(5, 300, 150, 3000)
     for P in (2, 5, 8):
