@@ -286,7 +286,9 @@ int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64
  * weights (node_weights.cpp:62-68).  graph_mode: 0 basic, 1 canonical.  suffix_length < 0 = the
  * build's default min(10, k).  *n_valid (may be NULL) = edges left valid by the mask (`nodes (k)` of
  * `metagraph stats`), else n - 1.  Host code: needs no device.  The sdsl-lite containers inside are
- * restated (their bytes are unpinned); mtg_boss_read_dbg reads exactly this layout.
+ * restated (their bytes are unpinned); mtg_boss_read_dbg reads exactly this layout, and a
+ * reference `metagraph` binary must NOT be given these files (it would pass the framing checks and
+ * misread W and last).
  */
 int mtg_boss_write_dbg(const mtg_boss_chunk *chunk, const char *outbase, int graph_mode, int mask_dummy,
                        int64_t suffix_length, uint64_t *n_valid);

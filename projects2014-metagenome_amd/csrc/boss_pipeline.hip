@@ -111,6 +111,7 @@ struct Small {  // one device word block, zeroed per use
     uint32_t root_same;
     uint32_t bad_dummy;
     uint32_t bruns;  // bucket_index: listed long runs
+    uint32_t fasta_bad;  // fasta_split_kernel: a '+' sequence line
     uint32_t error;
 };
 
@@ -3408,22 +3409,29 @@ static void split_fasta_files(mtg_boss_ctor *c, uint8_t *dseq, uint64_t *seq_bas
         HIP_CHECK(hipGetLastError());
         fasta_prefix_kernel<<<1, 1024, 0, s>>>(tlast, ta, nullptr, nt, prev, oa, nullptr);  // prev nl, lines
         HIP_CHECK(hipGetLastError());
-        const uint64_t fh = f.fastq ? 0 : f.first_header;
+        const uint64_t fh = f.first_header;
+        HIP_CHECK(hipMemsetAsync(&x.small->fasta_bad, 0, 4, s));
         fasta_split_kernel<false><<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(
-            raw, n, f.fastq ? 1 : 0, fh, prev, oa, ta, tb, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0);
+            raw, n, f.fastq ? 1 : 0, fh, prev, oa, ta, tb, nullptr, nullptr, nullptr, 0, nullptr, nullptr, 0,
+            f.lines_before, &x.small->fasta_bad);
         HIP_CHECK(hipGetLastError());
         uint64_t *koff = (uint64_t *)x.ws.get(Workspace::FA_KOFF, (nt + 1) * 8);
         fasta_prefix_kernel<<<1, 1024, 0, s>>>(nullptr, ta, tb, nt, nullptr, koff, ob);
         HIP_CHECK(hipGetLastError());
         uint64_t tot[2];
+        uint32_t bad = 0;
         HIP_CHECK(hipMemcpyAsync(&tot[0], koff + nt, 8, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipMemcpyAsync(&tot[1], ob + nt, 8, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipMemcpyAsync(&bad, &x.small->fasta_bad, 4, hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
+        if (bad)
+            throw std::runtime_error("ERROR: " + f.path + ": a FASTA sequence line starts with '+' (FASTQ quality in a "
+                                     "FASTA record) -- not supported");
         if (!count_only) {
             // the line-number prefix `oa` is still valid: the second prefix wrote koff / ob
             fasta_split_kernel<true><<<dim3((unsigned)nt), dim3(FA_BLOCK), 0, s>>>(
                 raw, n, f.fastq ? 1 : 0, fh, prev, oa, nullptr, nullptr, koff, ob, dseq, *seq_base, rstarts,
-                rcounts, *read_base);
+                rcounts, *read_base, f.lines_before, nullptr);
             HIP_CHECK(hipGetLastError());
             const uint8_t sep = '$';  // the last record's separator
             HIP_CHECK(hipMemcpyAsync(dseq + *seq_base + tot[0], &sep, 1, hipMemcpyHostToDevice, s));

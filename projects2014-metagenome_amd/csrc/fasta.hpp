@@ -12,9 +12,12 @@
 //             bytes it keeps and the records it starts;
 //   write  -- the kept bytes at the tile's scanned offset, '$' for every record boundary, and the
 //             read starts (for per-read counts).
-// Record rules (kseq): FASTA -- a line starting with '>' is a header, every other line belongs to
-// the current record's sequence, '\n' and '\r' are dropped (kseq strips line ends), bytes before
-// the first header are skipped; FASTQ -- four-line records ('@' header, sequence, '+', quality).
+// Record rules (kseq's kseq_read): FASTA -- a line starting with '>' or '@' is a header, every other
+// line belongs to the current record's sequence, '\n' and a '\r' right before it are dropped (a
+// '\r' inside a line stays a sequence byte, which breaks k-mer windows like any invalid char), bytes
+// before the first header are skipped; a sequence line starting with '+' (kseq would read FASTQ
+// quality lines there) is refused with an error.  FASTQ -- four-line records ('@' header, sequence,
+// '+', quality) counted from the first '@' (blank lines before it are skipped).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -44,7 +47,9 @@ struct FastaInput {
     char *data = nullptr;
     uint64_t size = 0;
     bool fastq = false;
-    uint64_t first_header = 0;  // FASTA: the first '>' at a line start (bytes before it are skipped)
+    uint64_t first_header = 0;  // FASTA: the first '>' at a line start; FASTQ: the first '@' (bytes
+                                // before it are skipped)
+    uint64_t lines_before = 0;  // FASTQ: newlines before first_header (the 4-line phase starts there)
     std::string path;
 };
 
@@ -126,7 +131,10 @@ inline FastaInput load_fasta_file(const std::string &path) {
     uint64_t i = 0;
     while (i < size && (buf[i] == '\n' || buf[i] == '\r' || buf[i] == ' ')) ++i;
     in.fastq = i < size && buf[i] == '@';
-    if (!in.fastq) {  // the first header: almost always byte 0, else a host scan
+    if (in.fastq) {
+        in.first_header = i;
+        for (uint64_t p = 0; p < i; ++p) in.lines_before += buf[p] == '\n';
+    } else {  // the first header: almost always byte 0, else a host scan
         uint64_t p = 0;
         while (p < size && !(buf[p] == '>' && (p == 0 || buf[p - 1] == '\n'))) {
             const void *nl = std::memchr(buf + p, '\n', size - p);
@@ -250,17 +258,20 @@ __device__ __forceinline__ void fa_load(const uint8_t *__restrict__ raw, uint64_
 }
 
 /*
- * count (WRITE = false) and write passes over the same tiles.  Per byte: FASTA -- skipped before
- * the first header; a header line writes '$' at its '>' (a record starts after it) and nothing
- * else; sequence lines write every byte but '\n' / '\r'.  FASTQ -- line r = 1 (mod 4) writes its
- * bytes but '\r', and '$' for its '\n'; the '\n' of a header line (r = 0) starts a record.
+ * count (WRITE = false) and write passes over the same tiles.  Per byte: skipped before the first
+ * header.  FASTA -- a header line writes '$' at its '>' / '@' (a record starts after it) and
+ * nothing else; sequence lines write every byte but '\n' and a '\r' before '\n' (or at the end);
+ * a sequence line starting with '+' raises *bad (count pass).  FASTQ -- line r = 1 (mod 4, counted
+ * from the first '@' line) writes its bytes but a line-ending '\r', and '$' for its '\n'; the '\n'
+ * of a header line (r = 0) starts a record.
  */
 template <bool WRITE>
 __global__ __launch_bounds__(FA_BLOCK) void fasta_split_kernel(
     const uint8_t *__restrict__ raw, uint64_t n, int fastq, uint64_t first_hdr, const int64_t *__restrict__ prev_nl,
     const uint64_t *__restrict__ nl_off, uint32_t *__restrict__ tkeep, uint32_t *__restrict__ tstart,
     const uint64_t *__restrict__ keep_off, const uint64_t *__restrict__ start_off, uint8_t *__restrict__ out,
-    uint64_t out_base, uint64_t *__restrict__ rstarts, uint32_t *__restrict__ rcounts, uint64_t read_base) {
+    uint64_t out_base, uint64_t *__restrict__ rstarts, uint32_t *__restrict__ rcounts, uint64_t read_base,
+    uint64_t line_base, uint32_t *__restrict__ bad) {
     constexpr int NW = FA_PER / 4;
     __shared__ int64_t s_last[FA_BLOCK];
     __shared__ uint32_t s_scan[FA_BLOCK / 64 + 1];
@@ -293,7 +304,9 @@ __global__ __launch_bounds__(FA_BLOCK) void fasta_split_kernel(
     uint32_t tot;
     const uint32_t nl_before = block_exclusive_sum<FA_BLOCK>(nls, s_scan, &tot);
     uint64_t line = fastq ? nl_off[t] + nl_before : 0;
-    bool hdr = !fastq && (uint64_t)(cur + 1) < n && raw[cur + 1] == '>';  // the current line's kind
+    auto is_hdr = [](uint32_t ch) { return ch == '>' || ch == '@'; };
+    bool hdr = !fastq && (uint64_t)(cur + 1) < n && is_hdr(raw[cur + 1]);  // the current line's kind
+    bool plus = false;
     uint32_t ev[NW];
     uint32_t keep = 0, starts = 0, stmask = 0;
 #pragma unroll
@@ -305,18 +318,22 @@ __global__ __launch_bounds__(FA_BLOCK) void fasta_split_kernel(
         const uint32_t ch = byte(j);
         uint32_t e = 0;
         bool st = false;
-        if (fastq) {
-            const uint64_t r = line & 3;
-            if (r == 1) e = ch == '\n' ? (uint32_t)'$' : (ch == '\r' ? 0u : ch);
+        // a '\r' that ends its line is dropped with the '\n'; any other '\r' is a sequence byte
+        const bool cr_end = ch == '\r' && (j + 1 < FA_PER ? byte(j + 1) : (i + 1 < n ? (uint32_t)raw[i + 1] : (uint32_t)'\n')) == '\n';
+        if (i < first_hdr) {
+        } else if (fastq) {
+            const uint64_t r = (line - line_base) & 3;
+            if (r == 1) e = ch == '\n' ? (uint32_t)'$' : (cr_end ? 0u : ch);
             else if (r == 0 && ch == '\n') st = true;
-        } else if (i >= first_hdr) {
+        } else {
             if (hdr) {
                 if (i == (uint64_t)(cur + 1)) {
                     e = '$';
                     st = true;
                 }
-            } else if (ch != '\n' && ch != '\r') {
-                e = ch;
+            } else {
+                if (ch == '+' && i == (uint64_t)(cur + 1)) plus = true;
+                if (ch != '\n' && !cr_end) e = ch;
             }
         }
         ev[j >> 2] |= e << (8 * (j & 3));
@@ -326,13 +343,14 @@ __global__ __launch_bounds__(FA_BLOCK) void fasta_split_kernel(
         if (ch == '\n') {
             cur = (int64_t)i;
             ++line;
-            if (!fastq) hdr = i + 1 < n && (j + 1 < FA_PER ? byte(j + 1) : (uint32_t)raw[i + 1]) == '>';
+            if (!fastq) hdr = i + 1 < n && is_hdr(j + 1 < FA_PER ? byte(j + 1) : (uint32_t)raw[i + 1]);
         }
     }
     uint32_t ktot, stot;
     const uint32_t koff = block_exclusive_sum<FA_BLOCK>(keep, s_scan, &ktot);
     const uint32_t soff = block_exclusive_sum<FA_BLOCK>(starts, s_scan, &stot);
     if constexpr (!WRITE) {
+        if (plus && bad) atomicOr(bad, 1u);
         if (tid == 0) {
             tkeep[t] = ktot;
             tstart[t] = stot;

@@ -21,6 +21,7 @@
 
 namespace mtg {
 
+
 constexpr int MSD_BLOCK = 512;
 constexpr int MSD_WIN = 2;    // previous-level segments a tile keeps in its LDS window
 constexpr int MSD_DBITS = 9;  // widest digit of one partition level
@@ -391,6 +392,16 @@ __device__ __forceinline__ uint32_t key_hash(const Key<L> &k) {
     return (uint32_t)(h >> 32);
 }
 
+// a 32-bit hash onto [0, N): a mask for a power of two, else the high half of hash * N.  (A 3072-slot
+// table with 384-thread workgroups -- 5 groups per CU instead of 4 -- measured slower for the configs[1]
+// sort: 11.5 vs 10.4 ms sort stage; so was a persistent kernel loading the next group's keys while
+// the current group sorts: 12.3-14.2 ms for 2-4 workgroups per CU.)
+template <int N>
+__device__ __forceinline__ uint32_t slot_of(uint32_t h) {
+    if constexpr ((N & (N - 1)) == 0) return h & (N - 1);
+    else return (uint32_t)(((uint64_t)h * (uint64_t)N) >> 32);
+}
+
 // atomicMax of a block-uniform LDS word from every lane, reduced over the wave first so that one lane
 // issues the atomic: a uniform-address atomic from all lanes becomes the atomic optimizer's lane-by-
 // lane loop (~5 scalar instructions per active lane; 0.8 ms of local_unique_kernel and 0.5 ms of
@@ -547,23 +558,21 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             }
 #pragma unroll
             for (int q = 0; q < BATCH * PAIR; ++q) {
-                if (!hv[q] || ovf) continue;
+                // LIST: the new keys of a wave take their list positions by ballot after the probe
+                // loop, one LDS atomic per wave (an atomicAdd on s_distinct from the inserting lanes
+                // is the atomic optimizer's lane-by-lane loop: ~5 SALU per new key)
+                int32_t ins = -1;
+                if (hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice)) {
                 const Key<L> key = kb[q];
-                if (sbits && bits_at(key, sshift, sbits) != slice) continue;
-                uint32_t h = key_hash(key) & (SLOTS - 1);
+                uint32_t h = slot_of<SLOTS>(key_hash(key));
                 for (uint32_t probes = 0;;) {
                     if (KEYCAS) {
                         const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
                                                        (unsigned long long)EMPTY,
                                                        (unsigned long long)key.w[0]);
                         if (old == EMPTY) {
-                            if (LIST) {
-                                const uint32_t pos = atomicAdd(&s_distinct, 1u);
-                                if (pos < LIMIT) s_slot[pos] = (uint16_t)h;
-                                else ovf = true;
-                            } else {
-                                ++mynew;
-                            }
+                            if (LIST) ins = (int32_t)h;
+                            else ++mynew;
                             break;
                         }
                         if (old == key.w[0]) break;
@@ -578,7 +587,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                         if (st != 2 && __atomic_load_n(&s_state[h], __ATOMIC_ACQUIRE) != 2) continue;
                         if (s_key[h] == key) break;
                     }
-                    h = (h + 1) & (SLOTS - 1);
+                    h = h + 1 == SLOTS ? 0 : h + 1;
                     if (++probes >= SLOTS) {
                         ovf = true;
                         break;
@@ -592,6 +601,21 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                         const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
                         old = atomicCAS(&s_sum[h], assumed, nv);
                     } while (old != assumed);
+                }
+                }
+                if constexpr (LIST) {
+                    const uint64_t m = __ballot(ins >= 0);
+                    if (m) {
+                        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
+                        uint32_t wb = 0;
+                        if (__lane_id() == leader) wb = atomicAdd(&s_distinct, (uint32_t)__popcll(m));
+                        wb = __shfl(wb, leader, 64);
+                        const uint32_t pos = wb + (uint32_t)__popcll(m & lanemask_lt());
+                        if (ins >= 0) {
+                            if (pos < LIMIT) s_slot[pos] = (uint16_t)ins;
+                            else ovf = true;
+                        }
+                    }
                 }
             }
         }
@@ -760,7 +784,11 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
  */
 template <int L>
 struct MergeLocalTraits {
-    static constexpr int CAP = L == 1 ? 2048 : L == 2 ? 1024 : 512;  // keys per array (3 arrays)
+    // keys per LDS array (3 arrays): a u64 group of the configs[1] rc sort holds ~710 rc + ~710
+    // canonical keys (up to ~1420 where either strand is twice as dense), so 1536-key arrays (36 KB,
+    // 4 workgroups per CU) instead of 2048 (48 KB, 3 per CU): rc stage 5.9 -> 5.5 ms; the few larger
+    // groups rerun with twice the arrays (1280: 6.4 ms, too many reruns)
+    static constexpr int CAP = L == 1 ? 1536 : L == 2 ? 1024 : 512;
 };
 
 // CAP: keys per LDS array; glist (optional): the groups to run (the big-CAP rerun of the groups

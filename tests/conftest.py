@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:  # load torch's own HIP runtime before libmtg_boss loads /opt/rocm's: a torch device first used
+    import torch  # noqa: F401  after the library initialised the GPU reports no device
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 for p in (ROOT, os.path.join(ROOT, "oracle")):

@@ -18,21 +18,29 @@ boss = importlib.import_module("projects2014-metagenome_amd.boss")
 pytestmark = pytest.mark.gpu
 
 
+def _strip_cr(line):
+    return line[:-1] if line.endswith("\r") else line
+
+
 def kseq_records(text):
-    """FASTA / FASTQ records by kseq's rules: FASTA headers start with '>' at a line start and
-    text before the first header is skipped; sequence lines are joined without their line ends;
-    FASTQ is four lines per record."""
+    """FASTA / FASTQ records by kseq's rules (kseq_read): FASTA headers are lines starting with '>'
+    (or '@' once a record is open), text before the first header is skipped, sequence lines are
+    joined without their line ends (a '\r' right before '\n' goes with it; any other '\r' stays);
+    FASTQ is four lines per record from the first '@' line."""
     lines = text.split("\n")
-    if text.lstrip("\r\n ").startswith("@"):
-        return [lines[i].replace("\r", "") for i in range(1, len(lines), 4)]
+    body = text.lstrip("\r\n ")
+    if body.startswith("@"):
+        first = text[:len(text) - len(body)].count("\n")
+        return [_strip_cr(lines[i]) for i in range(first + 1, len(lines), 4)]
     out, cur = [], None
     for ln in lines:
-        if ln.startswith(">"):
+        if ln.startswith(">") or (cur is not None and ln.startswith("@")):
             if cur is not None:
                 out.append(cur)
             cur = ""
         elif cur is not None:
-            cur += ln.replace("\r", "")
+            assert not ln.startswith("+"), "kseq would read FASTQ quality here"
+            cur += _strip_cr(ln)
     if cur is not None:
         out.append(cur)
     return out
@@ -144,3 +152,37 @@ def test_missing_file_raises():
     ctor = boss.IBOSSChunkConstructor.initialize(10)
     with pytest.raises(RuntimeError, match="Cannot read"):
         ctor.add_fasta("/nonexistent/reads.fa")
+
+
+def test_kseq_line_rules(tmp_path):
+    # '@' header lines inside a FASTA file, a '\r' inside a sequence line (breaks windows), CRLF
+    # line ends, blank lines before the first FASTQ record (the 4-line phase starts at the '@')
+    reads = _random_reads(11, 60, 90, 2000)
+    parts = []
+    for i, r in enumerate(reads):
+        r = r.decode()
+        parts.append(("@h%d\n" if i % 5 == 2 else ">h%d\n") % i)
+        if i % 4 == 1:
+            parts.append(r[:40] + "\r" + r[40:] + "\r\n")
+        else:
+            parts.append(r[:50] + "\n" + r[50:] + "\n")
+    fa = "".join(parts)
+    p = str(tmp_path / "rules.fa")
+    open(p, "w", newline="").write(fa)
+    fq = "\n\n  \n" + "".join("@q%d\n%s\r\n+\n%s\n" % (i, r.decode(), "I" * len(r)) for i, r in enumerate(reads[:20]))
+    q = str(tmp_path / "rules.fq")
+    open(q, "w", newline="").write(fq)
+    recs = kseq_records(fa)
+    assert len(recs) == len(reads) and any("\r" in x for x in recs)
+    assert kseq_records(fq) == [r.decode() for r in reads[:20]]
+    for k, canonical in ((20, True), (12, False)):
+        _check(k, [p, q], [fa, fq], canonical, 8)
+
+
+def test_plus_line_in_fasta_is_refused(tmp_path):
+    p = str(tmp_path / "plus.fa")
+    open(p, "w").write(">a\nACGTACGTAC\n+\nIIIIIIIIII\n")
+    ctor = boss.IBOSSChunkConstructor.initialize(5)
+    ctor.add_fasta(p)
+    with pytest.raises(RuntimeError, match="starts with '\\+'"):
+        ctor.build_chunk()

@@ -98,3 +98,22 @@ def test_ranges_empty_and_tiny(monkeypatch):
         _check(k, [], False, 0)
         _check(k, ["A" * k], True, 8)
         _check(k, ["N" * 100, "$" * 50, "."], False, 8)
+
+
+def test_config2_default_planner_many_ranges():
+    # configs[2]'s shape (k = 63, u128 keys, genome-sampled 150 bp reads) at 2 M reads, with a
+    # memory budget that makes the DEFAULT planner (no MTG_RANGES) cut the collection into >= 8 key
+    # ranges, the way the 100 M-read configs[2] build runs within HBM; bit for bit vs the oracle
+    import bench
+    asc = bench.make_reads_host_codes(2_000_000, 150, 4321, "genome", 10.0)
+    data = asc.reshape(-1)
+    off = np.arange(len(asc) + 1, dtype=np.uint64) * asc.shape[1]
+    ctor = boss.IBOSSChunkConstructor.initialize(62, both_strands=True, num_threads=8, memory_preallocated=5e9)
+    ctor.add_packed(data, off)
+    got = ctor.build_chunk()
+    t = ctor.timings()
+    assert t.n_batches >= 8, t.n_batches
+    assert t.n_extracted == len(asc) * (150 - 63 + 1)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(62, reads, canonical=True, bits_per_count=0)
+    assert_same(got, want, "configs[2] shape, %d ranges" % t.n_batches)

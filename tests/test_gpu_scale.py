@@ -224,3 +224,38 @@ def test_cfg4_share_dist_batched():
     W2, last2, _ = _device_arrays(dc2, 0)
     assert [int(f) for f in dc2.F] == F
     assert np.array_equal(W, W2) and np.array_equal(last, last2)
+
+
+# configs[3]'s per-GPU share: 125 M genome-sampled reads (1.5e10 windows, the share of one GPU in the
+# 1 B-read job over 8), too big for one pass, so the build collects in key rounds.  The distributed
+# build at P = 1 (an in-process one-rank group: the rounds of collect_ranges_dist, the dummy query
+# join, the owner emit) must return the single build's chunk (its own range-batched path) bit for
+# bit, with the size identities; the oracle would take ~10 minutes here.
+@pytest.mark.timeout(900)
+def test_config3_share_dist_equals_single():
+    torch = pytest.importorskip("torch")
+    import gc
+    dev = torch.device("cuda", 0)
+    n_reads, L = 125_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    out = []
+    for dist in (False, True):
+        ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, num_threads=16)
+        comms = boss.Comm.local_group(1) if dist else None
+        dc = ctor.build_device(seq.data_ptr(), seq.numel(), comm=comms[0] if dist else None)
+        t = ctor.timings()
+        assert t.n_extracted == n_reads * (L - 31 + 1)
+        assert t.n_batches >= 2, t.n_batches
+        assert dc.n == t.n_rows == 1 + dc.n_real + dc.n_dummy
+        W, last, _ = _device_arrays(dc, 0)
+        F = [int(f) for f in dc.F]
+        assert W.max() <= 9 and W[0] == 0 and last[0] == 0 and last[-1] == 1
+        assert F == sorted(F) and F[4] <= dc.n - 1
+        out.append((dc.n, dc.n_real, F, W, last))
+        del dc, ctor, comms
+        gc.collect()
+    a, b = out
+    assert a[:3] == b[:3]
+    assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
