@@ -128,6 +128,87 @@ __device__ __forceinline__ uint32_t slide_windows(const uint8_t *s_code, uint32_
 }
 
 /*
+ * K1 for an input whose every read is exactly one window: K chars + one separator, read r at
+ * r * (K + 1) -- a KMC database decoded into reads (kmc.hpp: one record per read, seq_io/
+ * kmc_parser.cpp:27-62), 1.9e8 reads of 32 bytes at configs[4].  The window extractor would visit
+ * all K + 1 positions of every read to keep one; here one thread takes one read (lanes on adjacent
+ * reads, so a wave reads 64 * (K + 1) contiguous bytes), builds its key as slide_windows does
+ * (canonical by take_rc) and its clamped count, and the valid ones go out in any order through one
+ * cursor atomic per workgroup: the sort that follows fixes the order, and saturating sums do not
+ * depend on it.  A read start or separator that breaks the layout raises *bad (the caller then
+ * takes the window extractor).
+ */
+template <int L, bool COUNTED>
+__global__ __launch_bounds__(256) void window_reads_kernel(
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
+    const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
+    uint32_t cmax, Key<L> *__restrict__ out, uint32_t *__restrict__ outc, unsigned long long *__restrict__ cursor,
+    uint32_t *__restrict__ bad) {
+    constexpr int PER = 8;  // reads per thread, 256 apart
+    __shared__ uint32_t s_scan[256 / 64 + 1];
+    __shared__ unsigned long long s_base;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t stride = K + 1;
+    const Key<L> low = Key<L>::lowmask(2 * (K - 1));
+    Key<L> kk[PER];
+    uint32_t cc[PER];
+    uint32_t valid = 0;
+    bool err = false;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint64_t r = (uint64_t)blockIdx.x * (256 * PER) + (uint64_t)q * 256 + tid;
+        if (r >= n_reads) continue;
+        const uint64_t s0 = r * stride;
+        err |= read_starts[r] != s0 || (s0 + K < seq_len && encode_dna(seq[s0 + K]) != 4u) || s0 + K > seq_len;
+        if (s0 + K > seq_len) continue;
+        Key<L> P = Key<L>::zero(), R = Key<L>::zero();
+        bool ok = true;
+        // the K chars through aligned 4-byte loads (a word never reaches past the one holding the
+        // read's last char, so never into another page)
+        const uint64_t a0 = s0 & ~3ull;
+        unsigned i = 0;
+        for (uint64_t a = a0; i < K; a += 4) {
+            const uint32_t w = *(const uint32_t *)(seq + a);
+            for (unsigned b = a == a0 ? (unsigned)(s0 - a0) : 0u; b < 4 && i < K; ++b, ++i) {
+                uint32_t c = encode_dna((w >> (8 * b)) & 0xFFu);
+                if (c == 4u) {
+                    ok = false;
+                    c = 0;
+                }
+                P = P | shl(Key<L>::from(c), 2 * i);
+                R = R | shl(Key<L>::from(3u - c), 2 * (K - 1 - i));
+            }
+        }
+        if (!ok) continue;
+        Key<L> f = plain_to_boss(P, K, low);
+        if (canonical) {
+            const Key<L> rr = plain_to_boss(R, K, low);
+            if (take_rc(canonical, f, rr, K)) f = rr;
+        }
+        kk[q] = f;
+        if (COUNTED) {
+            const uint32_t c = read_counts ? read_counts[r] : 1u;
+            cc[q] = c < cmax ? c : cmax;
+        }
+        valid |= 1u << q;
+    }
+    if (err) atomicOr(bad, 1u);
+    uint32_t total;
+    uint32_t o = block_exclusive_sum<256>((uint32_t)__popc(valid), s_scan, &total);
+    if (tid == 0) s_base = total ? atomicAdd(cursor, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    const uint64_t base = s_base + o;
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (!((valid >> q) & 1u)) continue;
+        out[base + j] = kk[q];
+        if (COUNTED) outc[base + j] = cc[q];
+        ++j;
+    }
+}
+
+/*
  * K1: extract_pack_canon.  Replaces KmerExtractorT<2>::sequence_to_kmers
  * (kmer/kmer_extractor.cpp:472-507; slides :86-108 / :165-196; skip rule from
  * utils::drag_and_mark_segments, common/algorithms.hpp:50-67) and the per-read count clamp of
@@ -1308,18 +1389,24 @@ __global__ void dummy_decode_kernel(const uint64_t *__restrict__ in, uint64_t n,
     const uint64_t T0 = dummy_rank_space(k);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         uint64_t r = in[i], T = T0;
+        // the real chars r_1, r_2, ... enter at the bottom of x one by one (r_p ends up at node
+        // position k - p + 1); then one shift leaves the $ run and the label below them
         unsigned __int128 x = 0;
+        unsigned m = 0;
+        uint64_t label = 0;  // $ for a sink
         for (unsigned p = 1; p <= k; ++p) {
             if (r < 4) {  // a source of level k - (p - 1): its label
-                x |= r + 1;
+                label = r + 1;
                 break;
             }
             r -= 4;
             T = (T - 4) >> 2;  // T(p): strings below one real char at depth p
             const uint64_t rp = (uint64_t)(r >= T) + (r >= 2 * T) + (r >= 3 * T);
             r -= rp * T;
-            x |= (unsigned __int128)(rp + 1) << (3 * (k - p + 1));  // r_p sits at node position k - p + 1
+            x = (x << 3) | (rp + 1);
+            ++m;
         }
+        x = (x << (3 * (k - m) + 3)) | label;
         Key<L3> o;  // all k node chars real and no label: a sink ($)
         o.w[0] = (uint64_t)x;
         if constexpr (L3 > 1) o.w[1] = (uint64_t)(x >> 64);

@@ -112,6 +112,8 @@ struct Small {  // one device word block, zeroed per use
     uint32_t bad_dummy;
     uint32_t bruns;  // bucket_index: listed long runs
     uint32_t fasta_bad;  // fasta_split_kernel: a '+' sequence line
+    uint32_t wbad;       // window_reads_kernel: the input is not one window per read
+    unsigned long long wcursor;  // window_reads_kernel: keys written
     uint32_t error;
 };
 
@@ -827,6 +829,49 @@ static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax,
     return N;
 }
 
+// Whether the reads may be one window each (K chars + a separator, read r at r * (K + 1): a KMC
+// database decoded into reads); window_reads_kernel checks every read and says if not.
+static bool window_layout(Ctx &c, unsigned K, const BuildInput &in) {
+    if (!in.read_starts || in.n_reads == 0 || c.use_lsd) return false;
+    const uint64_t n = in.n_reads, st = K + 1;
+    if (in.seq_len < (n - 1) * st + K || in.seq_len > n * st) return false;
+    uint64_t s[2] = {0, st};
+    HIP_CHECK(hipMemcpyAsync(s, in.read_starts, (n >= 2 ? 2 : 1) * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    return s[0] == 0 && (n < 2 || s[1] == st);
+}
+
+// K1 for one-window reads (boss_kernels.hpp: window_reads_kernel): every read's k-mer straight to *ka
+// in any order.  False (nothing kept) when the layout does not hold.
+template <int L2, bool COUNTED>
+static bool stage_extract_windows(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                                  Key<L2> **ka, Key<L2> **kb, uint32_t **ca, uint32_t **cb, uint64_t *N_out) {
+    if (!window_layout(c, K, in)) return false;
+    using K2 = Key<L2>;
+    const uint64_t n = in.n_reads;
+    *ka = (K2 *)c.ws.get(Workspace::KA, n * sizeof(K2));
+    *kb = (K2 *)c.ws.get(Workspace::KB, n * sizeof(K2));
+    *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, n * 4) : nullptr;
+    *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, n * 4) : nullptr;
+    HIP_CHECK(hipMemsetAsync(&c.small->wbad, 0, 4, c.stream));
+    HIP_CHECK(hipMemsetAsync(&c.small->wcursor, 0, 8, c.stream));
+    window_reads_kernel<L2, COUNTED><<<dim3((unsigned)ceil_div(n, 256 * 8)), dim3(256), 0, c.stream>>>(
+        in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, n, cmax, *ka,
+        COUNTED ? *ca : nullptr, &c.small->wcursor, &c.small->wbad);
+    HIP_CHECK(hipGetLastError());
+    uint32_t bad = 0;
+    unsigned long long N = 0;
+    HIP_CHECK(hipMemcpyAsync(&bad, &c.small->wbad, 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(&N, &c.small->wcursor, 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    if (bad) return false;
+    if (c.debug) fprintf(stderr, "[mtg debug] one-window reads: %lu reads -> %llu k-mers\n", (unsigned long)n, N);
+    c.timings.n_positions = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    c.timings.n_extracted = N;
+    *N_out = N;
+    return true;
+}
+
 // K1 fused with K2's first partition level (extract_partition.hpp), for 2-bit u64 keys on
 // inputs big enough to have one.  Returns false (nothing done) when it does not apply; else N,
 // the duplication estimate, and the level-1 counts in *hist1 (device) with *ka scattered.
@@ -1189,6 +1234,7 @@ static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3
     Key<1> *ra = ranks, *rb = (void *)ranks == (void *)xa ? (Key<1> *)xb : (Key<1> *)xa;
     uint32_t *nv = nullptr;
     const unsigned nbits = 64 - (unsigned)__builtin_clzll(dummy_rank_space(kb));
+    // (the real k-mers' MSD partition + LDS-hash unique on these ranks: dummy stage 4.4 -> 6.8 ms)
     radix_sort<1, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
     reset_small(c);
     const uint64_t ut = ceil_div(Draw, 2048);
@@ -1480,7 +1526,9 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         ev_sort = ev_unique = tm.mark();
         T.n_unique = U;
     } else {
-    if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+    if (stage_extract_windows<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N))
+        dup = 1.0;  // one k-mer per record: distinct up to a strand
+    else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
         N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
     ev_extract = tm.mark();
 
@@ -1958,6 +2006,18 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     using K2 = Key<1>;
     // the same on every rank (no input-size test: a rank may hold no reads)
     if (!c.fused || c.use_lsd || K - 1 < FUSED_HB / 2 || K > 32 || c.force_ranges) return false;
+    // one-window reads (KMC input) are cheaper through window_reads_kernel and the local collect; the
+    // decision must agree on every rank, so a rank's layout is shared by an all-reduce
+    {
+        uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, 8);
+        const uint64_t win = window_layout(c, K, in) || in.seq_len == 0 ? 0 : 1;
+        HIP_CHECK(hipMemcpyAsync(dv, &win, 8, hipMemcpyHostToDevice, c.stream));
+        d.comm.allreduce_sum_u64(dv, 1, c.stream);
+        uint64_t any_other = 0;
+        HIP_CHECK(hipMemcpyAsync(&any_other, dv, 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // `win` is a host local
+        if (!any_other) return false;
+    }
     constexpr unsigned OB = 8;   // owner-range prefix bits (4 node chars: whole chars for the lifted bounds)
     // canonical windows keep the strand whose key top hashes smaller (boss_kernels.hpp: take_rc): the
     // owners' canonical keys then follow the real edges, and one set of ranges balances both
@@ -2234,7 +2294,8 @@ static bool dist_superkmers(Ctx &c, Dist &d, unsigned K, bool canonical, const B
         if (nr > 1) {
             const uint64_t nq = (out->seq_len >> RID_SHIFT) + 2;
             uint64_t *rid = (uint64_t *)c.ws.get(Workspace::SK_RID, nq * 8);
-            read_index_kernel<<<dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, c.stream>>>(starts, nr, nq, rid);
+            read_index_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(nr, 256), 65536)), dim3(256), 0, c.stream>>>(
+                starts, nr, nq, rid);
             HIP_CHECK(hipGetLastError());
             out->rid_at = rid;
         }
@@ -2305,7 +2366,9 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         uint64_t N = 0;
         double dup = 0;
         const uint32_t *hist1 = nullptr;
-        if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+        if (stage_extract_windows<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N))
+            dup = 1.0;
+        else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
             N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb);
         if (sk) {  // the windows of this rank's reads, not of the received runs
             T.n_positions = in.seq_len >= K ? in.seq_len - K + 1 : 0;
@@ -3471,8 +3534,8 @@ static void dispatch_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &
     if (in.read_counts && in.n_reads > 1) {  // bracket the per-read count searches (device_common.hpp)
         const uint64_t nq = (in.seq_len >> mtg::RID_SHIFT) + 2;
         uint64_t *rid = (uint64_t *)c->ctx.ws.get(mtg::Workspace::RID_AT, nq * 8);
-        read_index_kernel<<<dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0, c->ctx.stream>>>(in.read_starts,
-                                                                                          in.n_reads, nq, rid);
+        read_index_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(in.n_reads, 256), 65536)), dim3(256), 0,
+                            c->ctx.stream>>>(in.read_starts, in.n_reads, nq, rid);
         HIP_CHECK(hipGetLastError());
         in.rid_at = rid;
     }

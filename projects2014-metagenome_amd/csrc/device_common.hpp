@@ -221,9 +221,10 @@ __device__ __forceinline__ void tile_base_lookback(uint64_t *desc, uint32_t tile
 //
 // The read holding buffer position p (the last r with read_starts[r] <= p), for per-read counts.
 // rid_at (optional, read_index_kernel) brackets the search: rid_at[q] = that read for position
-// q << RID_SHIFT, so a window searches the few reads of its 4 K-position block instead of all of
-// them (KMC input: one read per k + 1 bytes, 1.9e8 reads at configs[4]).
-constexpr unsigned RID_SHIFT = 12;
+// q << RID_SHIFT, so a window searches the one or two reads of its 32-position block instead of
+// all of them.  (4 K-position blocks left a 7-step search of global memory per window for KMC input
+// -- one 32-byte read per record, 1.9e8 reads at configs[4] -- 42.8 ms of extraction per step.)
+constexpr unsigned RID_SHIFT = 5;
 
 __device__ __forceinline__ uint64_t read_of(const uint64_t *__restrict__ read_starts, uint64_t n_reads,
                                             const uint64_t *__restrict__ rid_at, uint64_t p) {
@@ -240,10 +241,17 @@ __device__ __forceinline__ uint64_t read_of(const uint64_t *__restrict__ read_st
     return lo;
 }
 
+// rid_at[0..nq) from the sorted read starts, one thread per read: read r owns the blocks whose first
+// position lies in [start_r, start_{r+1}) (read 0 also every block before it), O(reads + blocks)
 __global__ void read_index_kernel(const uint64_t *__restrict__ read_starts, uint64_t n_reads, uint64_t nq,
                                   uint64_t *__restrict__ rid_at) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nq) rid_at[q] = read_of(read_starts, n_reads, nullptr, q << RID_SHIFT);
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    constexpr uint64_t B = 1ull << RID_SHIFT;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads; r += gs) {
+        const uint64_t q0 = r == 0 ? 0 : (read_starts[r] + B - 1) >> RID_SHIFT;
+        const uint64_t q1 = r + 1 < n_reads ? min(nq, (read_starts[r + 1] + B - 1) >> RID_SHIFT) : nq;
+        for (uint64_t q = q0; q < q1; ++q) rid_at[q] = r;
+    }
 }
 
 }  // namespace mtg

@@ -556,8 +556,12 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 }
                 continue;
             }
+            // (issuing the first-probe CASes of all the thread's keys back to back, one LDS round trip per
+            // batch instead of a chain per key, measured slower: 11.4 vs 10.5 ms sort stage, the
+            // in-flight results spill at 64 VGPRs; 10.6 ms with 4-key batches)
+            constexpr int NQ = BATCH * PAIR;
 #pragma unroll
-            for (int q = 0; q < BATCH * PAIR; ++q) {
+            for (int q = 0; q < NQ; ++q) {
                 // LIST: the new keys of a wave take their list positions by ballot after the probe
                 // loop, one LDS atomic per wave (an atomicAdd on s_distinct from the inserting lanes
                 // is the atomic optimizer's lane-by-lane loop: ~5 SALU per new key)
@@ -567,6 +571,8 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 uint32_t h = slot_of<SLOTS>(key_hash(key));
                 for (uint32_t probes = 0;;) {
                     if (KEYCAS) {
+                        // (a plain LDS read of the slot before the CAS -- most keys are repeats that
+                        // find themselves in their first slot -- measured 0.2-0.3 ms slower per step)
                         const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
                                                        (unsigned long long)EMPTY,
                                                        (unsigned long long)key.w[0]);
@@ -595,12 +601,19 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 }
                 if (COUNTED && !ovf) {
                     const uint32_t add = vb[q];
-                    uint32_t old = s_sum[h], assumed;
-                    do {
-                        assumed = old;
-                        const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
-                        old = atomicCAS(&s_sum[h], assumed, nv);
-                    } while (old != assumed);
+                    if (cmax <= 0xFFFFu) {
+                        // 8/16-bit containers: a plain add, clamped on output; a sum past 2^30 is
+                        // pulled back to cmax at once, so it never wraps (every add is <= cmax)
+                        const uint32_t o = atomicAdd(&s_sum[h], add);
+                        if (o + add > 0x40000000u) atomicMin(&s_sum[h], cmax);
+                    } else {
+                        uint32_t old = s_sum[h], assumed;
+                        do {
+                            assumed = old;
+                            const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
+                            old = atomicCAS(&s_sum[h], assumed, nv);
+                        } while (old != assumed);
+                    }
                 }
                 }
                 if constexpr (LIST) {
@@ -762,7 +775,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             uint32_t rank = 0;
             for (uint32_t j = b0; j < b1; ++j) rank += scratch[j] < key;
             tmp[g0 + out_off + b0 + rank] = key;
-            if (COUNTED) tcnt[g0 + out_off + b0 + rank] = sscr[p];
+            if (COUNTED) tcnt[g0 + out_off + b0 + rank] = min(sscr[p], cmax);
         }
         out_off += D;
         __syncthreads();  // the next slice reuses the table
