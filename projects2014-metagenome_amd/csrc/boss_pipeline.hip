@@ -64,7 +64,7 @@ class Workspace {
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
-        SK_STARTS, SK_RID, NSLOTS
+        SK_STARTS, SK_RID, CANON_IDX, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -179,6 +179,14 @@ struct Ctx {
                                    // (=superkmer), 2 local collect + exchange of sorted runs (=local)
     bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
                                    // dense u64 ranks (dummy_encode_kernel)
+    // bucket index of the last msd_sort_unique's output over its final bucket bits, when every group
+    // was one bucket (its group starts are that index): the fused rc merge reuses it for the canonical keys
+    struct GroupIndex {
+        const void *keys = nullptr;
+        uint64_t n = 0;
+        unsigned bits = 0, nbits = 0;
+        const uint64_t *start = nullptr;
+    } gidx;
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
     const void *bidx_keys = nullptr;
     uint64_t bidx_n = 0;
@@ -430,6 +438,8 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     // distinct: the input has no duplicates (the local pass skips its hash table);
     // runs: the input is runs->size() - 1 sorted runs at these offsets (one gather replaces
     // the partition passes)
+    const Ctx::GroupIndex saved_gidx = c.gidx;  // the canonical sort's, for the fused rc merge below
+    c.gidx = Ctx::GroupIndex{};
     if (n == 0) return 0;
     constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
     constexpr int TILE = MsdTraits<L>::TILE;
@@ -530,6 +540,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         const uint64_t G = LIMIT / 4;
         uint64_t ngroups = 1;
         uint64_t *gstart;
+        const uint64_t *gbucket_out = nullptr;
         if (b == 0) {
             gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, 16);
             set_pair_kernel<<<1, 1, 0, c.stream>>>(gstart, 0, n);
@@ -542,8 +553,13 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             if (fuse) {
                 // fused rc merge: the canonical keys of every bucket (bucket index of the sorted
                 // set), and groups sized by rc + canonical keys together
-                cstart = (uint64_t *)c.ws.get(Workspace::RC_CSTART, (nbuckets + 2) * 8);
-                bucket_index<L>(c, rm->ck, rm->nc, nbits - b, nbuckets, cstart);
+                if (saved_gidx.keys == (const void *)rm->ck && saved_gidx.n == rm->nc && saved_gidx.bits == b &&
+                    saved_gidx.nbits == nbits) {
+                    cstart = const_cast<uint64_t *>(saved_gidx.start);  // the canonical sort's group starts
+                } else {
+                    cstart = (uint64_t *)c.ws.get(Workspace::RC_CSTART, (nbuckets + 2) * 8);
+                    bucket_index<L>(c, rm->ck, rm->nc, nbits - b, nbuckets, cstart);
+                }
                 uint64_t *comb = (uint64_t *)c.ws.get(Workspace::RC_COMB, (nbuckets + 1) * 8);
                 add_starts_kernel<<<dim3((unsigned)ceil_div(nbuckets + 1, 256)), dim3(256), 0, c.stream>>>(
                     bstart, cstart, nbuckets + 1, comb);
@@ -564,7 +580,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             HIP_CHECK(hipMemcpyAsync(&ngroups, gpos + nbuckets, 8, hipMemcpyDeviceToHost, c.stream));
             HIP_CHECK(hipStreamSynchronize(c.stream));
             gstart = (uint64_t *)c.ws.get(Workspace::MSD_GSTART, (ngroups + 1) * 8);
-            uint64_t *gbucket = fuse ? (uint64_t *)c.ws.get(Workspace::MSD_GBUCKET, (ngroups + 1) * 8) : nullptr;
+            // each group's bucket range: the fused rc merge's canonical ranges, or the output's bucket index
+            uint64_t *gbucket = b <= 32 ? (uint64_t *)c.ws.get(Workspace::MSD_GBUCKET, (ngroups + 1) * 8) : nullptr;
+            gbucket_out = gbucket;
             group_scatter_kernel<<<dim3((unsigned)ceil_div(nbuckets + 1, 256)), dim3(256), 0, c.stream>>>(
                 bstart, gf, gpos, nbuckets, n, gstart, gbucket);
             HIP_CHECK(hipGetLastError());
@@ -720,12 +738,22 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(ucount, ngroups, ustart, desc, ep,
                                                                       &c.small->counter, &c.small->error);
         HIP_CHECK(hipGetLastError());
+        // the output's bucket index over the top b bits comes out of the gather (the fused rc merge
+        // of the canonical keys reuses it instead of a bucket_index pass: 0.44 ms at configs[1])
+        const bool index = gbucket_out && b > 0;
+        uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nbuckets + 2) * 8) : nullptr;
         group_gather_kernel<L, COUNTED><<<dim3((unsigned)ngroups), dim3(256), 0, c.stream>>>(
-            *alt, COUNTED ? *valt : nullptr, gstart, ustart, *keys, COUNTED ? *vals : nullptr);
+            *alt, COUNTED ? *valt : nullptr, gstart, ustart, *keys, COUNTED ? *vals : nullptr, gbucket_out,
+            nbits - b, gi);
         HIP_CHECK(hipGetLastError());
         uint64_t u = 0;
         HIP_CHECK(hipMemcpyAsync(&u, ustart + ngroups, 8, hipMemcpyDeviceToHost, c.stream));
+        if (index) {  // entries nbuckets, nbuckets + 1 = the key count
+            HIP_CHECK(hipMemcpyAsync(gi + nbuckets, ustart + ngroups, 8, hipMemcpyDeviceToDevice, c.stream));
+            HIP_CHECK(hipMemcpyAsync(gi + nbuckets + 1, ustart + ngroups, 8, hipMemcpyDeviceToDevice, c.stream));
+        }
         HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (index) c.gidx = Ctx::GroupIndex{*keys, u, b, nbits, gi};
         return u;
     }
 }

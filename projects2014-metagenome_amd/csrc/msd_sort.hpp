@@ -932,17 +932,32 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     }
 }
 
-// copy every group's distinct keys from tmp[gstart[g]..] to out[ustart[g]..]
+// copy every group's distinct keys from tmp[gstart[g]..] to out[ustart[g]..].  istart (optional):
+// the bucket index of out over the top bits of the keys above ishift (bucket_index_kernel's layout),
+// each group filling the entries of its buckets [gbucket[g], gbucket[g + 1]) as it copies -- the
+// fused rc merge then needs no bucket_index pass over the canonical keys
 template <int L, bool COUNTED>
 __global__ __launch_bounds__(256) void group_gather_kernel(
     const Key<L> *__restrict__ tmp, const uint32_t *__restrict__ tcnt,
     const uint64_t *__restrict__ gstart, const uint64_t *__restrict__ ustart,
-    Key<L> *__restrict__ out, uint32_t *__restrict__ ocnt) {
+    Key<L> *__restrict__ out, uint32_t *__restrict__ ocnt, const uint64_t *__restrict__ gbucket = nullptr,
+    unsigned ishift = 0, uint64_t *__restrict__ istart = nullptr) {
     const uint64_t g = blockIdx.x;
     const uint64_t src = gstart[g], dst = ustart[g], m = ustart[g + 1] - dst;
+    const uint64_t gb0 = istart ? gbucket[g] : 0;
     for (uint64_t i = threadIdx.x; i < m; i += 256) {
-        out[dst + i] = tmp[src + i];
+        const Key<L> key = tmp[src + i];
+        out[dst + i] = key;
         if (COUNTED) ocnt[dst + i] = tcnt[src + i];
+        if (istart) {  // buckets (previous key's, this key's] start here
+            const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
+            const uint64_t pb = i == 0 ? gb0 - 1 : bits_at(shr(tmp[src + i - 1], ishift), 0, 32);
+            for (uint64_t x = pb + 1; x <= kb; ++x) istart[x] = dst + i;
+        }
+    }
+    if (istart) {  // the group's buckets after its last key start at its end
+        const uint64_t lb = m ? bits_at(shr(tmp[src + m - 1], ishift), 0, 32) : gb0 - 1;
+        for (uint64_t x = lb + 1 + threadIdx.x; x < gbucket[g + 1]; x += 256) istart[x] = dst + m;
     }
 }
 

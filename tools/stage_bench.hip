@@ -401,7 +401,7 @@ static void extract_bench(hipStream_t s, uint64_t reads) {
     HIP_CHECK(hipMalloc(&out, npos * 8));
     float t = time_ms(s, 3, [&] {
         extract_kernel<1, false, true><<<dim3((unsigned)tiles), dim3(256), 0, s>>>(
-            seq, len, K, 1, nullptr, nullptr, 0, 255, nullptr, nullptr, tcnt, nullptr, nullptr, 0);
+            seq, len, K, 1, nullptr, nullptr, 0, nullptr, 255, nullptr, nullptr, tcnt, nullptr, nullptr, 0);
     });
     printf("extract count: %.3f ms\n", t);
     std::vector<uint32_t> h(tiles);
@@ -412,7 +412,7 @@ static void extract_bench(hipStream_t s, uint64_t reads) {
     const double bytes = len + o[tiles] * 8.0;
     t = time_ms(s, 3, [&] {
         extract_kernel<1, false, false><<<dim3((unsigned)tiles), dim3(256), 0, s>>>(
-            seq, len, K, 1, nullptr, nullptr, 0, 255, out, nullptr, nullptr, toff, nullptr, 0);
+            seq, len, K, 1, nullptr, nullptr, 0, nullptr, 255, out, nullptr, nullptr, toff, nullptr, 0);
     });
     printf("extract write: %.3f ms = %.0f GB/s (%lu k-mers)\n", t, bytes / 1e9 / (t * 1e-3),
            (unsigned long)o[tiles]);
