@@ -64,7 +64,7 @@ class Workspace {
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
-        SK_STARTS, SK_RID, CANON_IDX, NSLOTS
+        SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -93,6 +93,7 @@ class Workspace {
         for (const auto &b : bufs_) t += b.cap;
         return t;
     }
+    uint64_t held_slot(Slot s) const { return bufs_[s].cap; }
 
   private:
     struct Buf {
@@ -112,6 +113,8 @@ struct Small {  // one device word block, zeroed per use
     uint32_t bad_dummy;
     uint32_t bruns;  // bucket_index: listed long runs
     uint32_t fasta_bad;  // fasta_split_kernel: a '+' sequence line
+    uint32_t gidx_bad;   // group_gather_kernel: the output bucket index was abandoned
+    uint32_t spec_ovf;   // msd_partition_kernel: a speculative bucket overflowed
     uint32_t wbad;       // window_reads_kernel: the input is not one window per read
     unsigned long long wcursor;  // window_reads_kernel: keys written
     uint32_t error;
@@ -187,6 +190,9 @@ struct Ctx {
         unsigned bits = 0, nbits = 0;
         const uint64_t *start = nullptr;
     } gidx;
+    bool want_gidx = false;  // the next msd_sort_unique's output feeds the fused rc merge
+    bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
+                             // sample-sized one (spec_final_level)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
     const void *bidx_keys = nullptr;
     uint64_t bidx_n = 0;
@@ -209,6 +215,7 @@ static void load_knobs(Ctx &c) {
     c.fused = !is("MTG_FUSED", "0");
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
+    c.spec_final = !is("MTG_SPEC", "0");
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
     c.force_spill = is("MTG_SPILL", "1");
@@ -426,6 +433,140 @@ struct RcMerge {
     unsigned ib = 0;
 };
 
+// bucket capacities of the speculative final level: the sampled count scaled up, 20 % + 512 keys
+// of slack (a bucket of ~4600 keys overflows with probability ~1e-10 at a 1/8 sample)
+__global__ void spec_caps_kernel(const uint32_t *__restrict__ sample, uint64_t nb, uint32_t stride,
+                                 uint32_t *__restrict__ cap) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) cap[b] = (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
+}
+
+// The final MSD level of the main sort (level 2 after the fused K1's level 1) without its exact
+// histogram pass (msd_hist_kernel reads all N keys: 1.68 ms at configs[1]): the buckets are sized
+// from a histogram of every 8th tile with slack, the partition writes into them (a reservation past
+// a bucket's end is refused and flagged), and every bucket is one local_unique group whose keys end
+// where its cursor stopped.  Returns the distinct count with the sorted keys in *keys, or ~0 when
+// it does not apply (too little free HBM for the two slack-sized buffers) or a bucket or a group
+// overflowed -- then nothing the caller needs was touched and it runs the exact level.
+template <int L, bool COUNTED>
+static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbits, unsigned bp, unsigned bb,
+                                 uint32_t cmax) {
+    if constexpr (L != 1 || COUNTED) {
+        return ~0ull;
+    } else {
+        constexpr uint32_t SS = 8;
+        constexpr int TILE = MsdTraits<L>::TILE;
+        const uint64_t tiles = ceil_div(n, TILE);
+        if (c.use_lsd || !c.spec_final || tiles < 64 * SS || bb - bp > 9 || bb > 24) return ~0ull;
+        const uint64_t nb = 1ull << bb;
+        // the two slack-sized buffers must fit next to everything else
+        {
+            size_t fr = 0, tot = 0;
+            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            if ((double)n * 8.0 * 1.4 * 2.0 > 0.5 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
+                                                   (double)c.ws.held_slot(Workspace::SPEC_B))
+                return ~0ull;
+        }
+        uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nb * 4);
+        HIP_CHECK(hipMemsetAsync(h, 0, nb * 4, c.stream));
+        msd_hist_kernel<L><<<dim3((unsigned)ceil_div(tiles, SS)), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb,
+                                                                                                  bp, h, SS);
+        HIP_CHECK(hipGetLastError());
+        uint32_t *cap = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
+        spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap);
+        HIP_CHECK(hipGetLastError());
+        uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nb + 1) * 8);
+        {
+            uint32_t ep;
+            const uint64_t st = ceil_div(nb, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(cap, nb, bstart, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+        }
+        const uint64_t C = read_u64(c, (const unsigned long long *)(bstart + nb));
+        Key<L> *sa = (Key<L> *)c.ws.get(Workspace::SPEC_A, C * sizeof(Key<L>));
+        Key<L> *sb = (Key<L> *)c.ws.get(Workspace::SPEC_B, C * sizeof(Key<L>));
+        auto *cur = (unsigned long long *)c.ws.get(Workspace::SPEC_CUR, nb * 8);
+        HIP_CHECK(hipMemcpyAsync(cur, bstart, nb * 8, hipMemcpyDeviceToDevice, c.stream));
+        HIP_CHECK(hipMemsetAsync(&c.small->spec_ovf, 0, 4, c.stream));
+        EventTimer tm(c.stream);
+        tm.mark();
+        msd_partition_kernel<L, false><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, sa, nullptr, nullptr, n, nbits, bb, bp, cur, 1, (const unsigned long long *)(bstart + 1),
+            &c.small->spec_ovf);
+        HIP_CHECK(hipGetLastError());
+        tm.mark();
+        uint32_t povf = 0;
+        HIP_CHECK(hipMemcpyAsync(&povf, &c.small->spec_ovf, 4, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (c.track_partition && c.radix_launches == 0) {
+            c.radix_ms += tm.ms(0, 1);
+            c.radix_launches += 1;
+            c.radix_bytes += 2.0 * n * sizeof(Key<L>);
+        }
+        if (povf) {
+            if (c.debug) fprintf(stderr, "[mtg debug] speculative level: a bucket overflowed, exact level\n");
+            c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
+            return ~0ull;
+        }
+        // every bucket one group: [bstart[b], cur[b])
+        uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nb + 1) * 4);
+        uint32_t *ovf = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);
+        HIP_CHECK(hipMemsetAsync(ovf, 0, nb * 4, c.stream));
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        const bool keycas = nbits < 64;
+        if (keycas)
+            local_unique_kernel<1, false, true, 512, LocalTraits<1>::SLOTS / 2, false, 8>
+                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, nullptr, bstart, nullptr, nbits, bb, 0, sb, nullptr,
+                                                                 ucount, ovf, &c.small->counter, cmax, cur);
+        else
+            local_unique_kernel<1, false, false, 512, LocalTraits<1>::SLOTS / 2, false, 1>
+                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, nullptr, bstart, nullptr, nbits, bb, 0, sb, nullptr,
+                                                                 ucount, ovf, &c.small->counter, cmax, cur);
+        HIP_CHECK(hipGetLastError());
+        uint32_t novf = 0;
+        HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (novf) {
+            if (c.debug) fprintf(stderr, "[mtg debug] speculative level: %u groups overflowed, exact level\n", novf);
+            c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
+            return ~0ull;
+        }
+        uint64_t *ustart = (uint64_t *)c.ws.get(Workspace::MSD_USTART, (nb + 1) * 8);
+        {
+            uint32_t ep;
+            const uint64_t st = ceil_div(nb, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(ucount, nb, ustart, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+        }
+        const bool index = c.want_gidx;
+        uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8) : nullptr;
+        if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
+        group_gather_kernel<L, false><<<dim3((unsigned)nb), dim3(256), 0, c.stream>>>(
+            sb, nullptr, bstart, ustart, *keys, nullptr, nullptr, nbits - bb, gi, &c.small->gidx_bad);
+        HIP_CHECK(hipGetLastError());
+        uint64_t u = 0;
+        uint32_t ibad = 0;
+        HIP_CHECK(hipMemcpyAsync(&u, ustart + nb, 8, hipMemcpyDeviceToHost, c.stream));
+        if (index) {
+            HIP_CHECK(hipMemcpyAsync(gi + nb, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
+            HIP_CHECK(hipMemcpyAsync(gi + nb + 1, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
+            HIP_CHECK(hipMemcpyAsync(&ibad, &c.small->gidx_bad, 4, hipMemcpyDeviceToHost, c.stream));
+        }
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (index && !ibad) c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gi};
+        if (c.debug)
+            fprintf(stderr, "[mtg debug] speculative level: n=%lu capacity=%lu (%.2fx) -> %lu distinct\n",
+                    (unsigned long)n, (unsigned long)C, (double)C / (double)n, (unsigned long)u);
+        return u;
+    }
+}
+
 template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
@@ -532,7 +673,13 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         if (COUNTED) std::swap(*vals, *valt);
         b = T;
     } else {
-        for (unsigned lev = 1; lev <= levels; ++lev) run_level(lev);
+        for (unsigned lev = 1; lev <= levels; ++lev) {
+            if (lev == levels && lev == 2 && level1_done) {
+                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[1], digit_end[2], cmax);
+                if (u != ~0ull) return u;
+            }
+            run_level(lev);
+        }
     }
 
     while (true) {
@@ -740,20 +887,24 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         HIP_CHECK(hipGetLastError());
         // the output's bucket index over the top b bits comes out of the gather (the fused rc merge
         // of the canonical keys reuses it instead of a bucket_index pass: 0.44 ms at configs[1])
-        const bool index = gbucket_out && b > 0;
+        // (only for the sorts the fused rc merge follows: c.want_gidx)
+        const bool index = c.want_gidx && gbucket_out && b > 0;
         uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nbuckets + 2) * 8) : nullptr;
+        if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
         group_gather_kernel<L, COUNTED><<<dim3((unsigned)ngroups), dim3(256), 0, c.stream>>>(
             *alt, COUNTED ? *valt : nullptr, gstart, ustart, *keys, COUNTED ? *vals : nullptr, gbucket_out,
-            nbits - b, gi);
+            nbits - b, gi, &c.small->gidx_bad);
         HIP_CHECK(hipGetLastError());
         uint64_t u = 0;
+        uint32_t ibad = 0;
         HIP_CHECK(hipMemcpyAsync(&u, ustart + ngroups, 8, hipMemcpyDeviceToHost, c.stream));
         if (index) {  // entries nbuckets, nbuckets + 1 = the key count
             HIP_CHECK(hipMemcpyAsync(gi + nbuckets, ustart + ngroups, 8, hipMemcpyDeviceToDevice, c.stream));
             HIP_CHECK(hipMemcpyAsync(gi + nbuckets + 1, ustart + ngroups, 8, hipMemcpyDeviceToDevice, c.stream));
+            HIP_CHECK(hipMemcpyAsync(&ibad, &c.small->gidx_bad, 4, hipMemcpyDeviceToHost, c.stream));
         }
         HIP_CHECK(hipStreamSynchronize(c.stream));
-        if (index) c.gidx = Ctx::GroupIndex{*keys, u, b, nbits, gi};
+        if (index && !ibad) c.gidx = Ctx::GroupIndex{*keys, u, b, nbits, gi};
         return u;
     }
 }
@@ -1561,7 +1712,9 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     ev_extract = tm.mark();
 
     // ---- K2 sort + K3 unique / saturating count merge (ka)
+    c.want_gidx = canonical;  // the fused rc merge reads the canonical keys' bucket index
     U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
+    c.want_gidx = false;
     ev_sort = tm.mark();
     T.n_unique = U;
     debug_check_sorted(c, "collected k-mers", ka, U);
@@ -2209,8 +2362,10 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
         fp.digit_end[1] = B1;
         for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
         c.track_partition = true;
+        c.want_gidx = canonical;
         U = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup, dh1, false, nullptr, true,
                                         nullptr, &fp);
+        c.want_gidx = false;
         c.track_partition = false;
     }
     *ev_sort = tm.mark();
@@ -2433,8 +2588,10 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
                 // their counts add with saturation (sorted_multiset.cpp:54-84).  The keys cover ~1/P of
                 // the prefix space: P times denser buckets than their count says
                 const double dup1 = estimate_dup<L2>(c, xa, n1, 1.0) / d.P;
+                c.want_gidx = canonical;
                 T.n_unique = msd_sort_unique<L2, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup1, nullptr,
                                                           false, &runs);
+                c.want_gidx = false;
             }
         }
         }

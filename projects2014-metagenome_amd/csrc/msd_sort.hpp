@@ -47,11 +47,14 @@ template <int L>
 __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__restrict__ keys,
                                                              uint64_t n, unsigned nbits,
                                                              unsigned b, unsigned bp,
-                                                             uint32_t *__restrict__ counts) {
+                                                             uint32_t *__restrict__ counts,
+                                                             uint32_t tstride = 1) {
+    // tstride > 1: a sample -- workgroup i counts tile i * tstride (msd_sort_unique's speculative
+    // final level sizes its buckets from it)
     constexpr int TILE = MsdTraits<L>::TILE;
     constexpr int WMAX = MSD_WIN << 8;
     __shared__ uint32_t s_cnt[WMAX];
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t base = (uint64_t)blockIdx.x * tstride * TILE;
     const unsigned sub = b - bp;
     const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
     for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
@@ -190,9 +193,12 @@ template <int L, bool HAS_VAL, int BLOCK = MSD_BLOCK, bool NT = false>
 __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
-    unsigned long long *__restrict__ cursor, unsigned cstride = 1) {
+    unsigned long long *__restrict__ cursor, unsigned cstride = 1,
+    const unsigned long long *__restrict__ bend = nullptr, uint32_t *__restrict__ povf = nullptr) {
     // NT: nontemporal loads and stores (the streaming wide-digit pass: nothing it touches is
     // re-read from L2; measured 4.65 vs 4.67 ms on the cfg2 pass)
+    // bend (speculative buckets, sized from a sample): a reservation past its bucket's end writes
+    // nothing and raises *povf -- the caller then partitions again from the exact histogram
     constexpr int ITEMS = MsdTraits<L>::ITEMS;
     constexpr int TILE = ITEMS * BLOCK;
     constexpr int WMAX = MSD_WIN << 8;
@@ -235,8 +241,12 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
                 r[j] = atomicAdd(&s_cnt[lb], 1u);
             } else {  // outside the window: reserve and write directly
                 const unsigned long long o = atomicAdd(&cursor[(size_t)(lb + wbase) * cstride], 1ull);
-                kout[o] = k[j];
-                if (HAS_VAL) vout[o] = v[j];
+                if (bend && o >= bend[lb + wbase]) {
+                    *povf = 1u;
+                } else {
+                    kout[o] = k[j];
+                    if (HAS_VAL) vout[o] = v[j];
+                }
             }
         }
     }
@@ -258,7 +268,12 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
         const uint32_t i = tid * PER + q;
         if (i < wsize) {
             s_loff[i] = off;
-            s_gbase[i] = c[q] ? atomicAdd(&cursor[(size_t)(wbase + i) * cstride], (unsigned long long)c[q]) : 0;
+            unsigned long long gb = c[q] ? atomicAdd(&cursor[(size_t)(wbase + i) * cstride], (unsigned long long)c[q]) : 0;
+            if (bend && c[q] && gb + c[q] > bend[wbase + i]) {
+                *povf = 1u;
+                gb = ~0ull;  // this run is not written
+            }
+            s_gbase[i] = gb;
         }
         off += c[q];
     }
@@ -276,6 +291,7 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     for (uint32_t p = tid; p < total; p += BLOCK) {
         const Key<L> key = s_keys[p];
         const uint32_t lb = key_prefix(key, nbits, b) - wbase;
+        if (bend && s_gbase[lb] == ~0ull) continue;
         const uint64_t o = s_gbase[lb] + (p - s_loff[lb]);
         store_key(kout + o, key, NT);
         if (HAS_VAL) vout[o] = s_vals[p];
@@ -441,7 +457,8 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
     unsigned b, unsigned sbits, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
     uint32_t *__restrict__ ucount, uint32_t *__restrict__ overflow, uint32_t *__restrict__ novf,
-    uint32_t cmax) {
+    uint32_t cmax, const unsigned long long *__restrict__ gend = nullptr) {
+    // gend (speculative buckets): group g is [gstart[g], gend[g]), with gaps between groups
     constexpr int SLOTS = SL;
     constexpr uint32_t LIMIT = SL / 2;
     constexpr uint64_t EMPTY = ~0ull;
@@ -459,7 +476,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __shared__ int s_hb;
 
     const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
-    const uint64_t g0 = gstart[g], g1 = gstart[g + 1];
+    const uint64_t g0 = gstart[g], g1 = gend ? (uint64_t)gend[g] : gstart[g + 1];
     const uint32_t tid = threadIdx.x;
     if (g0 >= g1) {
         if (tid == 0) ucount[g] = 0;
@@ -768,6 +785,9 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             if (COUNTED) sscr[p] = s_sum[i];
         }
         __syncthreads();
+        // (staging the sorted run in LDS for one coalesced store halves the HBM write bytes -- PMC
+        // WRITE_SIZE 2.89 GB for 1.5 GB of keys stored one by one at their ranks -- but the extra
+        // barrier cost more: sort stage 10.5 -> 11.0 ms)
         for (uint32_t p = tid; p < D; p += LB) {
             const Key<L> key = scratch[p];
             const uint32_t d = bits_at(key, dshift, 8);
@@ -941,10 +961,16 @@ __global__ __launch_bounds__(256) void group_gather_kernel(
     const Key<L> *__restrict__ tmp, const uint32_t *__restrict__ tcnt,
     const uint64_t *__restrict__ gstart, const uint64_t *__restrict__ ustart,
     Key<L> *__restrict__ out, uint32_t *__restrict__ ocnt, const uint64_t *__restrict__ gbucket = nullptr,
-    unsigned ishift = 0, uint64_t *__restrict__ istart = nullptr) {
+    unsigned ishift = 0, uint64_t *__restrict__ istart = nullptr, uint32_t *__restrict__ ibad = nullptr) {
+    // a run of more than IRUN empty buckets between two keys would be one thread's serial loop:
+    // the index is abandoned (*ibad) and the caller builds it with bucket_index_kernel
+    constexpr uint64_t IRUN = 4096;
     const uint64_t g = blockIdx.x;
     const uint64_t src = gstart[g], dst = ustart[g], m = ustart[g + 1] - dst;
-    const uint64_t gb0 = istart ? gbucket[g] : 0;
+    // gbucket == nullptr: one bucket per group (the speculative final level)
+    const uint64_t gb0 = istart ? (gbucket ? gbucket[g] : g) : 0;
+    const uint64_t gb1 = istart ? (gbucket ? gbucket[g + 1] : g + 1) : 0;
+    bool bad = false;
     for (uint64_t i = threadIdx.x; i < m; i += 256) {
         const Key<L> key = tmp[src + i];
         out[dst + i] = key;
@@ -952,12 +978,15 @@ __global__ __launch_bounds__(256) void group_gather_kernel(
         if (istart) {  // buckets (previous key's, this key's] start here
             const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
             const uint64_t pb = i == 0 ? gb0 - 1 : bits_at(shr(tmp[src + i - 1], ishift), 0, 32);
-            for (uint64_t x = pb + 1; x <= kb; ++x) istart[x] = dst + i;
+            if (kb - pb > IRUN) bad = true;
+            else for (uint64_t x = pb + 1; x <= kb; ++x) istart[x] = dst + i;
         }
     }
     if (istart) {  // the group's buckets after its last key start at its end
         const uint64_t lb = m ? bits_at(shr(tmp[src + m - 1], ishift), 0, 32) : gb0 - 1;
-        for (uint64_t x = lb + 1 + threadIdx.x; x < gbucket[g + 1]; x += 256) istart[x] = dst + m;
+        if (gb1 - (lb + 1) > 256 * IRUN) bad = true;
+        else for (uint64_t x = lb + 1 + threadIdx.x; x < gb1; x += 256) istart[x] = dst + m;
+        if (bad) atomicOr(ibad, 1u);
     }
 }
 
