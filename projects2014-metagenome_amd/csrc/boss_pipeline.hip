@@ -147,6 +147,9 @@ class EventTimer {
 struct Ctx {
     Workspace ws;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;            // a second stream for independent small launches (the dup sample)
+    hipEvent_t side_in = nullptr, side_out = nullptr;
+    bool use_side = true;                  // MTG_SIDE=0: everything on the build stream
     Small *small = nullptr;
     mtg_boss_timings timings{};
     uint32_t epoch = 0;           // look-back granule epoch of the last launch
@@ -216,6 +219,7 @@ static void load_knobs(Ctx &c) {
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
     c.spec_final = !is("MTG_SPEC", "0");
+    c.use_side = !is("MTG_SIDE", "0");
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
     c.force_spill = is("MTG_SPILL", "1");
@@ -448,12 +452,26 @@ __global__ void spec_caps_kernel(const uint32_t *__restrict__ sample, uint64_t n
 // where its cursor stopped.  Returns the distinct count with the sorted keys in *keys, or ~0 when
 // it does not apply (too little free HBM for the two slack-sized buffers) or a bucket or a group
 // overflowed -- then nothing the caller needs was touched and it runs the exact level.
+// spec_counts_kernel: the keys each speculative bucket received (its cursor minus its start)
+__global__ void spec_counts_kernel(const uint64_t *__restrict__ bstart, const unsigned long long *__restrict__ cur,
+                                   uint64_t nb, uint32_t *__restrict__ cnt) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) cnt[b] = (uint32_t)(cur[b] - bstart[b]);
+}
+
+// rm (the rc sort fused with the merge, distinct input): the same buckets go to local_merge_kernel,
+// one bucket per group, each group's output after the canonical keys before its bucket (cidx, the
+// canonical sort's bucket index) and the rc keys the buckets before it received.
 template <int L, bool COUNTED>
 static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbits, unsigned bp, unsigned bb,
-                                 uint32_t cmax) {
+                                 uint32_t cmax, bool distinct, RcMerge<L> *rm, const Ctx::GroupIndex &cidx) {
     if constexpr (L != 1 || COUNTED) {
         return ~0ull;
     } else {
+        if (distinct != (rm != nullptr)) return ~0ull;  // the plain unique, or the fused rc merge
+        if (rm && !(cidx.keys == (const void *)rm->ck && cidx.n == rm->nc && cidx.bits == bb && cidx.nbits == nbits &&
+                    bb <= 32 && (!rm->istart || rm->ib >= bb)))
+            return ~0ull;
         constexpr uint32_t SS = 8;
         constexpr int TILE = MsdTraits<L>::TILE;
         const uint64_t tiles = ceil_div(n, TILE);
@@ -510,6 +528,65 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             if (c.debug) fprintf(stderr, "[mtg debug] speculative level: a bucket overflowed, exact level\n");
             c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
             return ~0ull;
+        }
+        if (rm) {  // the fused rc merge over the speculative buckets
+            uint32_t *cnt = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
+            spec_counts_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(bstart, cur, nb, cnt);
+            HIP_CHECK(hipGetLastError());
+            uint64_t *gbase = (uint64_t *)c.ws.get(Workspace::MSD_USTART, (nb + 1) * 8);
+            {
+                uint32_t ep;
+                const uint64_t st = ceil_div(nb, 4096);
+                uint64_t *desc = acquire_desc(c, st, &ep);
+                HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+                scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(cnt, nb, gbase, desc, ep,
+                                                                                  &c.small->counter, &c.small->error);
+                HIP_CHECK(hipGetLastError());
+            }
+            constexpr int CAP = MergeLocalTraits<L>::CAP;
+            uint32_t *gflag = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);
+            HIP_CHECK(hipMemsetAsync(gflag, 0, nb * 4, c.stream));
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            uint64_t *istart = rm->istart;
+            local_merge_kernel<L, false, CAP><<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(
+                sa, nullptr, bstart, nullptr, nullptr, rm->ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase);
+            HIP_CHECK(hipGetLastError());
+            uint32_t novf = 0;
+            HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            if (novf) {  // the few big groups again with twice the LDS arrays
+                std::vector<uint32_t> fl(nb), list;
+                HIP_CHECK(hipMemcpyAsync(fl.data(), gflag, nb * 4, hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));
+                for (uint64_t g = 0; g < nb; ++g)
+                    if (fl[g]) list.push_back((uint32_t)g);
+                uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
+                HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
+                HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+                local_merge_kernel<L, false, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
+                    sa, nullptr, bstart, nullptr, dlist, rm->ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase);
+                HIP_CHECK(hipGetLastError());
+                HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
+            }
+            if (novf) {
+                if (c.debug) fprintf(stderr, "[mtg debug] speculative rc level: %u groups overflowed, exact level\n", novf);
+                c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
+                return ~0ull;
+            }
+            rm->done = true;
+            if (istart) {  // index end = the merged count
+                const uint64_t R = n + rm->nc;
+                HIP_CHECK(hipMemcpyAsync(istart + (1ull << rm->ib), &R, 8, hipMemcpyHostToDevice, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));  // R is a host local
+                note_bucket_index(c, rm->out, R, istart, nbits - rm->ib);
+            }
+            if (c.debug)
+                fprintf(stderr, "[mtg debug] speculative rc level: n=%lu capacity=%lu -> merged %lu\n", (unsigned long)n,
+                        (unsigned long)C, (unsigned long)(n + rm->nc));
+            return n;
         }
         // every bucket one group: [bstart[b], cur[b])
         uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nb + 1) * 4);
@@ -674,8 +751,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         b = T;
     } else {
         for (unsigned lev = 1; lev <= levels; ++lev) {
-            if (lev == levels && lev == 2 && level1_done) {
-                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[1], digit_end[2], cmax);
+            if (lev == levels && lev == 2 && (level1_done || (rm && distinct))) {  // level 1 is in place
+                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[1], digit_end[2], cmax,
+                                                                distinct, rm, saved_gidx);
                 if (u != ~0ull) return u;
             }
             run_level(lev);
@@ -1063,13 +1141,21 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
     } else {
         const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
         if (!c.fused || c.use_lsd || npos < c.fused_min || npos < 4096 || K - 1 < FUSED_HB / 2) return false;
-        // the duplication estimate from a sample of windows
+        // the duplication estimate from a sample of windows, on the side stream: a latency-bound
+        // 0.26 ms launch that overlaps pass A
         constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
         unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
-        HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
-        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
-                                                                            M, table, SLOTS - 1, table + SLOTS);
+        const bool side = c.side && c.use_side;
+        hipStream_t ss = side ? c.side : c.stream;
+        if (side) {
+            HIP_CHECK(hipEventRecord(c.side_in, c.stream));
+            HIP_CHECK(hipStreamWaitEvent(c.side, c.side_in, 0));
+        }
+        HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, ss));
+        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, ss>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                      M, table, SLOTS - 1, table + SLOTS);
         HIP_CHECK(hipGetLastError());
+        if (side) HIP_CHECK(hipEventRecord(c.side_out, c.side));
         // pass A: histogram of the top bits of every valid k-mer
         constexpr int TILE = ExtractTraits<1>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
@@ -1106,6 +1192,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         std::vector<uint32_t> h(nbh);
         unsigned long long st[2];
         HIP_CHECK(hipMemcpyAsync(h.data(), h12, nbh * 4, hipMemcpyDeviceToHost, c.stream));
+        if (side) HIP_CHECK(hipStreamWaitEvent(c.stream, c.side_out, 0));
         HIP_CHECK(hipMemcpyAsync(st, table + SLOTS, 16, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
         uint64_t N = 0;
@@ -3514,6 +3601,9 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
     try {
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.side, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&c->ctx.side_in, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&c->ctx.side_out, hipEventDisableTiming));
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
         load_knobs(c->ctx);
         c->ctx.mem_budget = p->memory_preallocated;
@@ -3535,6 +3625,9 @@ void mtg_boss_ctor_destroy(mtg_boss_ctor *c) {
     if (c->ctx.stream) (void)hipStreamSynchronize(c->ctx.stream);
     if (c->ctx.small) (void)hipFree(c->ctx.small);
     if (c->ctx.stream) (void)hipStreamDestroy(c->ctx.stream);
+    if (c->ctx.side) (void)hipStreamDestroy(c->ctx.side);
+    if (c->ctx.side_in) (void)hipEventDestroy(c->ctx.side_in);
+    if (c->ctx.side_out) (void)hipEventDestroy(c->ctx.side_out);
     delete c;
 }
 

@@ -832,9 +832,12 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     const uint64_t *__restrict__ gbucket, const uint32_t *__restrict__ glist, const Key<L> *__restrict__ ck,
     const uint32_t *__restrict__ cv, const uint64_t *__restrict__ cstart, Key<L> *__restrict__ out,
     uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf,
-    unsigned b, unsigned nbits, unsigned ib, uint64_t *__restrict__ istart) {
+    unsigned b, unsigned nbits, unsigned ib, uint64_t *__restrict__ istart,
+    const unsigned long long *__restrict__ gend = nullptr, const uint64_t *__restrict__ gbase = nullptr) {
     // istart (optional): the bucket index over the top ib >= b bits of the merged output that the
-    // dummy stage uses (bucket_index_kernel's layout); the group fills the entries of its range
+    // dummy stage uses (bucket_index_kernel's layout); the group fills the entries of its range.
+    // gend (speculative buckets, one per group, gbucket == nullptr): the group's rc keys are
+    // [gstart[g], gend[g]) with gaps between groups, and gbase[g] counts the rc keys before it
     __shared__ Key<L> s_r[CAP];  // rc keys, then sorted
     __shared__ Key<L> s_s[CAP];  // rc keys by sub-bucket
     __shared__ Key<L> s_c[CAP];  // canonical keys of the range
@@ -843,8 +846,9 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     __shared__ int s_hb;
     const uint32_t tid = threadIdx.x;
     const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
-    const uint64_t g0 = gstart[g], g1 = gstart[g + 1];
-    const uint64_t c0 = cstart[gbucket[g]], c1 = cstart[gbucket[g + 1]];
+    const uint64_t g0 = gstart[g], g1 = gend ? (uint64_t)gend[g] : gstart[g + 1];
+    const uint64_t gb0 = gbucket ? gbucket[g] : g, gb1 = gbucket ? gbucket[g + 1] : g + 1;
+    const uint64_t c0 = cstart[gb0], c1 = cstart[gb1];
     if (g1 - g0 > (uint64_t)CAP || c1 - c0 > (uint64_t)CAP) {
         if (tid == 0) {
             gflag[g] = 1;
@@ -920,10 +924,10 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         if (s_r[mid] < s_c[o0 - mid - 1]) lo = mid + 1; else hi = mid;
     }
     uint32_t i = lo, j = o0 - lo;
-    const uint64_t base = c0 + g0;
+    const uint64_t base = c0 + (gbase ? gbase[g] : g0);
     const unsigned ishift = nbits - ib;
     // index bucket of the output before o0 (or the first bucket of the group's range - 1)
-    const uint64_t ifirst = gbucket[g] << (ib - b), iend = gbucket[g + 1] << (ib - b);
+    const uint64_t ifirst = gb0 << (ib - b), iend = gb1 << (ib - b);
     uint64_t prevb = ifirst - 1;
     if (istart && o0 > 0 && o0 < o1) {
         const uint32_t pi = lo, pj = o0 - lo;  // the merged element o0 - 1
