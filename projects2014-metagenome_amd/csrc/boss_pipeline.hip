@@ -147,9 +147,6 @@ class EventTimer {
 struct Ctx {
     Workspace ws;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;            // a second stream for independent small launches (the dup sample)
-    hipEvent_t side_in = nullptr, side_out = nullptr;
-    bool use_side = true;                  // MTG_SIDE=0: everything on the build stream
     Small *small = nullptr;
     mtg_boss_timings timings{};
     uint32_t epoch = 0;           // look-back granule epoch of the last launch
@@ -219,7 +216,6 @@ static void load_knobs(Ctx &c) {
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
     c.spec_final = !is("MTG_SPEC", "0");
-    c.use_side = !is("MTG_SIDE", "0");
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
     c.force_spill = is("MTG_SPILL", "1");
@@ -1141,21 +1137,14 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
     } else {
         const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
         if (!c.fused || c.use_lsd || npos < c.fused_min || npos < 4096 || K - 1 < FUSED_HB / 2) return false;
-        // the duplication estimate from a sample of windows, on the side stream: a latency-bound
-        // 0.26 ms launch that overlaps pass A
+        // the duplication estimate from a sample of windows (on a side stream it overlapped pass A but
+        // measured no faster: 26.3 vs 26.2 ms per step)
         constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
         unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
-        const bool side = c.side && c.use_side;
-        hipStream_t ss = side ? c.side : c.stream;
-        if (side) {
-            HIP_CHECK(hipEventRecord(c.side_in, c.stream));
-            HIP_CHECK(hipStreamWaitEvent(c.side, c.side_in, 0));
-        }
-        HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, ss));
-        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, ss>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+        HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
+        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
                                                                       M, table, SLOTS - 1, table + SLOTS);
         HIP_CHECK(hipGetLastError());
-        if (side) HIP_CHECK(hipEventRecord(c.side_out, c.side));
         // pass A: histogram of the top bits of every valid k-mer
         constexpr int TILE = ExtractTraits<1>::TILE;
         const uint64_t tiles = ceil_div(npos, TILE);
@@ -1192,7 +1181,6 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         std::vector<uint32_t> h(nbh);
         unsigned long long st[2];
         HIP_CHECK(hipMemcpyAsync(h.data(), h12, nbh * 4, hipMemcpyDeviceToHost, c.stream));
-        if (side) HIP_CHECK(hipStreamWaitEvent(c.stream, c.side_out, 0));
         HIP_CHECK(hipMemcpyAsync(st, table + SLOTS, 16, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
         uint64_t N = 0;
@@ -3601,9 +3589,6 @@ mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *p) {
     try {
         HIP_CHECK(hipSetDevice(c->device));
         HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&c->ctx.side, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&c->ctx.side_in, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&c->ctx.side_out, hipEventDisableTiming));
         HIP_CHECK(hipMalloc(&c->ctx.small, sizeof(Small)));
         load_knobs(c->ctx);
         c->ctx.mem_budget = p->memory_preallocated;
@@ -3625,9 +3610,6 @@ void mtg_boss_ctor_destroy(mtg_boss_ctor *c) {
     if (c->ctx.stream) (void)hipStreamSynchronize(c->ctx.stream);
     if (c->ctx.small) (void)hipFree(c->ctx.small);
     if (c->ctx.stream) (void)hipStreamDestroy(c->ctx.stream);
-    if (c->ctx.side) (void)hipStreamDestroy(c->ctx.side);
-    if (c->ctx.side_in) (void)hipEventDestroy(c->ctx.side_in);
-    if (c->ctx.side_out) (void)hipEventDestroy(c->ctx.side_out);
     delete c;
 }
 
