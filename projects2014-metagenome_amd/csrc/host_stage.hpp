@@ -217,16 +217,18 @@ class HostStage {
     // (windows never span an invalid char, so a run maps each of its windows to the right count),
     // and a batch without counts is one run -- no per-read bookkeeping on the common path.
     void add(const char *const *ptrs, const uint64_t *lens, const uint64_t *counts, size_t n, unsigned threads) {
-        add_reads(n, [&](size_t i) { return ptrs[i]; }, [&](size_t i) { return lens[i]; }, counts, threads);
+        add_reads(n, [&](size_t i) { return ptrs[i]; }, [&](size_t i) { return lens[i]; }, counts, threads, nullptr);
     }
     // n reads back to back in `data`, read i = [offsets[i], offsets[i + 1])
     void add_packed(const char *data, const uint64_t *offsets, const uint64_t *counts, size_t n, unsigned threads) {
+        // reads back to back: a read's last partial block may load bytes of the next read (masked
+        // off), up to the end of the last read
         add_reads(n, [&](size_t i) { return data + offsets[i]; },
-                  [&](size_t i) { return offsets[i + 1] - offsets[i]; }, counts, threads);
+                  [&](size_t i) { return offsets[i + 1] - offsets[i]; }, counts, threads, data + offsets[n]);
     }
 
     template <typename Ptr, typename Len>
-    void add_reads(size_t n, Ptr ptr, Len len, const uint64_t *counts, unsigned threads) {
+    void add_reads(size_t n, Ptr ptr, Len len, const uint64_t *counts, unsigned threads, const char *load_end) {
         if (!n) return;
         // chunk c packs reads [n c / t, n (c + 1) / t) from char cbase[c] (a multiple of 32)
         const unsigned t = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(std::max(1u, threads), n / 4096));
@@ -314,6 +316,14 @@ class HostStage {
                             pack32_avx2(p + j, &codes, &valid);
                             put(codes, valid, 32);
                         }
+                        if (j < l && load_end && p + j + 32 <= load_end) {
+                            // the tail straight from the buffer, masked, with the separator (an invalid
+                            // char) in the same put: 3.3-4.3 -> 5.0-5.3 GB/s per thread on 150-char reads
+                            const unsigned m = (unsigned)(l - j);
+                            pack32_avx2(p + j, &codes, &valid);
+                            put(codes & ((1ull << (2 * m)) - 1), valid & ((1u << m) - 1), m + 1);
+                            goto next_read;
+                        }
                         if (j < l) {  // the tail through a zero-padded copy (zero bytes are invalid)
                             const unsigned m = (unsigned)(l - j);
                             alignas(32) char tail[32] = {};
@@ -329,6 +339,7 @@ class HostStage {
                         put(codes, valid, m);
                     }
                     put(0, 0, 1);  // the separator
+                next_read:
                     if (mirror && w - piece >= kPieceWords) {
                         send(piece, w - piece);
                         piece = w;
