@@ -457,6 +457,43 @@ __global__ __launch_bounds__(256) void rc_map_kernel(const Key<L> *__restrict__ 
     }
 }
 
+// rc_map_kernel over a canonical set left in its speculative buckets (Ctx::gap in boss_pipeline.hip):
+// bucket g's keys keys[bstart[g] ..) map to rc_out[ustart[g] .. ustart[g + 1]), one wave per bucket,
+// 4 loads in flight per lane
+template <int L>
+__global__ __launch_bounds__(256) void rc_map_gapped_kernel(const Key<L> *__restrict__ keys,
+                                                            const uint64_t *__restrict__ bstart,
+                                                            const uint64_t *__restrict__ ustart, uint64_t nb,
+                                                            Key<L> *__restrict__ rc_out, unsigned K,
+                                                            uint32_t *__restrict__ hist, unsigned hist_bits) {
+    __shared__ uint32_t s_hist[512];
+    if (hist_bits)
+        for (uint32_t i = threadIdx.x; i < (1u << hist_bits); i += 256) s_hist[i] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint64_t g = (uint64_t)blockIdx.x * 4 + wid; g < nb; g += (uint64_t)gridDim.x * 4) {
+        const uint64_t src = bstart[g], dst = ustart[g], m = ustart[g + 1] - dst;
+        for (uint64_t i0 = lane; i0 < m; i0 += 256) {
+            Key<L> x[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (i0 + 64 * q < m) x[q] = keys[src + i0 + 64 * q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (i0 + 64 * q >= m) break;
+                const Key<L> r = revcomp2(x[q], K);
+                rc_out[dst + i0 + 64 * q] = r;
+                if (hist_bits) atomicAdd(&s_hist[bits_at(r, 2 * K - hist_bits, hist_bits)], 1u);
+            }
+        }
+    }
+    if (hist_bits) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < (1u << hist_bits); i += 256)
+            if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
+    }
+}
+
 /*
  * Bucket index over the top B bits of a sorted 2K-bit key array: start[b] = lower_bound of the
  * first key whose top bits are >= b.  Turns every membership probe below into a short binary

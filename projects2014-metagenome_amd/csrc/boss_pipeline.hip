@@ -64,7 +64,7 @@ class Workspace {
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
-        SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, NSLOTS
+        SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -191,6 +191,20 @@ struct Ctx {
         const uint64_t *start = nullptr;
     } gidx;
     bool want_gidx = false;  // the next msd_sort_unique's output feeds the fused rc merge
+    // the single build's canonical set left in the speculative level's bucket layout (no
+    // group_gather_kernel): bucket g's keys at keys[bstart[g] ..), compact at ustart[g] ..
+    // (ustart[g + 1] - ustart[g] keys).  rc_map and the fused rc merge read it there;
+    // ensure_compact() writes the compact array to dst when anything else needs it.
+    struct GappedSet {
+        bool valid = false;
+        const void *keys = nullptr;
+        void *dst = nullptr;
+        uint64_t u = 0, nb = 0;
+        const uint64_t *bstart = nullptr, *ustart = nullptr;
+    } gap;
+    bool defer_gather_req = false;  // set around the single build's canonical collect
+    bool defer_gather = true;       // MTG_DEFER_GATHER=0: the speculative level always gathers
+    bool spec_rc = true;            // MTG_SPEC_RC=0: the rc sort's final level exact (tests the fallbacks)
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
@@ -216,6 +230,8 @@ static void load_knobs(Ctx &c) {
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
     c.spec_final = !is("MTG_SPEC", "0");
+    c.defer_gather = !is("MTG_DEFER_GATHER", "0");
+    c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
     c.force_spill = is("MTG_SPILL", "1");
@@ -455,6 +471,17 @@ __global__ void spec_counts_kernel(const uint64_t *__restrict__ bstart, const un
     if (b < nb) cnt[b] = (uint32_t)(cur[b] - bstart[b]);
 }
 
+// the deferred gather of a canonical set left in bucket layout (Ctx::gap), for a consumer that reads
+// it compact
+static void ensure_compact(Ctx &c) {
+    if (!c.gap.valid) return;
+    c.gap.valid = false;
+    if (!c.gap.nb) return;
+    group_gather_kernel<1, false><<<dim3((unsigned)c.gap.nb), dim3(256), 0, c.stream>>>(
+        (const Key<1> *)c.gap.keys, nullptr, c.gap.bstart, c.gap.ustart, (Key<1> *)c.gap.dst, nullptr);
+    HIP_CHECK(hipGetLastError());
+}
+
 // rm (the rc sort fused with the merge, distinct input): the same buckets go to local_merge_kernel,
 // one bucket per group, each group's output after the canonical keys before its bucket (cidx, the
 // canonical sort's bucket index) and the rc keys the buckets before it received.
@@ -465,6 +492,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         return ~0ull;
     } else {
         if (distinct != (rm != nullptr)) return ~0ull;  // the plain unique, or the fused rc merge
+        if (rm && !c.spec_rc) return ~0ull;
         if (rm && !(cidx.keys == (const void *)rm->ck && cidx.n == rm->nc && cidx.bits == bb && cidx.nbits == nbits &&
                     bb <= 32 && (!rm->istart || rm->ib >= bb)))
             return ~0ull;
@@ -501,7 +529,6 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         }
         const uint64_t C = read_u64(c, (const unsigned long long *)(bstart + nb));
         Key<L> *sa = (Key<L> *)c.ws.get(Workspace::SPEC_A, C * sizeof(Key<L>));
-        Key<L> *sb = (Key<L> *)c.ws.get(Workspace::SPEC_B, C * sizeof(Key<L>));
         auto *cur = (unsigned long long *)c.ws.get(Workspace::SPEC_CUR, nb * 8);
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nb * 8, hipMemcpyDeviceToDevice, c.stream));
         HIP_CHECK(hipMemsetAsync(&c.small->spec_ovf, 0, 4, c.stream));
@@ -544,9 +571,14 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             HIP_CHECK(hipMemsetAsync(gflag, 0, nb * 4, c.stream));
             HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
             uint64_t *istart = rm->istart;
+            // the canonical keys where they are: compact, or still in their own bucket layout (c.gap,
+            // whose compact index is cidx.start)
+            const bool gapped = c.gap.valid && c.gap.dst == (const void *)rm->ck;
+            const Key<L> *ck = gapped ? (const Key<L> *)c.gap.keys : rm->ck;
+            const uint64_t *cgap = gapped ? c.gap.bstart : nullptr;
             local_merge_kernel<L, false, CAP><<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(
-                sa, nullptr, bstart, nullptr, nullptr, rm->ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
-                &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase);
+                sa, nullptr, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
             HIP_CHECK(hipGetLastError());
             uint32_t novf = 0;
             HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
@@ -561,8 +593,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
                 HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
                 local_merge_kernel<L, false, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
-                    sa, nullptr, bstart, nullptr, dlist, rm->ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
-                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase);
+                    sa, nullptr, bstart, nullptr, dlist, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
                 HIP_CHECK(hipGetLastError());
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
                 HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
@@ -573,6 +605,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
                 return ~0ull;
             }
             rm->done = true;
+            if (gapped) c.gap.valid = false;  // merged: the canonical set is not needed compact
             if (istart) {  // index end = the merged count
                 const uint64_t R = n + rm->nc;
                 HIP_CHECK(hipMemcpyAsync(istart + (1ull << rm->ib), &R, 8, hipMemcpyHostToDevice, c.stream));
@@ -585,6 +618,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             return n;
         }
         // every bucket one group: [bstart[b], cur[b])
+        Key<L> *sb = (Key<L> *)c.ws.get(Workspace::SPEC_B, C * sizeof(Key<L>));
         uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nb + 1) * 4);
         uint32_t *ovf = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);
         HIP_CHECK(hipMemsetAsync(ovf, 0, nb * 4, c.stream));
@@ -616,6 +650,22 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(ucount, nb, ustart, desc, ep,
                                                                               &c.small->counter, &c.small->error);
             HIP_CHECK(hipGetLastError());
+        }
+        if (c.defer_gather_req && c.defer_gather && c.want_gidx) {
+            // the fused rc merge follows: leave the distinct keys in their buckets (Ctx::gap); the
+            // compact index of bucket g is ustart[g] (one bucket per group)
+            uint64_t *gb = (uint64_t *)c.ws.get(Workspace::GAP_BSTART, (nb + 1) * 8);
+            uint64_t *gu = (uint64_t *)c.ws.get(Workspace::GAP_USTART, (nb + 2) * 8);
+            HIP_CHECK(hipMemcpyAsync(gb, bstart, (nb + 1) * 8, hipMemcpyDeviceToDevice, c.stream));
+            HIP_CHECK(hipMemcpyAsync(gu, ustart, (nb + 1) * 8, hipMemcpyDeviceToDevice, c.stream));
+            HIP_CHECK(hipMemcpyAsync(gu + nb + 1, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
+            const uint64_t u = read_u64(c, (const unsigned long long *)(ustart + nb));
+            c.gap = Ctx::GappedSet{true, sb, *keys, u, nb, gb, gu};
+            c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gu};
+            if (c.debug)
+                fprintf(stderr, "[mtg debug] speculative level: n=%lu capacity=%lu (%.2fx) -> %lu distinct, left in buckets\n",
+                        (unsigned long)n, (unsigned long)C, (double)C / (double)n, (unsigned long)u);
+            return u;
         }
         const bool index = c.want_gidx;
         uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8) : nullptr;
@@ -772,6 +822,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             uint64_t *cstart = nullptr;
             const uint64_t *gsize = bstart;
             if (fuse) {
+                ensure_compact(c);  // this path reads the canonical keys compact
                 // fused rc merge: the canonical keys of every bucket (bucket index of the sorted
                 // set), and groups sized by rc + canonical keys together
                 if (saved_gidx.keys == (const void *)rm->ck && saved_gidx.n == rm->nc && saved_gidx.bits == b &&
@@ -1445,10 +1496,25 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
                 HIP_CHECK(hipMemsetAsync(rc_hist, 0, (1u << rc_hist_bits) * 4, c.stream));
             }
         }
-        rc_map_kernel<L2, COUNTED><<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256 * 4), 16384)),
-                                     dim3(256), 0, c.stream>>>(ka, ca, buf, bufc, U, K, rc_hist, rc_hist_bits);
-        HIP_CHECK(hipGetLastError());
+        bool done = false;
+        if constexpr (!COUNTED) {
+            if (c.gap.valid && c.gap.dst == (const void *)ka && sort) {
+                // the canonical set still in its speculative buckets (Ctx::gap): read it there
+                rc_map_gapped_kernel<L2><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(c.gap.nb, 16), 16384))),
+                                           dim3(256), 0, c.stream>>>((const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart,
+                                                                     c.gap.nb, buf, K, rc_hist, rc_hist_bits);
+                HIP_CHECK(hipGetLastError());
+                done = true;
+            }
+        }
+        if (!done) {
+            ensure_compact(c);
+            rc_map_kernel<L2, COUNTED><<<dim3((unsigned)std::min<uint64_t>(ceil_div(U, 256 * 4), 16384)),
+                                         dim3(256), 0, c.stream>>>(ka, ca, buf, bufc, U, K, rc_hist, rc_hist_bits);
+            HIP_CHECK(hipGetLastError());
+        }
     } else {
+        ensure_compact(c);
         reset_small(c);
         const uint64_t tiles = ceil_div(U, 1024);
         uint32_t desc_ep;
@@ -1751,6 +1817,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     mtg_boss_timings &T = c.timings;
     T = mtg_boss_timings{};
     note_bucket_index(c, nullptr, 0, nullptr, 0);
+    c.gap = Ctx::GappedSet{};
     T.world = 1;
     T.n_batches = 1;
     HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
@@ -1788,10 +1855,13 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
 
     // ---- K2 sort + K3 unique / saturating count merge (ka)
     c.want_gidx = canonical;  // the fused rc merge reads the canonical keys' bucket index
+    c.defer_gather_req = canonical;  // ... and may read them in their speculative buckets (Ctx::gap)
     U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
+    c.defer_gather_req = false;
     c.want_gidx = false;
     ev_sort = tm.mark();
     T.n_unique = U;
+    if (c.debug) ensure_compact(c);
     debug_check_sorted(c, "collected k-mers", ka, U);
     ev_unique = tm.mark();
 
@@ -1813,10 +1883,14 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         rm.istart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << rm.ib) + 2) * 8);
         const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc, &rm);
         R = U + Urc;
-        if (!rm.done) merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, rk, rkc, Urc, K, real, realc, 0);
+        if (!rm.done) {
+            ensure_compact(c);
+            merge_sorted<L2, L2, false, COUNTED, true>(c, ka, ca, U, rk, rkc, Urc, K, real, realc, 0);
+        }
         ka = real;
         ca = realc;
     }
+    ensure_compact(c);  // (a no-op unless the canonical set is still in buckets)
     T.n_real = R;
     debug_check_sorted(c, "real k-mers", ka, R);
     const int ev_rc = tm.mark();

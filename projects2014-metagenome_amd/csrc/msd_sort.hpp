@@ -833,7 +833,11 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     const uint32_t *__restrict__ cv, const uint64_t *__restrict__ cstart, Key<L> *__restrict__ out,
     uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf,
     unsigned b, unsigned nbits, unsigned ib, uint64_t *__restrict__ istart,
-    const unsigned long long *__restrict__ gend = nullptr, const uint64_t *__restrict__ gbase = nullptr) {
+    const unsigned long long *__restrict__ gend = nullptr, const uint64_t *__restrict__ gbase = nullptr,
+    const uint64_t *__restrict__ cgap = nullptr) {
+    // cgap (optional, one bucket per group): the canonical keys of bucket g are read at ck[cgap[g] ..)
+    // (a set left in its speculative buckets) instead of ck[cstart[g] ..); cstart stays their compact
+    // index
     // istart (optional): the bucket index over the top ib >= b bits of the merged output that the
     // dummy stage uses (bucket_index_kernel's layout); the group fills the entries of its range.
     // gend (speculative buckets, one per group, gbucket == nullptr): the group's rc keys are
@@ -861,9 +865,10 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         s_r[i] = keys[g0 + i];
         if (COUNTED) s_rv[i] = vals[g0 + i];
     }
+    const uint64_t cr = cgap ? cgap[gb0] : c0;
     for (uint32_t i = tid; i < nc; i += LB) {
-        s_c[i] = ck[c0 + i];
-        if (COUNTED) s_cv[i] = cv[c0 + i];
+        s_c[i] = ck[cr + i];
+        if (COUNTED) s_cv[i] = cv[cr + i];
     }
     if (tid < 256) {
         s_hist[tid] = 0;

@@ -62,6 +62,19 @@ def test_bench_generator_2m_reads_k31(canonical, bits):
     _assert_same(got, want, "2M reads k=31 canonical=%s bits=%d" % (canonical, bits))
 
 
+@pytest.mark.parametrize("knob", ["MTG_SPEC_RC", "MTG_DEFER_GATHER"])
+def test_bench_generator_speculative_fallbacks(monkeypatch, knob):
+    # the canonical set is left in its speculative buckets for the rc stage (no gather); with the rc
+    # sort's final level exact (MTG_SPEC_RC=0) the compact array is gathered on demand, and
+    # MTG_DEFER_GATHER=0 is the always-gather path
+    monkeypatch.setenv(knob, "0")
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    got, _ = _gpu_build(30, asc, True, 0)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=True, bits_per_count=0)
+    _assert_same(got, want, "2M reads k=31 canonical, %s=0" % knob)
+
+
 @pytest.mark.parametrize("canonical", [False, True])
 def test_config0_k12_full_transcripts(transcripts_1000, canonical):
     for bits in (0, 8):
