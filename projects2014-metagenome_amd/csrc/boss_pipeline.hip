@@ -205,6 +205,12 @@ struct Ctx {
     bool defer_gather_req = false;  // set around the single build's canonical collect
     bool defer_gather = true;       // MTG_DEFER_GATHER=0: the speculative level always gathers
     bool spec_rc = true;            // MTG_SPEC_RC=0: the rc sort's final level exact (tests the fallbacks)
+    unsigned min_levels = 0;        // MTG_MSD_LEVELS=n: plan at least n MSD levels (tests the 3-level path)
+    // MTG_SPEC3=1: the speculative final level also for 3-level plans (off: its 1/8-tile sample sizes the
+    // level-3 buckets of level-2 buckets only a few tiles long badly, and at 20 M reads every step
+    // overflowed into the exact level -- sort 30.3 -> 38.9 ms; a sample of every tile's first slice
+    // would fix it)
+    bool spec3 = false;
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
@@ -232,6 +238,8 @@ static void load_knobs(Ctx &c) {
     c.spec_final = !is("MTG_SPEC", "0");
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
+    c.spec3 = is("MTG_SPEC3", "1");
+    if (const char *v = getenv("MTG_MSD_LEVELS")) c.min_levels = (unsigned)std::min(3, std::max(0, atoi(v)));
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
     c.force_spill = is("MTG_SPILL", "1");
@@ -430,6 +438,7 @@ static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
         ++T;
     MsdPlan p{};
     p.levels = (T + dmax - 1) / dmax;
+    if (c.min_levels > p.levels && T >= c.min_levels) p.levels = c.min_levels;  // (tests: MTG_MSD_LEVELS)
     for (unsigned l = 1; l <= p.levels; ++l) p.digit_end[l] = T * l / p.levels;
     return p;
 }
@@ -797,9 +806,10 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         b = T;
     } else {
         for (unsigned lev = 1; lev <= levels; ++lev) {
-            if (lev == levels && lev == 2 && (level1_done || (rm && distinct))) {  // level 1 is in place
-                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[1], digit_end[2], cmax,
-                                                                distinct, rm, saved_gidx);
+            // the last of 2 or 3 levels, the ones before it in place (3 levels: inputs over ~1.6e9 keys)
+            if (lev == levels && lev >= 2 && (lev == 2 || c.spec3) && (level1_done || (rm && distinct))) {
+                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[lev - 1], digit_end[lev],
+                                                                cmax, distinct, rm, saved_gidx);
                 if (u != ~0ull) return u;
             }
             run_level(lev);

@@ -76,6 +76,20 @@ def test_bench_generator_speculative_fallbacks(monkeypatch, knob):
 
 
 @pytest.mark.parametrize("canonical", [False, True])
+def test_bench_generator_three_msd_levels(monkeypatch, canonical):
+    # a 3-level MSD plan (inputs over ~1.6e9 keys plan one at configs[1]'s bucket size) forced on 2 M
+    # reads: levels 1-2 exact, the speculative final level 3 (and the rc sort's, fused with the merge),
+    # or its fallback to the exact level when a bucket overflows
+    monkeypatch.setenv("MTG_MSD_LEVELS", "3")
+    monkeypatch.setenv("MTG_SPEC3", "1")
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    got, _ = _gpu_build(30, asc, canonical, 0)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=0)
+    _assert_same(got, want, "2M reads k=31 canonical=%s, 3 MSD levels" % canonical)
+
+
+@pytest.mark.parametrize("canonical", [False, True])
 def test_config0_k12_full_transcripts(transcripts_1000, canonical):
     for bits in (0, 8):
         ctor = boss.IBOSSChunkConstructor.initialize(11, both_strands=canonical, bits_per_count=bits)
