@@ -206,11 +206,11 @@ struct Ctx {
     bool defer_gather = true;       // MTG_DEFER_GATHER=0: the speculative level always gathers
     bool spec_rc = true;            // MTG_SPEC_RC=0: the rc sort's final level exact (tests the fallbacks)
     unsigned min_levels = 0;        // MTG_MSD_LEVELS=n: plan at least n MSD levels (tests the 3-level path)
-    // MTG_SPEC3=1: the speculative final level also for 3-level plans (off: its 1/8-tile sample sizes the
-    // level-3 buckets of level-2 buckets only a few tiles long badly, and at 20 M reads every step
-    // overflowed into the exact level -- sort 30.3 -> 38.9 ms; a sample of every tile's first slice
-    // would fix it)
-    bool spec3 = false;
+    // MTG_SPEC3=0: the speculative final level only for 2-level plans.  (Sampled every 8th tile, the
+    // level-3 buckets of level-2 buckets only a few tiles long were sized badly: at 20 M reads every
+    // step overflowed into the exact level, sort 30.3 -> 38.9 ms; level 3 now samples every tile's
+    // first eighth.)
+    bool spec3 = true;
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
@@ -238,7 +238,7 @@ static void load_knobs(Ctx &c) {
     c.spec_final = !is("MTG_SPEC", "0");
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
-    c.spec3 = is("MTG_SPEC3", "1");
+    c.spec3 = !is("MTG_SPEC3", "0");
     if (const char *v = getenv("MTG_MSD_LEVELS")) c.min_levels = (unsigned)std::min(3, std::max(0, atoi(v)));
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
@@ -496,7 +496,8 @@ static void ensure_compact(Ctx &c) {
 // canonical sort's bucket index) and the rc keys the buckets before it received.
 template <int L, bool COUNTED>
 static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbits, unsigned bp, unsigned bb,
-                                 uint32_t cmax, bool distinct, RcMerge<L> *rm, const Ctx::GroupIndex &cidx) {
+                                 uint32_t cmax, bool distinct, RcMerge<L> *rm, const Ctx::GroupIndex &cidx,
+                                 bool fine = false) {
     if constexpr (L != 1 || COUNTED) {
         return ~0ull;
     } else {
@@ -520,8 +521,10 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         }
         uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nb * 4);
         HIP_CHECK(hipMemsetAsync(h, 0, nb * 4, c.stream));
-        msd_hist_kernel<L><<<dim3((unsigned)ceil_div(tiles, SS)), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb,
-                                                                                                  bp, h, SS);
+        // 2 levels: every 8th tile (level-1 buckets span hundreds of tiles); 3 levels: the first 1/8 of every
+        // tile (level-2 buckets can be only a few tiles long, and a tile-granular sample missed them)
+        msd_hist_kernel<L><<<dim3((unsigned)(fine ? tiles : ceil_div(tiles, SS))), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, n, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1);
         HIP_CHECK(hipGetLastError());
         uint32_t *cap = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
         spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap);
@@ -809,7 +812,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             // the last of 2 or 3 levels, the ones before it in place (3 levels: inputs over ~1.6e9 keys)
             if (lev == levels && lev >= 2 && (lev == 2 || c.spec3) && (level1_done || (rm && distinct))) {
                 const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[lev - 1], digit_end[lev],
-                                                                cmax, distinct, rm, saved_gidx);
+                                                                cmax, distinct, rm, saved_gidx, lev >= 3);
                 if (u != ~0ull) return u;
             }
             run_level(lev);

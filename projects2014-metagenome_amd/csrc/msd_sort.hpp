@@ -48,9 +48,10 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
                                                              uint64_t n, unsigned nbits,
                                                              unsigned b, unsigned bp,
                                                              uint32_t *__restrict__ counts,
-                                                             uint32_t tstride = 1) {
+                                                             uint32_t tstride = 1, uint32_t slice = 1) {
     // tstride > 1: a sample -- workgroup i counts tile i * tstride (msd_sort_unique's speculative
-    // final level sizes its buckets from it)
+    // final level sizes its buckets from it); slice > 1: a finer sample -- workgroup i counts the
+    // first 1/slice of tile i (previous-level buckets only a few tiles long are still sampled evenly)
     constexpr int TILE = MsdTraits<L>::TILE;
     constexpr int WMAX = MSD_WIN << 8;
     __shared__ uint32_t s_cnt[WMAX];
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
     for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
     const uint32_t wbase = key_prefix(keys[base], nbits, bp) << sub;
     __syncthreads();
-    const uint64_t end = min(n, base + TILE);
+    const uint64_t end = min(n, base + TILE / slice);
     auto add = [&](const Key<L> &key) {
         const uint32_t bucket = key_prefix(key, nbits, b);
         const uint32_t lb = bucket - wbase;
