@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--parity-full-max", type=int, default=10_000_000,
                     help="largest read count whose whole workload the bench checks against the oracle")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check on the CPU: every rank joins a gloo group and rank 0 prints the "
+                         "world it saw (no GPU, no build)")
     args = ap.parse_args()
     if args.config:
         given = {a.split("=")[0].lstrip("-").replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
@@ -409,14 +412,84 @@ def job_throughput(kmers_per_rank, world, steps, elapsed):
     return kmers_per_rank * world * steps / elapsed
 
 
-def main():
-    args = parse()
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv=None, timeout=None):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of this script, one
+    per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, before this process
+    makes any GPU call (the parent never imports torch).  Rank 0's stdout is the bench line; the
+    parent waits for all ranks and returns non-zero if any rank failed (the others are stopped)."""
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    t0 = time.time()
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                sys.stderr.write("bench.py: rank %d exited with %d; stopping the others\n"
+                                 % (procs.index(p), code))
+                for q in pending:
+                    q.terminate()
+        if timeout is not None and time.time() - t0 > timeout and pending:
+            for q in pending:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """The launcher's CPU check: a gloo group of `world` ranks; rank 0 prints what every rank saw."""
     import torch
     import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    seen = [(rank, world)]
+    if world > 1:
+        seen = [None] * world
+        dist.all_gather_object(seen, (rank, world))
+    elapsed = max_over_ranks(0.001 * (rank + 1), world, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": seen, "max_elapsed_s": elapsed}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%d (one rank per GPU)\n" % (args.gpus, world))
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -574,6 +647,7 @@ def main():
         import shutil
         del dreads
         shutil.rmtree(kmc_dir, ignore_errors=True)
+    assert result["n_gpus"] == args.gpus, (result["n_gpus"], args.gpus)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 3
+#define MTG_BOSS_ABI_VERSION 4
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -140,6 +140,9 @@ typedef struct mtg_boss_timings {
     uint64_t peak_bytes;         /* device workspace held at the end of the build */
     double input_ms;             /* host-buffer builds: KMC decode + FASTA split on the device (incl. their copies) */
     uint64_t spilled_bytes;      /* bytes the build kept outside HBM (the disk container's spill; 0 = none) */
+    uint64_t spec_levels;        /* speculative final MSD levels that completed (sample-sized buckets) */
+    uint64_t spec_fine_levels;   /* of those, levels sampled per tile (the final level of 3-level plans) */
+    uint64_t spec_fallbacks;     /* speculative levels that overflowed and reran as the exact level */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);

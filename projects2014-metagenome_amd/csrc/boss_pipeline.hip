@@ -213,6 +213,8 @@ struct Ctx {
     bool spec3 = true;
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
+    bool spec_tiny = false;  // MTG_SPEC_CAPS=tiny: speculative buckets without slack (tests force the
+                             // overflow fallback with it)
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
     const void *bidx_keys = nullptr;
     uint64_t bidx_n = 0;
@@ -239,6 +241,7 @@ static void load_knobs(Ctx &c) {
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
+    c.spec_tiny = is("MTG_SPEC_CAPS", "tiny");
     if (const char *v = getenv("MTG_MSD_LEVELS")) c.min_levels = (unsigned)std::min(3, std::max(0, atoi(v)));
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
@@ -461,9 +464,10 @@ struct RcMerge {
 // bucket capacities of the speculative final level: the sampled count scaled up, 20 % + 512 keys
 // of slack (a bucket of ~4600 keys overflows with probability ~1e-10 at a 1/8 sample)
 __global__ void spec_caps_kernel(const uint32_t *__restrict__ sample, uint64_t nb, uint32_t stride,
-                                 uint32_t *__restrict__ cap) {
+                                 uint32_t *__restrict__ cap, bool tiny) {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) cap[b] = (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
+    if (b < nb) cap[b] = tiny ? (uint32_t)(((uint64_t)sample[b] * stride) / 2)
+                              : (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
 }
 
 // The final MSD level of the main sort (level 2 after the fused K1's level 1) without its exact
@@ -527,7 +531,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             *keys, n, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1);
         HIP_CHECK(hipGetLastError());
         uint32_t *cap = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
-        spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap);
+        spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap, c.spec_tiny);
         HIP_CHECK(hipGetLastError());
         uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nb + 1) * 8);
         {
@@ -540,6 +544,18 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             HIP_CHECK(hipGetLastError());
         }
         const uint64_t C = read_u64(c, (const unsigned long long *)(bstart + nb));
+        {  // the capacity is known now: both slack-sized buffers (one for the fused rc merge) must fit
+            size_t fr = 0, tot = 0;
+            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            const double need = (double)C * sizeof(Key<L>) * (rm ? 1.0 : 2.0);
+            const double have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
+                                (rm ? 0.0 : (double)c.ws.held_slot(Workspace::SPEC_B));
+            if (need > have) {
+                if (c.debug) fprintf(stderr, "[mtg debug] speculative level: capacity %lu does not fit, exact level\n",
+                                     (unsigned long)C);
+                return ~0ull;
+            }
+        }
         Key<L> *sa = (Key<L> *)c.ws.get(Workspace::SPEC_A, C * sizeof(Key<L>));
         auto *cur = (unsigned long long *)c.ws.get(Workspace::SPEC_CUR, nb * 8);
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nb * 8, hipMemcpyDeviceToDevice, c.stream));
@@ -562,6 +578,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         if (povf) {
             if (c.debug) fprintf(stderr, "[mtg debug] speculative level: a bucket overflowed, exact level\n");
             c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
+            ++c.timings.spec_fallbacks;
             return ~0ull;
         }
         if (rm) {  // the fused rc merge over the speculative buckets
@@ -614,9 +631,12 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             if (novf) {
                 if (c.debug) fprintf(stderr, "[mtg debug] speculative rc level: %u groups overflowed, exact level\n", novf);
                 c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
+                ++c.timings.spec_fallbacks;
                 return ~0ull;
             }
             rm->done = true;
+            ++c.timings.spec_levels;
+            if (fine) ++c.timings.spec_fine_levels;
             if (gapped) c.gap.valid = false;  // merged: the canonical set is not needed compact
             if (istart) {  // index end = the merged count
                 const uint64_t R = n + rm->nc;
@@ -651,6 +671,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         if (novf) {
             if (c.debug) fprintf(stderr, "[mtg debug] speculative level: %u groups overflowed, exact level\n", novf);
             c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
+            ++c.timings.spec_fallbacks;
             return ~0ull;
         }
         uint64_t *ustart = (uint64_t *)c.ws.get(Workspace::MSD_USTART, (nb + 1) * 8);
@@ -673,6 +694,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             HIP_CHECK(hipMemcpyAsync(gu + nb + 1, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
             const uint64_t u = read_u64(c, (const unsigned long long *)(ustart + nb));
             c.gap = Ctx::GappedSet{true, sb, *keys, u, nb, gb, gu};
+            ++c.timings.spec_levels;
+            if (fine) ++c.timings.spec_fine_levels;
             c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gu};
             if (c.debug)
                 fprintf(stderr, "[mtg debug] speculative level: n=%lu capacity=%lu (%.2fx) -> %lu distinct, left in buckets\n",
@@ -695,6 +718,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         }
         HIP_CHECK(hipStreamSynchronize(c.stream));
         if (index && !ibad) c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gi};
+        ++c.timings.spec_levels;
+        if (fine) ++c.timings.spec_fine_levels;
         if (c.debug)
             fprintf(stderr, "[mtg debug] speculative level: n=%lu capacity=%lu (%.2fx) -> %lu distinct\n",
                     (unsigned long)n, (unsigned long)C, (double)C / (double)n, (unsigned long)u);

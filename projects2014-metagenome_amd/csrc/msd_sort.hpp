@@ -50,8 +50,9 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
                                                              uint32_t *__restrict__ counts,
                                                              uint32_t tstride = 1, uint32_t slice = 1) {
     // tstride > 1: a sample -- workgroup i counts tile i * tstride (msd_sort_unique's speculative
-    // final level sizes its buckets from it); slice > 1: a finer sample -- workgroup i counts the
-    // first 1/slice of tile i (previous-level buckets only a few tiles long are still sampled evenly)
+    // final level sizes its buckets from it); slice > 1: a finer sample -- workgroup i counts 1/slice
+    // of tile i, one line of every 8 * slice keys (previous-level buckets only a few tiles long, or
+    // a fraction of one, are still sampled evenly)
     constexpr int TILE = MsdTraits<L>::TILE;
     constexpr int WMAX = MSD_WIN << 8;
     __shared__ uint32_t s_cnt[WMAX];
@@ -68,7 +69,24 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
         if (lb < wsize) atomicAdd(&s_cnt[lb], 1u);
         else atomicAdd(&counts[bucket], 1u);
     };
-    if constexpr (L == 1) {  // 16-byte loads: two keys per lane
+    if constexpr (L == 1) {
+      if (slice > 1) {
+        // the finer sample spread over the whole tile: the first 64-byte line (8 keys) of every
+        // 8 * slice keys, four lanes per line (a contiguous 1/slice prefix would miss previous-level
+        // buckets that start late in the tile)
+        const uint64_t tend = min(n, base + TILE);
+        const uint32_t lines = TILE / (8 * slice);
+        for (uint32_t j = threadIdx.x; j < 4 * lines; j += MSD_BLOCK) {
+            const uint64_t i = base + (uint64_t)(j >> 2) * (8 * slice) + 2 * (j & 3);
+            if (i + 1 < tend) {
+                const ulonglong2 v = *(const ulonglong2 *)(keys + i);
+                add(Key<L>::from(v.x));
+                add(Key<L>::from(v.y));
+            } else if (i < tend) {
+                add(keys[i]);
+            }
+        }
+      } else {  // 16-byte loads: two keys per lane
         for (uint64_t i = base + 2 * threadIdx.x; i < end; i += 2 * MSD_BLOCK) {
             if (i + 1 < end) {
                 const ulonglong2 v = *(const ulonglong2 *)(keys + i);
@@ -78,6 +96,7 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
                 add(keys[i]);
             }
         }
+      }
     } else {
         for (uint64_t i = base + threadIdx.x; i < end; i += MSD_BLOCK) add(keys[i]);
     }

@@ -22,6 +22,5 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def transcripts_1000():
-    import importlib
-    seq_io = importlib.import_module("projects2014-metagenome_amd.seq_io")
+    import seq_io  # tests/seq_io.py: the test-side FASTA reader
     return seq_io.read_sequences(os.path.join(GOLDEN, "transcripts_1000.fa"))

@@ -155,3 +155,47 @@ def test_host_staged_exchange_functions_gloo():
             n = 0 if (i == 1 and r == 1) else r + 1 + i
             want += [16 * i + r] * n
         assert a == want
+
+
+# ---- bench.py --gpus N as the driver runs it (no launcher): the script starts its own ranks
+
+import json  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+_BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+
+
+def _clean_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch_world(n):
+    # python3 bench.py --gpus N starts N child ranks; rank 0's line reports n_gpus == N and every
+    # rank saw the same world
+    out = subprocess.run([sys.executable, _BENCH, "--gpus", str(n), "--dry-run"], env=_clean_env(),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == n
+    assert sorted(tuple(r) for r in line["ranks"]) == [(r, n) for r in range(n)]
+
+
+def test_bench_world_mismatch_fails():
+    # under a launcher, WORLD_SIZE must equal --gpus
+    env = dict(_clean_env(), WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, _BENCH, "--gpus", "4", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_bench_launcher_propagates_rank_failure():
+    # a rank that fails makes the whole launch fail (the launcher exits non-zero)
+    rc = bench.launch_ranks(2, ["--gpus", "2", "--dry-run", "--steps", "-x"], timeout=120)
+    assert rc != 0

@@ -132,8 +132,9 @@ def test_dist_empty_and_lopsided_ranks():
 
 
 def test_dist_large_multi_tile():
+    # (8, True) is configs[3]'s shape: canonical, BOSS k = 30 (k = 31), the default routed collect on 8 ranks
     reads = _random_reads(77, 30000, 150, 400000, n_rate=0.0005)
-    for P, canonical in ((2, True), (4, True), (8, False)):
+    for P, canonical in ((2, True), (4, True), (8, False), (8, True)):
         check_dist(30, reads, P, canonical, bits=8)
 
 
@@ -222,5 +223,5 @@ def test_dist_rounds_planned_from_memory_budget():
 def test_dist_rounds_large_multi_tile(monkeypatch):
     monkeypatch.setenv("MTG_RANGES", "3")
     reads = _random_reads(78, 30000, 150, 400000, n_rate=0.0005)
-    for P, canonical in ((2, True), (4, False)):
+    for P, canonical in ((2, True), (4, False), (8, True)):
         check_dist(30, reads, P, canonical, bits=8)

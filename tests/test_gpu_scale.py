@@ -57,6 +57,8 @@ def test_bench_generator_2m_reads_k31(canonical, bits):
     got, t = _gpu_build(30, asc, canonical, bits)
     assert t.n_extracted == 2_000_000 * 120
     assert t.radix_launches >= 1, "the multi-level MSD plan did not run"
+    if not bits:  # the uncounted build's main sort (and rc sort) take the speculative final level
+        assert t.spec_levels >= (2 if canonical else 1) and t.spec_fallbacks == 0, (t.spec_levels, t.spec_fallbacks)
     reads = [asc[i].tobytes() for i in range(len(asc))]
     want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=bits)
     _assert_same(got, want, "2M reads k=31 canonical=%s bits=%d" % (canonical, bits))
@@ -75,18 +77,38 @@ def test_bench_generator_speculative_fallbacks(monkeypatch, knob):
     _assert_same(got, want, "2M reads k=31 canonical, %s=0" % knob)
 
 
+@pytest.mark.parametrize("spec3", ["0", "1"])
 @pytest.mark.parametrize("canonical", [False, True])
-def test_bench_generator_three_msd_levels(monkeypatch, canonical):
+def test_bench_generator_three_msd_levels(monkeypatch, canonical, spec3):
     # a 3-level MSD plan (inputs over ~1.6e9 keys plan one at configs[1]'s bucket size) forced on 2 M
-    # reads: levels 1-2 exact, the speculative final level 3 (and the rc sort's, fused with the merge),
-    # or its fallback to the exact level when a bucket overflows
+    # reads: levels 1-2 exact, then the final level 3 either speculative (MTG_SPEC3=1: buckets sized
+    # from a per-tile sample; the rc sort's fused with the merge) or exact (MTG_SPEC3=0)
     monkeypatch.setenv("MTG_MSD_LEVELS", "3")
-    monkeypatch.setenv("MTG_SPEC3", "1")
+    monkeypatch.setenv("MTG_SPEC3", spec3)
     asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
-    got, _ = _gpu_build(30, asc, canonical, 0)
+    got, t = _gpu_build(30, asc, canonical, 0)
+    if spec3 == "1":  # the speculative level 3 ran and completed (no overflow fallback)
+        assert t.spec_fine_levels >= 1 and t.spec_fallbacks == 0, (t.spec_levels, t.spec_fine_levels,
+                                                                    t.spec_fallbacks)
+    else:
+        assert t.spec_fine_levels == 0
     reads = [asc[i].tobytes() for i in range(len(asc))]
     want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=0)
-    _assert_same(got, want, "2M reads k=31 canonical=%s, 3 MSD levels" % canonical)
+    _assert_same(got, want, "2M reads k=31 canonical=%s, 3 MSD levels, MTG_SPEC3=%s" % (canonical, spec3))
+
+
+@pytest.mark.parametrize("levels", ["2", "3"])
+def test_bench_generator_speculative_overflow(monkeypatch, levels):
+    # speculative buckets without slack (MTG_SPEC_CAPS=tiny) overflow: every speculative level falls
+    # back to the exact one after its partition ran, and the result is still the oracle's
+    monkeypatch.setenv("MTG_SPEC_CAPS", "tiny")
+    monkeypatch.setenv("MTG_MSD_LEVELS", levels)
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    got, t = _gpu_build(30, asc, True, 0)
+    assert t.spec_fallbacks >= 1 and t.spec_levels == 0, (t.spec_levels, t.spec_fallbacks)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=True, bits_per_count=0)
+    _assert_same(got, want, "2M reads k=31 canonical, tiny speculative buckets, %s levels" % levels)
 
 
 @pytest.mark.parametrize("canonical", [False, True])
