@@ -288,13 +288,19 @@ int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64
  * build_boss_from_chunks takes none), <outbase>.dbg.weights when the chunk has
  * weights (node_weights.cpp:62-68).  graph_mode: 0 basic, 1 canonical.  suffix_length < 0 = the
  * build's default min(10, k).  *n_valid (may be NULL) = edges left valid by the mask (`nodes (k)` of
- * `metagraph stats`), else n - 1.  Host code: needs no device.  The sdsl-lite containers inside are
- * restated (their bytes are unpinned); mtg_boss_read_dbg reads exactly this layout, and a
- * reference `metagraph` binary must NOT be given these files (it would pass the framing checks and
- * misread W and last).
+ * `metagraph stats`), else n - 1.  Host code: needs no device.  The sdsl-lite containers inside
+ * (wt_huff<> for W, bit_vector_stat for last, bit_vector_small for the mask, int_vector<> for the
+ * weights) are written field by field as sdsl-lite 2.x serializes them (csrc/sdsl_io.hpp, DESIGN.md
+ * §9); no reference-written file exists to pin their bytes.
  */
 int mtg_boss_write_dbg(const mtg_boss_chunk *chunk, const char *outbase, int graph_mode, int mask_dummy,
                        int64_t suffix_length, uint64_t *n_valid);
+
+/* One sdsl-lite container of the graph files written alone to `path` (the layout tests): kind 0
+ * bit_vector_stat over `nbits` bits of `data`, 1 bit_vector_small (sd_vector or rrr_vector<63>,
+ * whichever predict_size picks), 2 wt_huff<> over `nbits` bytes of `data`, 3 the sd_vector<> of the
+ * set bits, 4 rrr_vector<63>. */
+int mtg_sdsl_write(const char *path, int kind, const void *data, uint64_t nbits);
 
 typedef struct mtg_dbg_file {
     uint64_t k;

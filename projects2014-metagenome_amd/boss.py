@@ -102,7 +102,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
            "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
-           "mtg_boss_write_dbg", "mtg_boss_read_dbg", "mtg_dbg_file_free",
+           "mtg_boss_write_dbg", "mtg_sdsl_write", "mtg_boss_read_dbg", "mtg_dbg_file_free",
            "mtg_boss_ctor_add_fasta", "mtg_device_copy", "mtg_kmc_load_device",
            "mtg_device_reads_free", "mtg_kmc_write_device", "mtg_host_pool_bytes",
            "mtg_host_pool_trim", "mtg_comm_create_callbacks", "mtg_comm_local_held_ms")
@@ -174,6 +174,7 @@ def lib():
         L.mtg_boss_write_dbg.argtypes = [P(_Chunk), ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int64, P(ctypes.c_uint64)]
         L.mtg_boss_read_dbg.argtypes = [ctypes.c_char_p, P(_DbgFile)]
+        L.mtg_sdsl_write.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
         L.mtg_kmc_load_device.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                                           ctypes.c_int, P(_DeviceReads)]
         L.mtg_device_reads_free.argtypes = [P(_DeviceReads)]

@@ -4469,6 +4469,36 @@ int mtg_boss_write_dbg(const mtg_boss_chunk *chunk, const char *outbase, int gra
     }
 }
 
+int mtg_sdsl_write(const char *path, int kind, const void *data, uint64_t nbits) {
+    if (!path || (!data && nbits) || kind < 0 || kind > 4) {
+        set_error("sdsl_write: bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    try {
+        std::ofstream o(path, std::ios::binary);
+        if (!o.good()) throw std::runtime_error(std::string("Can't write to file ") + path);
+        const uint64_t *w = (const uint64_t *)data;
+        std::vector<uint64_t> zero(1, 0);
+        if (!nbits) w = zero.data();
+        if (kind == 0) sdslio::put_bit_vector_stat(o, w, nbits);
+        else if (kind == 1) sdslio::put_bit_vector_small(o, w, nbits);
+        else if (kind == 2) sdslio::put_wt_huff(o, (const uint8_t *)data, nbits);
+        else if (kind == 3) {
+            std::vector<uint64_t> pos;
+            for (uint64_t i = 0; i < nbits; ++i)
+                if (sdslio::bit(w, i)) pos.push_back(i);
+            sdslio::put_sd_vector(o, pos, nbits);
+        } else {
+            sdslio::put_rrr_vector(o, w, nbits);
+        }
+        if (!o.good()) throw std::runtime_error(std::string("Can't write to file ") + path);
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_ARGUMENT;
+    }
+}
+
 int mtg_boss_read_dbg(const char *outbase, mtg_dbg_file *out) {
     if (!outbase || !out) return MTG_ERR_ARGUMENT;
     std::memset(out, 0, sizeof(*out));

@@ -9,15 +9,14 @@
 // The BOSS navigation the index and the mask need (rank_W, rank_last, select_last, fwd,
 // tighten_range: boss.hpp:655-666, boss.cpp:381-385, 521-536, 586-597) runs on the chunk arrays.
 //
-// Byte layout.  The reference's own framing is exact: numbers are serialize_number (8-byte
-// big-endian, common/serialization.cpp:38-46), F is serialize_number_vector_raw (count + values,
-// :84-90), the suffix index is a raw native-endian pair<u64,u64> array.  The sdsl-lite containers
-// (wt_huff<> for W, bit_vector_stat = bit_vector + rank_support_v5 + select_support_mcl +
-// select_support_scan for last, bit_vector_small for the mask) are RESTATED, not reproduced:
-// sdsl-lite is an empty submodule in the reference snapshot and no .dbg file exists in its tests,
-// so their bytes are unpinned.  The restatement keeps sdsl's int_vector framing (u64 size in bits,
-// u8 width for width-0 vectors, u64 words) for every bit/int vector and writes each auxiliary
-// structure as documented below; read_dbg parses exactly this layout back.
+// Byte layout.  The reference's own framing: numbers are serialize_number (8-byte big-endian,
+// common/serialization.cpp:38-46), F is serialize_number_vector_raw (count + values, :84-90), the
+// suffix index is a raw native-endian pair<u64,u64> array.  The sdsl-lite containers (wt_huff<> for
+// W, bit_vector_stat for last, bit_vector_small for the mask, int_vector<> for the weights) are
+// written field by field as sdsl-lite 2.x serializes them (sdsl_io.hpp).  sdsl-lite is an empty
+// submodule of the reference snapshot and no .dbg file exists in its tests, so the bytes are a
+// restatement of the library's published layout, unpinned by a golden file; read_dbg parses the
+// same layout back and checks the rank supports it can recompute.
 #pragma once
 
 #include <stdint.h>
@@ -31,290 +30,18 @@
 #include <utility>
 #include <vector>
 
+#include "sdsl_io.hpp"
+
 namespace mtg {
 namespace dbgio {
 
 // ---------------------------------------------------------------------------------- framing
 
-inline void put_be(std::ostream &o, uint64_t v) {  // serialize_number
-    uint8_t b[8];
-    for (int i = 0; i < 8; ++i) b[i] = (uint8_t)(v >> (56 - 8 * i));
-    o.write((const char *)b, 8);
-}
-inline uint64_t get_be(std::istream &in) {
-    uint8_t b[8];
-    if (!in.read((char *)b, 8)) throw std::runtime_error("truncated .dbg file");
-    uint64_t v = 0;
-    for (int i = 0; i < 8; ++i) v = v << 8 | b[i];
-    return v;
-}
-template <typename T>
-inline void put_raw(std::ostream &o, const T &v) { o.write((const char *)&v, sizeof(T)); }
-template <typename T>
-inline T get_raw(std::istream &in) {
-    T v;
-    if (!in.read((char *)&v, sizeof(T))) throw std::runtime_error("truncated .dbg file");
-    return v;
-}
-
-// sdsl int_vector framing: u64 size in bits, [u8 width when the width is a run-time value], then
-// ceil(bits / 64) u64 words
-inline void put_bits(std::ostream &o, const std::vector<uint64_t> &words, uint64_t nbits, int width = -1) {
-    put_raw<uint64_t>(o, nbits);
-    if (width >= 0) put_raw<uint8_t>(o, (uint8_t)width);
-    o.write((const char *)words.data(), (std::streamsize)(((nbits + 63) / 64) * 8));
-}
-inline std::vector<uint64_t> get_bits(std::istream &in, uint64_t *nbits, bool has_width = false, int *width = nullptr) {
-    *nbits = get_raw<uint64_t>(in);
-    if (has_width) {
-        const uint8_t w = get_raw<uint8_t>(in);
-        if (width) *width = w;
-    }
-    std::vector<uint64_t> words((*nbits + 63) / 64);
-    if (!words.empty() && !in.read((char *)words.data(), (std::streamsize)(words.size() * 8)))
-        throw std::runtime_error("truncated .dbg file");
-    return words;
-}
-inline void put_u64s(std::ostream &o, const std::vector<uint64_t> &v) {  // int_vector<64>
-    put_bits(o, v, 64 * (uint64_t)v.size());
-}
-inline std::vector<uint64_t> get_u64s(std::istream &in) {
-    uint64_t nb;
-    return get_bits(in, &nb);
-}
-
-inline bool bit(const uint64_t *w, uint64_t i) { return (w[i >> 6] >> (i & 63)) & 1; }
-
-// ---------------------------------------------------------------- rank / select supports
-
-// cumulative ones before every 2048-bit superblock (rank_support_v5's block size), plus the end
-struct RankSupport {
-    std::vector<uint64_t> super;
-    void build(const uint64_t *w, uint64_t nbits) {
-        const uint64_t nw = (nbits + 63) / 64;
-        super.assign(nw / 32 + 2, 0);
-        uint64_t c = 0;
-        for (uint64_t i = 0; i < nw; ++i) {
-            if (i % 32 == 0) super[i / 32] = c;
-            c += __builtin_popcountll(w[i]);
-        }
-        super[nw / 32 + 1] = c;
-        if (nw % 32 == 0) super[nw / 32] = c;
-    }
-};
-
-// position of every 4096-th one (select_support_mcl's superblock sampling), as int_vector<64>
-inline std::vector<uint64_t> select_samples(const uint64_t *w, uint64_t nbits, bool ones) {
-    std::vector<uint64_t> s;
-    uint64_t c = 0;
-    for (uint64_t i = 0; i < nbits; ++i) {
-        if (bit(w, i) == ones) {
-            if (c % 4096 == 0) s.push_back(i);
-            ++c;
-        }
-    }
-    return s;
-}
-
-// bit_vector_stat (bit_vector_sdsl.hpp:270-277): bit_vector, num_set_bits (BE), then the
-// restated supports: rank (int_vector<64> superblock counts), select-1 (u64 count + int_vector<64>
-// samples); select_support_scan<0> stores nothing
-inline void put_bit_vector_stat(std::ostream &o, const std::vector<uint64_t> &w, uint64_t nbits) {
-    put_bits(o, w, nbits);
-    uint64_t ones = 0;
-    for (uint64_t x : w) ones += __builtin_popcountll(x);
-    put_be(o, ones);
-    RankSupport r;
-    r.build(w.data(), nbits);
-    put_u64s(o, r.super);
-    put_raw<uint64_t>(o, ones);
-    put_u64s(o, select_samples(w.data(), nbits, true));
-}
-inline std::vector<uint64_t> get_bit_vector_stat(std::istream &in, uint64_t *nbits) {
-    std::vector<uint64_t> w = get_bits(in, nbits);
-    const uint64_t ones = get_be(in);
-    uint64_t c = 0;
-    for (uint64_t x : w) c += __builtin_popcountll(x);
-    if (c != ones) throw std::runtime_error("bit_vector_stat: set-bit count mismatch");
-    get_u64s(in);
-    if (get_raw<uint64_t>(in) != ones) throw std::runtime_error("bit_vector_stat: select support mismatch");
-    get_u64s(in);
-    return w;
-}
-
-// --------------------------------------------------------------------------- W: wt_huff<>
-
-// Huffman-shaped wavelet tree over the W symbols (sdsl wt_pc<huff_shape>): node 0 the root, nodes
-// numbered breadth first; the concatenated bit vector holds each inner node's bits (0 = left
-// child) in node order, each in text order.  Layout: u64 size, u64 sigma, bit_vector, rank
-// support (as above), select-1 and select-0 supports (u64 count + int_vector<64> samples each),
-// then the tree: u64 node count, per node (u64 bv_pos, u64 bv_pos_rank, u16 parent, u16 child[2],
-// 0xFFFF = none), u16 symbol -> leaf[256], u64 symbol -> path[256] (code length << 56 | code bits,
-// root bit first).  Followed by the BE logsigma of wavelet_tree_sdsl (wavelet_tree.cpp:365-368).
-struct HuffTree {
-    struct Node {
-        uint64_t bv_pos = 0, bv_pos_rank = 0, count = 0;
-        uint16_t parent = 0xFFFF, child[2] = {0xFFFF, 0xFFFF};
-        int symbol = -1;
-    };
-    std::vector<Node> nodes;
-    uint16_t leaf[256];
-    uint64_t path[256];
-};
-
-inline HuffTree huff_build(const uint64_t freq[256]) {
-    // deterministic Huffman: repeatedly join the two lightest trees (ties: smaller id first)
-    struct T {
-        uint64_t f;
-        int id;
-    };
-    auto cmp = [](const T &a, const T &b) { return a.f != b.f ? a.f > b.f : a.id > b.id; };
-    std::priority_queue<T, std::vector<T>, decltype(cmp)> pq(cmp);
-    std::vector<std::pair<int, int>> kids;  // tree id >= 256: (left, right)
-    std::vector<uint64_t> tf;
-    for (int s = 0; s < 256; ++s)
-        if (freq[s]) pq.push({freq[s], s});
-    int next = 256;
-    while (pq.size() > 1) {
-        T a = pq.top();
-        pq.pop();
-        T b = pq.top();
-        pq.pop();
-        kids.push_back({a.id, b.id});
-        pq.push({a.f + b.f, next++});
-    }
-    HuffTree h;
-    std::fill(h.leaf, h.leaf + 256, (uint16_t)0xFFFF);
-    std::fill(h.path, h.path + 256, 0ull);
-    if (pq.empty()) return h;
-    // breadth-first numbering from the root
-    std::vector<std::pair<int, uint64_t>> q{{pq.top().id, 0}};  // (tree id, code << 8 | len)
-    std::vector<int> parent_of{-1};
-    for (size_t i = 0; i < q.size(); ++i) {
-        const int id = q[i].first;
-        HuffTree::Node n;
-        if (parent_of[i] >= 0) n.parent = (uint16_t)parent_of[i];
-        if (id < 256) {
-            n.symbol = id;
-            const uint64_t code = q[i].second >> 8, len = q[i].second & 0xFF;
-            h.leaf[id] = (uint16_t)i;
-            h.path[id] = len << 56 | code;
-        } else {
-            const auto &kv = kids[id - 256];
-            const uint64_t code = q[i].second >> 8, len = q[i].second & 0xFF;
-            for (int c = 0; c < 2; ++c) {
-                n.child[c] = (uint16_t)q.size();
-                q.push_back({c ? kv.second : kv.first, ((code | (uint64_t)c << len) << 8) | (len + 1)});
-                parent_of.push_back((int)i);
-            }
-        }
-        h.nodes.push_back(n);
-    }
-    if (h.nodes.size() == 1) {  // one symbol: a leaf root, no bits
-        h.path[h.nodes[0].symbol] = 0;
-    }
-    return h;
-}
-
-inline void put_wt_huff(std::ostream &o, const uint8_t *W, uint64_t n) {
-    uint64_t freq[256] = {0};
-    for (uint64_t i = 0; i < n; ++i) ++freq[W[i]];
-    HuffTree h = huff_build(freq);
-    uint64_t sigma = 0;
-    for (int s = 0; s < 256; ++s) sigma += freq[s] != 0;
-    // bits per inner node = symbols passing through it; positions in node order
-    for (int s = 0; s < 256; ++s) {
-        if (!freq[s]) continue;
-        for (int v = h.nodes[h.leaf[s]].parent; v != 0xFFFF; v = h.nodes[v].parent) h.nodes[v].count += freq[s];
-    }
-    uint64_t total = 0;
-    for (auto &v : h.nodes) {
-        v.bv_pos = total;
-        total += v.symbol < 0 ? v.count : 0;
-    }
-    std::vector<uint64_t> bv((total + 63) / 64, 0);
-    std::vector<uint64_t> cur(h.nodes.size(), 0);
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t p = h.path[W[i]], len = p >> 56;
-        uint16_t v = 0;
-        for (uint64_t d = 0; d < len; ++d) {
-            const uint64_t b = (p >> d) & 1, pos = h.nodes[v].bv_pos + cur[v]++;
-            if (b) bv[pos >> 6] |= 1ull << (pos & 63);
-            v = h.nodes[v].child[b];
-        }
-    }
-    RankSupport r;
-    r.build(bv.data(), total);
-    uint64_t ones = 0;
-    for (uint64_t x : bv) ones += __builtin_popcountll(x);
-    for (auto &v : h.nodes) {  // ones before each node's bits
-        const uint64_t w = v.bv_pos >> 6, b = v.bv_pos & 63;
-        uint64_t c = r.super[w / 32];
-        for (uint64_t q = w / 32 * 32; q < w; ++q) c += __builtin_popcountll(bv[q]);
-        if (b) c += __builtin_popcountll(bv[w] & ((1ull << b) - 1));
-        v.bv_pos_rank = c;
-    }
-    put_raw<uint64_t>(o, n);
-    put_raw<uint64_t>(o, sigma);
-    put_bits(o, bv, total);
-    put_u64s(o, r.super);
-    put_raw<uint64_t>(o, ones);
-    put_u64s(o, select_samples(bv.data(), total, true));
-    put_raw<uint64_t>(o, total - ones);
-    put_u64s(o, select_samples(bv.data(), total, false));
-    put_raw<uint64_t>(o, (uint64_t)h.nodes.size());
-    for (const auto &v : h.nodes) {
-        put_raw<uint64_t>(o, v.bv_pos);
-        put_raw<uint64_t>(o, v.bv_pos_rank);
-        put_raw<uint16_t>(o, v.parent);
-        put_raw<uint16_t>(o, v.child[0]);
-        put_raw<uint16_t>(o, v.child[1]);
-    }
-    o.write((const char *)h.leaf, sizeof(h.leaf));
-    o.write((const char *)h.path, sizeof(h.path));
-}
-
-inline std::vector<uint8_t> get_wt_huff(std::istream &in) {
-    const uint64_t n = get_raw<uint64_t>(in);
-    get_raw<uint64_t>(in);  // sigma
-    uint64_t total;
-    const std::vector<uint64_t> bv = get_bits(in, &total);
-    get_u64s(in);
-    get_raw<uint64_t>(in);
-    get_u64s(in);
-    get_raw<uint64_t>(in);
-    get_u64s(in);
-    const uint64_t nn = get_raw<uint64_t>(in);
-    if (nn > 511) throw std::runtime_error("wt_huff: bad tree");
-    std::vector<HuffTree::Node> nodes(nn);
-    for (auto &v : nodes) {
-        v.bv_pos = get_raw<uint64_t>(in);
-        v.bv_pos_rank = get_raw<uint64_t>(in);
-        v.parent = get_raw<uint16_t>(in);
-        v.child[0] = get_raw<uint16_t>(in);
-        v.child[1] = get_raw<uint16_t>(in);
-    }
-    uint16_t leaf[256];
-    uint64_t path[256];
-    if (!in.read((char *)leaf, sizeof(leaf)) || !in.read((char *)path, sizeof(path)))
-        throw std::runtime_error("truncated .dbg file");
-    std::vector<int> sym(nn, -1);
-    for (int s = 0; s < 256; ++s)
-        if (leaf[s] != 0xFFFF && leaf[s] < nn) sym[leaf[s]] = s;
-    std::vector<uint8_t> W(n);
-    std::vector<uint64_t> cur(nn, 0);
-    for (uint64_t i = 0; i < n; ++i) {  // walk root -> leaf with one cursor per inner node
-        uint16_t v = 0;
-        while (nn && nodes[v].child[0] != 0xFFFF) {
-            const uint64_t pos = nodes[v].bv_pos + cur[v]++;
-            if (pos >= total) throw std::runtime_error("wt_huff: bits out of range");
-            v = nodes[v].child[bit(bv.data(), pos)];
-        }
-        if (!nn || sym[v] < 0) throw std::runtime_error("wt_huff: leaf without symbol");
-        W[i] = (uint8_t)sym[v];
-    }
-    return W;
-}
+using sdslio::get_be;
+using sdslio::get_raw;
+using sdslio::put_be;
+using sdslio::put_raw;
+using sdslio::bit;
 
 // ----------------------------------------------------------------------- BOSS navigation
 
@@ -579,17 +306,6 @@ inline Pruned prune_dummy_edges(const BossNav &b) {
     return out;
 }
 
-// bit_vector_small (bit_vector_adaptive.hpp:319) restated as a type tag (BE 0 = the stat
-// representation) followed by bit_vector_stat
-inline void put_bit_vector_small(std::ostream &o, const std::vector<uint64_t> &w, uint64_t nbits) {
-    put_be(o, 0);
-    put_bit_vector_stat(o, w, nbits);
-}
-inline std::vector<uint64_t> get_bit_vector_small(std::istream &in, uint64_t *nbits) {
-    if (get_be(in) != 0) throw std::runtime_error("bit_vector_small: unknown representation");
-    return get_bit_vector_stat(in, nbits);
-}
-
 // ------------------------------------------------------------------------ the graph files
 
 constexpr uint64_t kStateStat = 3;  // BOSS::State::STAT (boss.hpp:325), the build's default state
@@ -643,10 +359,9 @@ inline uint64_t write_dbg_arrays(const std::string &base, const uint8_t *W, cons
         for (int c = 0; c < 5; ++c) put_be(o, F[c]);
         put_be(o, k);
         put_be(o, kStateStat);
-        put_wt_huff(o, W, n);
+        sdslio::put_wt_huff(o, W, n);
         put_be(o, 4);  // logsigma of W: bits_per_char_W_
-        const uint64_t nw = (n + 63) / 64;
-        put_bit_vector_stat(o, std::vector<uint64_t>(last, last + nw), n);
+        sdslio::put_bit_vector_stat(o, last, n);
         put_be(o, mode);
         const auto ranges = index_suffix_ranges(nav, L);
         put_be(o, L);
@@ -660,7 +375,7 @@ inline uint64_t write_dbg_arrays(const std::string &base, const uint8_t *W, cons
         n_valid = 0;
         for (uint64_t x : *valid) n_valid += __builtin_popcountll(x);
         std::ofstream o(base + ".edgemask", std::ios::binary);
-        put_bit_vector_small(o, *valid, n);
+        sdslio::put_bit_vector_small(o, valid->data(), n);
         if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".edgemask");
     }
     if (weights && bits_per_count) {  // the chunk's weights buffer renamed (node_weights.cpp:62-68)
@@ -673,7 +388,7 @@ inline uint64_t write_dbg_arrays(const std::string &base, const uint8_t *W, cons
             if (b + w > 64) words[q + 1] |= v >> (64 - b);
         }
         std::ofstream o(base + ".dbg.weights", std::ios::binary);
-        put_bits(o, words, n * w, (int)w);
+        sdslio::put_int_vector(o, words.data(), n * w, (uint8_t)w, false);
         if (!o.good()) throw std::runtime_error("Can't write to file " + base + ".dbg.weights");
     }
     return n_valid;
@@ -688,10 +403,10 @@ inline DbgFile read_dbg(const std::string &base) {
     f.k = get_be(in);
     f.state = get_be(in);
     if (f.state != kStateStat) throw std::runtime_error("only the STAT representation is written here");
-    f.W = get_wt_huff(in);
+    f.W = sdslio::get_wt_huff(in);
     if (get_be(in) != 4) throw std::runtime_error("ERROR: failed to load W vector");
     uint64_t nb;
-    f.last = get_bit_vector_stat(in, &nb);
+    f.last = sdslio::get_bit_vector_stat(in, &nb);
     if (nb != f.W.size()) throw std::runtime_error("ERROR: failed to load L vector");
     f.n = nb;
     f.mode = get_be(in);
@@ -708,7 +423,7 @@ inline DbgFile read_dbg(const std::string &base) {
     std::ifstream m(base + ".edgemask", std::ios::binary);
     if (m.good()) {
         uint64_t mb;
-        f.valid = get_bit_vector_small(m, &mb);
+        f.valid = sdslio::get_bit_vector_small(m, &mb);
         if (mb != f.n) throw std::runtime_error("edgemask size differs from the graph");
         f.has_mask = true;
     }

@@ -134,3 +134,99 @@ def test_gpu_chunk_to_dbg_goldens(tmp_path, transcripts_1000, canonical, nodes):
     f = boss.DbgFile(base)
     assert np.array_equal(f.W, want.W) and np.array_equal(f.last, want.last)
     assert np.array_equal(f.F, want.F) and f.n_valid == nodes
+
+
+# ---- the sdsl-lite layout, checked field by field by an independent reader (tests/sdsl_layout.py)
+
+import ctypes  # noqa: E402
+
+import sdsl_layout as S  # noqa: E402
+
+
+def _write(tmp_path, kind, data, nbits, name):
+    path = str(tmp_path / name)
+    buf = np.ascontiguousarray(data)
+    rc = boss.lib().mtg_sdsl_write(os.fsencode(path), kind, buf.ctypes.data_as(ctypes.c_void_p), nbits)
+    assert rc == 0, boss.lib().mtg_last_error()
+    return open(path, "rb").read()
+
+
+def _packed(bits):
+    words = np.zeros((len(bits) + 63) // 64 + 1, np.uint64)
+    if len(bits):
+        pb = np.packbits(np.asarray(bits, np.uint8), bitorder="little")
+        words.view(np.uint8)[:len(pb)] = pb
+    return words
+
+
+def _bit_cases():
+    rng = np.random.default_rng(5)
+    yield "one", np.array([1], np.uint8)
+    yield "zero", np.array([0], np.uint8)
+    for n in (63, 64, 65, 126, 511, 512, 513, 2047, 2048, 2049, 2016, 4032, 6000, 64 * 32 * 3):
+        yield "dense%d" % n, (rng.random(n) < 0.6).astype(np.uint8)
+    yield "words8", (rng.random(512 * 5) < 0.5).astype(np.uint8)
+    yield "mostly_ones", (rng.random(200000) < 0.97).astype(np.uint8)
+    yield "mostly_zeros", (rng.random(200000) < 0.02).astype(np.uint8)
+    sparse = np.zeros(3_000_000, np.uint8)  # superblocks of 4096 ones spanning > logn^4 bits (long form)
+    sparse[rng.choice(3_000_000, 9000, replace=False)] = 1
+    yield "long_superblocks", sparse
+    mixed = np.zeros(400000, np.uint8)  # one dense superblock, then sparse ones
+    mixed[:5000] = 1
+    mixed[rng.choice(np.arange(5000, 400000), 5000, replace=False)] = 1
+    yield "mixed", mixed
+    yield "all_ones_2016", np.ones(2016, np.uint8)
+
+
+@pytest.mark.parametrize("name,bits", list(_bit_cases()))
+def test_sdsl_bit_containers_layout(tmp_path, name, bits):
+    words = _packed(bits)
+    n = len(bits)
+    r = S.Reader(_write(tmp_path, 0, words, n, name + ".stat"))
+    assert np.array_equal(S.check_bit_vector_stat(r), bits) and r.done()
+    r = S.Reader(_write(tmp_path, 3, words, n, name + ".sd"))
+    S.check_sd_vector(r, np.flatnonzero(bits), n)
+    assert r.done()
+    r = S.Reader(_write(tmp_path, 4, words, n, name + ".rrr"))
+    S.check_rrr_vector(r, bits)
+    assert r.done()
+    r = S.Reader(_write(tmp_path, 1, words, n, name + ".small"))
+    S.check_bit_vector_small(r, bits)
+    assert r.done()
+
+
+@pytest.mark.parametrize("case", ["one_symbol", "two", "skewed", "boss_like", "all_256", "ties"])
+def test_sdsl_wt_huff_layout(tmp_path, case):
+    rng = np.random.default_rng(9)
+    if case == "one_symbol":
+        W = np.zeros(1, np.uint8)
+    elif case == "two":
+        W = np.array([0, 3, 3, 0, 3], np.uint8)
+    elif case == "skewed":
+        W = rng.choice(10, size=50000, p=[.01, .2, .3, .2, .19, .02, .02, .02, .02, .02]).astype(np.uint8)
+    elif case == "boss_like":
+        W = rng.integers(0, 10, size=100003).astype(np.uint8)
+    elif case == "all_256":
+        W = rng.integers(0, 256, size=70000).astype(np.uint8)
+    else:  # equal frequencies everywhere: the heap's (frequency, id) tie rule decides the shape
+        W = np.repeat(np.arange(7, dtype=np.uint8), 64)
+        rng.shuffle(W)
+    r = S.Reader(_write(tmp_path, 2, W, len(W), case + ".wt"))
+    S.check_wt_huff(r, W)
+    assert r.done()
+
+
+@pytest.mark.parametrize("k,canonical", [(3, False), (12, True), (19, False), (19, True)])
+def test_dbg_file_layout(tmp_path, transcripts_1000, k, canonical):
+    # the whole .dbg and .edgemask of real graphs, field by field
+    seqs = transcripts_1000 if k == 19 else CONSTRUCT_SEQS
+    ch = _chunk(k, seqs, canonical, 8)
+    base = str(tmp_path / "g")
+    ch.write_dbg(base, canonical=canonical, mask_dummy=True)
+    last = np.asarray(ch.last, np.uint8)
+    F, kk, state, mode, L = S.check_dbg(base + ".dbg", np.asarray(ch.W, np.uint8), last)
+    assert list(F) == [int(x) for x in ch.F] and kk == k and state == 3 and mode == int(canonical)
+    f = boss.DbgFile(base)
+    r = S.Reader(open(base + ".edgemask", "rb").read())
+    S.check_bit_vector_small(r, np.asarray(f.valid, np.uint8))
+    assert r.done()
