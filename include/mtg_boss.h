@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 4
+#define MTG_BOSS_ABI_VERSION 5
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -143,6 +143,8 @@ typedef struct mtg_boss_timings {
     uint64_t spec_levels;        /* speculative final MSD levels that completed (sample-sized buckets) */
     uint64_t spec_fine_levels;   /* of those, levels sampled per tile (the final level of 3-level plans) */
     uint64_t spec_fallbacks;     /* speculative levels that overflowed and reran as the exact level */
+    uint64_t collect_mode;       /* how the real k-mers were collected: 0 one pass, 1 key ranges re-scanning
+                                    the reads (both strands), 2 canonical rounds of the fused extraction */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);

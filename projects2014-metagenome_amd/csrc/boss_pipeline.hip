@@ -64,7 +64,8 @@ class Workspace {
         QFLAG, QTCNT, QTOFF, DSRC, DSEND, DRECV, RUN_IDX, RUN_DELTA, RUN_OFF, KMC_LUT, KMC_REC, DUP_TABLE, FUSED_HIST, FUSED_CUR, STRIPE_CUR,
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
-        SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, NSLOTS
+        SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
+        FUSED_SEL, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -88,6 +89,16 @@ class Workspace {
         return b.ptr;
     }
     void swap(Slot a, Slot b) { std::swap(bufs_[a], bufs_[b]); }
+    // frees a slot's buffer (batched builds drop their round buffers before the later stages grow)
+    void release(Slot s) {
+        Buf &b = bufs_[s];
+        if (b.ptr) {
+            HIP_CHECK(hipDeviceSynchronize());
+            (void)hipFree(b.ptr);
+        }
+        b.ptr = nullptr;
+        b.cap = 0;
+    }
     uint64_t held() const {
         uint64_t t = 0;
         for (const auto &b : bufs_) t += b.cap;
@@ -180,6 +191,9 @@ struct Ctx {
     bool routed_min = false;       // MTG_ROUTED_CANON=min: the routed collect keeps min(fwd, rc)
     int dist_collect = 1;          // MTG_DIST_COLLECT: 1 routed keys (default), 0 super-k-mers
                                    // (=superkmer), 2 local collect + exchange of sorted runs (=local)
+    bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
+                                   // that re-scan the reads (both strands) even where the canonical
+                                   // rounds of the fused K1 apply (collect_rounds_fused)
     bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
                                    // dense u64 ranks (dummy_encode_kernel)
     // bucket index of the last msd_sort_unique's output over its final bucket bits, when every group
@@ -237,6 +251,7 @@ static void load_knobs(Ctx &c) {
     c.fused = !is("MTG_FUSED", "0");
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
+    c.range_scan = is("MTG_COLLECT", "ranges");
     c.spec_final = !is("MTG_SPEC", "0");
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
@@ -1215,8 +1230,156 @@ static bool stage_extract_windows(Ctx &c, unsigned K, bool canonical, uint32_t c
 }
 
 // K1 fused with K2's first partition level (extract_partition.hpp), for 2-bit u64 keys on
-// inputs big enough to have one.  Returns false (nothing done) when it does not apply; else N,
-// the duplication estimate, and the level-1 counts in *hist1 (device) with *ka scattered.
+// inputs big enough to have one: pass A (fused_pass_a, the histogram of the top FUSED_HB bits of
+// every k-mer) then pass B (fused_pass_b, the k-mers scattered by their level-1 digit).
+struct FusedA {
+    uint64_t npos = 0, N = 0;
+    double dup = 8.0;
+    uint32_t nrows = 0, rps = 0, stripes = 0;
+    uint64_t per_stripe = 0;
+    uint32_t *rows = nullptr;  // per-row histograms (device), rps rows per stripe of pass-B tiles
+    std::vector<uint32_t> h;   // their sum over the 2^FUSED_HB top-bit bins (host)
+};
+
+static bool fused_applies(const Ctx &c, unsigned K, uint64_t npos) {
+    return c.fused && !c.use_lsd && npos >= c.fused_min && npos >= 4096 && K - 1 >= FUSED_HB / 2 && K <= 32;
+}
+
+// pass A over every window, and the duplication estimate from a sample of windows (on a side stream
+// it overlapped pass A but measured no faster: 26.3 vs 26.2 ms per step)
+static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &in, FusedA *A) {
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
+    unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
+    HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
+    dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                          M, table, SLOTS - 1, table + SLOTS);
+    HIP_CHECK(hipGetLastError());
+    constexpr int TILE = ExtractTraits<1>::TILE;
+    const uint64_t tiles = ceil_div(npos, TILE);
+    // rows in multiples of rps = pass-B tile / pass-A tile: rps consecutive rows count one stripe of
+    // pass B's tiles (stripe_cursor_kernel).  Pass-B workgroup: 512 threads (8 K-window tiles, two
+    // workgroups per CU).  With XCD-contiguous tiles and stripes the short runs of neighbouring tiles
+    // meet in one L2: extract stage 6.97 -> 5.61 ms vs 1024-thread tiles (16 K windows), which won
+    // before the XCD mapping (their longer runs: PMC writes 1.16 vs 1.30 x N w)
+    const int fbk = 512;
+    const uint32_t rps = (uint32_t)(16 * fbk / TILE);
+    uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
+    if (nrows >= rps) nrows -= nrows % rps;
+    const unsigned hb = FUSED_HB;
+    const uint32_t nbh = 1u << hb;
+    uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
+    uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, nbh * 4);
+    HIP_CHECK(hipMemsetAsync(h12, 0, nbh * 4, c.stream));
+    // stripes of pass B's tiles: S = nrows / rps stripes of per_stripe consecutive pass-B tiles
+    // (= rps per_stripe pass-A tiles); pass-A row r counts the per_row pass-A tiles
+    // [r per_row, (r + 1) per_row), so rows rps s .. rps s + rps - 1 cover stripe s.  One stripe
+    // (fewer rows than rps) takes every row, each an equal share of the tiles.
+    const uint64_t tiles_b = ceil_div(npos, (uint64_t)16 * fbk);
+    const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
+    const uint64_t per_stripe = ceil_div(tiles_b, stripes);
+    const uint64_t per_row = stripes == 1 ? ceil_div(tiles_b * rps, nrows) : per_stripe;
+    extract_hist_fast_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                   tiles, per_row, rows);
+    HIP_CHECK(hipGetLastError());
+    hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
+                              c.stream>>>(rows, nrows, nbh, h12);
+    HIP_CHECK(hipGetLastError());
+    A->h.assign(nbh, 0);
+    unsigned long long st[2];
+    HIP_CHECK(hipMemcpyAsync(A->h.data(), h12, nbh * 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(st, table + SLOTS, 16, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    uint64_t N = 0;
+    for (uint32_t v : A->h) N += v;
+    const double mv = (double)std::max<unsigned long long>(st[1], 1);
+    const double ew = 2.0 * (double)N * (double)st[0] / (mv * mv);
+    A->npos = npos;
+    A->N = N;
+    A->dup = N >= 16ull * M ? std::max(1.0, ew / 1.2) : 8.0;
+    A->nrows = nrows;
+    A->rps = rps;
+    A->stripes = stripes;
+    A->per_stripe = per_stripe;
+    A->rows = rows;
+}
+
+// a level-1 bucket mask of one collect round (extract_partition.hpp: FUSED_SEL_WORDS words)
+struct BucketSel {
+    uint32_t m[FUSED_SEL_WORDS] = {};
+    bool has(uint32_t b) const { return (m[b >> 5] >> (b & 31)) & 1u; }
+    void add(uint64_t lo, uint64_t hi) {
+        for (uint64_t b = lo; b < hi; ++b) m[b >> 5] |= 1u << (b & 31);
+    }
+};
+
+// pass B: the k-mers whose level-1 bucket (top b1 bits) is in `sel` (nullptr: every bucket)
+// scattered into ka by that bucket; returns their number and their level-1 counts in *dh1 (device;
+// zero outside `sel`)
+template <bool COUNTED>
+static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                             const FusedA &A, unsigned b1, const BucketSel *sel, Key<1> *ka, uint32_t *ca,
+                             const uint32_t **dh1_out) {
+    const uint32_t nb1 = 1u << b1;
+    const unsigned hb = FUSED_HB;
+    if (sel && nb1 > 32 * FUSED_SEL_WORDS) throw std::runtime_error("collect round mask: level-1 digit too wide");
+    std::vector<uint32_t> h1(nb1, 0);
+    for (uint32_t i = 0; i < (1u << hb); ++i) {
+        const uint32_t b = i >> (hb - b1);
+        if (!sel || sel->has(b)) h1[b] += A.h[i];
+    }
+    uint32_t *dsel = nullptr;
+    if (sel) {
+        dsel = (uint32_t *)c.ws.get(Workspace::FUSED_SEL, sizeof(sel->m));
+        HIP_CHECK(hipMemcpyAsync(dsel, sel->m, sizeof(sel->m), hipMemcpyHostToDevice, c.stream));
+    }
+    // level-1 bucket starts = the scatter cursors, then the bucket ends pass B checks its
+    // reservations against
+    std::vector<unsigned long long> cur(2 * nb1);
+    unsigned long long acc = 0;
+    for (uint32_t i = 0; i < nb1; ++i) {
+        cur[i] = acc;
+        acc += h1[i];
+    }
+    for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
+    uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, h1.size() * 4);
+    unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
+    HIP_CHECK(hipMemcpyAsync(dh1, h1.data(), h1.size() * 4, hipMemcpyHostToDevice, c.stream));
+    HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
+    // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t / per_stripe
+    static_assert(FusedTraits<COUNTED, 512>::TILE == 2 * ExtractTraits<1>::TILE, "a pass-B tile = 2 pass-A tiles");
+    auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)A.stripes * nb1 * 16);
+    unsigned long long *send = scur + (size_t)A.stripes * nb1;
+    stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(A.rows, A.nrows, hb, b1, A.stripes, A.rps, dcur, scur,
+                                                                 send, dsel);
+    HIP_CHECK(hipGetLastError());
+    EventTimer tm(c.stream);
+    tm.mark();
+    const bool fast_b = !COUNTED && K <= 32;
+    if (fast_b) {
+        constexpr int B = 512;
+        extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(A.npos, 16 * B))), dim3(B), 0,
+                                            c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe,
+                                                        scur, send, ka, &c.small->error, dsel);
+    } else {
+        const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, 512>::TILE);
+        extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
+            A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
+    }
+    HIP_CHECK(hipGetLastError());
+    cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)A.stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
+        scur, send, A.stripes * nb1, &c.small->error);
+    HIP_CHECK(hipGetLastError());
+    tm.mark();
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // `h1` / `cur` / `sel` are host memory
+    c.fused_ms = tm.ms(0, 1);
+    *dh1_out = dh1;
+    return acc;
+}
+
+// Returns false (nothing done) when the fused path does not apply; else N, the duplication
+// estimate, and the level-1 counts in *hist1 (device) with *ka scattered.
 template <int L2, bool COUNTED>
 static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                                 Key<L2> **ka, Key<L2> **kb, uint32_t **ca, uint32_t **cb, uint64_t *N_out,
@@ -1225,122 +1388,25 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         return false;
     } else {
         const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
-        if (!c.fused || c.use_lsd || npos < c.fused_min || npos < 4096 || K - 1 < FUSED_HB / 2) return false;
-        // the duplication estimate from a sample of windows (on a side stream it overlapped pass A but
-        // measured no faster: 26.3 vs 26.2 ms per step)
-        constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
-        unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
-        HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
-        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
-                                                                      M, table, SLOTS - 1, table + SLOTS);
-        HIP_CHECK(hipGetLastError());
-        // pass A: histogram of the top bits of every valid k-mer
-        constexpr int TILE = ExtractTraits<1>::TILE;
-        const uint64_t tiles = ceil_div(npos, TILE);
-        // rows in multiples of rps = pass-B tile / pass-A tile: rps consecutive rows count one
-        // stripe of pass B's tiles (stripe_cursor_kernel)
-        const bool fast_b = !COUNTED && K <= 32;
-        // pass-B workgroup: 512 threads (8 K-window tiles, two workgroups per CU).  With XCD-contiguous
-        // tiles and stripes the short runs of neighbouring tiles meet in one L2: extract stage 6.97 ->
-        // 5.61 ms vs 1024-thread tiles (16 K windows), which won before the XCD mapping (their longer
-        // runs: PMC writes 1.16 vs 1.30 x N w)
-        const int fbk = 512;
-        const uint32_t rps = (uint32_t)(16 * fbk / TILE);
-        uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
-        if (nrows >= rps) nrows -= nrows % rps;
-        const unsigned hb = FUSED_HB;
-        const uint32_t nbh = 1u << hb;
-        uint32_t *rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
-        uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, nbh * 4);
-        HIP_CHECK(hipMemsetAsync(h12, 0, nbh * 4, c.stream));
-        // stripes of pass B's tiles: S = nrows / rps stripes of per_stripe consecutive pass-B tiles
-        // (= rps per_stripe pass-A tiles); pass-A row r counts the per_row pass-A tiles
-        // [r per_row, (r + 1) per_row), so rows rps s .. rps s + rps - 1 cover stripe s.  One stripe
-        // (fewer rows than rps) takes every row, each an equal share of the tiles.
-        const uint64_t tiles_b = ceil_div(npos, (uint64_t)16 * fbk);
-        const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
-        const uint64_t per_stripe = ceil_div(tiles_b, stripes);
-        const uint64_t per_row = stripes == 1 ? ceil_div(tiles_b * rps, nrows) : per_stripe;
-        extract_hist_fast_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K,
-                                                                       canonical ? 1 : 0, tiles, per_row, rows);
-        HIP_CHECK(hipGetLastError());
-        hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
-                                  c.stream>>>(rows, nrows, nbh, h12);
-        HIP_CHECK(hipGetLastError());
-        std::vector<uint32_t> h(nbh);
-        unsigned long long st[2];
-        HIP_CHECK(hipMemcpyAsync(h.data(), h12, nbh * 4, hipMemcpyDeviceToHost, c.stream));
-        HIP_CHECK(hipMemcpyAsync(st, table + SLOTS, 16, hipMemcpyDeviceToHost, c.stream));
-        HIP_CHECK(hipStreamSynchronize(c.stream));
-        uint64_t N = 0;
-        for (uint32_t v : h) N += v;
-        const double mv = (double)std::max<unsigned long long>(st[1], 1);
-        const double ew = 2.0 * (double)N * (double)st[0] / (mv * mv);
-        const double dup = N >= 16ull * M ? std::max(1.0, ew / 1.2) : 8.0;
-        const MsdPlan plan = msd_plan<1>(c, N, 2 * K, dup);
+        if (!fused_applies(c, K, npos)) return false;
+        FusedA A;
+        fused_pass_a(c, K, canonical, in, &A);
+        const uint64_t N = A.N;
+        const MsdPlan plan = msd_plan<1>(c, N, 2 * K, A.dup);
         if (c.debug)
-            fprintf(stderr, "[mtg debug] fused extract N=%lu dup=%.2f levels=%u digit1=%u\n", (unsigned long)N, dup,
+            fprintf(stderr, "[mtg debug] fused extract N=%lu dup=%.2f levels=%u digit1=%u\n", (unsigned long)N, A.dup,
                     plan.levels, plan.levels ? plan.digit_end[1] : 0);
         if (!plan.levels) return false;  // nothing to partition: the plain extraction path
         const unsigned b1 = plan.digit_end[1];
-        // level-1 counts (fold of the pass-A histogram) and bucket starts = the scatter cursors
-        std::vector<uint32_t> h1(1u << b1, 0);
-        for (uint32_t i = 0; i < nbh; ++i) h1[i >> (hb - b1)] += h[i];
-        std::vector<unsigned long long> cur(1u << b1);
-        unsigned long long acc = 0;
-        for (uint32_t i = 0; i < (1u << b1); ++i) {
-            cur[i] = acc;
-            acc += h1[i];
-        }
-        // cursors, then the bucket ends pass B checks its reservations against
-        const uint32_t nb1 = 1u << b1;
-        cur.resize(2 * nb1);
-        for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
-        uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, h1.size() * 4);
-        unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
-        HIP_CHECK(hipMemcpyAsync(dh1, h1.data(), h1.size() * 4, hipMemcpyHostToDevice, c.stream));
-        HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
-        // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t / per_stripe
-        static_assert(FusedTraits<COUNTED, 512>::TILE == 2 * ExtractTraits<1>::TILE, "a pass-B tile = 2 pass-A tiles");
-        auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
-        unsigned long long *send = scur + (size_t)stripes * nb1;
-        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, hb, b1, stripes, rps, dcur, scur,
-                                                                     send);
-        HIP_CHECK(hipGetLastError());
         *ka = (Key<1> *)c.ws.get(Workspace::KA, std::max<uint64_t>(N, 1) * 8);
         *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(N, 1) * 8);
         *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
         *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(N, 1) * 4) : nullptr;
-        // pass B
-        EventTimer tm(c.stream);
-        tm.mark();
-        auto launch = [&](auto blk) {
-            constexpr int B = decltype(blk)::value;
-            const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, B>::TILE);
-            extract_partition_kernel<COUNTED, B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
-                per_stripe, scur, send, *ka, COUNTED ? *ca : nullptr, &c.small->error);
-        };
-        if (fast_b) {
-            constexpr int B = 512;
-            extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * B))), dim3(B), 0,
-                                                c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, per_stripe,
-                                                            scur, send, *ka, &c.small->error);
-        } else {
-            launch(std::integral_constant<int, 512>());
-        }
-        HIP_CHECK(hipGetLastError());
-        cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
-            scur, send, stripes * nb1, &c.small->error);
-        HIP_CHECK(hipGetLastError());
-        tm.mark();
-        HIP_CHECK(hipStreamSynchronize(c.stream));  // `h1` / `cur` are host locals
-        c.fused_ms = tm.ms(0, 1);
+        fused_pass_b<COUNTED>(c, K, canonical, cmax, in, A, b1, nullptr, *ka, COUNTED ? *ca : nullptr, hist1_out);
         c.timings.n_positions = npos;
         c.timings.n_extracted = N;
         *N_out = N;
-        *dup_out = dup;
-        *hist1_out = dh1;
+        *dup_out = A.dup;
         return true;
     }
 }
@@ -1509,6 +1575,129 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
     }
     c.timings.n_extracted = total / (canonical ? 2 : 1);  // valid windows (one k-mer per strand each)
     return off;
+}
+
+// ------------------------------------------------ canonical key rounds of the fused K1 (configs[3])
+//
+// configs[3]'s share of one GPU (125 M reads, 1.5e10 windows) does not fit one pass: its canonical
+// k-mers alone are 120 GB, twice that with the sort's ping-pong buffer.  collect_ranges re-scans
+// every read once per key range and extracts BOTH strands (19 ranges and 3.0e10 keys sorted there:
+// 1.35 s of a 1.45 s step).  Here the fused K1's pass A runs once, and the canonical k-mers are
+// collected in R rounds, each a contiguous interval of the level-1 buckets of the WHOLE input's MSD
+// plan: pass B keeps only the round's buckets (extract_partition.hpp: a bucket mask), and the round's keys
+// are sorted and deduplicated with that plan's later levels -- every final bucket has the size it
+// has in a one-pass build -- and appended to the canonical set, in BOSS order since the rounds are.
+// The rc stage, the dummies and the emit then run on the whole canonical set exactly as in the
+// one-pass build (the role of SortedSetDisk's merged chunks, boss_chunk_construct.cpp:664-933).
+// R is the fewest rounds whose sort buffers fit next to what the later stages hold
+// (memory_preallocated, else the free HBM).  False (nothing kept) where the fused K1 does not apply.
+template <bool COUNTED>
+static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
+                                 Key<1> **out, uint32_t **outc, uint64_t *U_out) {
+    using K2 = Key<1>;
+    const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
+    if (c.range_scan || c.disk || !fused_applies(c, K, npos)) return false;
+    FusedA A;
+    fused_pass_a(c, K, canonical, in, &A);
+    const uint64_t N = A.N;
+    const MsdPlan plan = msd_plan<1>(c, N, 2 * K, A.dup);
+    if (!plan.levels) return false;
+    const unsigned b1 = plan.digit_end[1];
+    const uint32_t nb1 = 1u << b1;
+    std::vector<uint64_t> h1(nb1, 0);
+    for (uint32_t i = 0; i < (1u << FUSED_HB); ++i) h1[i >> (FUSED_HB - b1)] += A.h[i];
+    // rounds: the later stages hold ~5 keys of 8 B per distinct canonical k-mer (the canonical set, the
+    // real edges, the rc sort's two buffers) plus the rows; a round holds its keys twice (+ counts)
+    uint32_t R = c.force_ranges;
+    if (!R) {
+        double budget = c.mem_budget;
+        if (budget <= 0) {
+            size_t fr = 0, tot = 0;
+            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            budget = 0.9 * ((double)fr + (double)c.ws.held());
+        }
+        const double u_est = std::min((double)N, (double)N / A.dup * 1.25);
+        const double per_u = 8.0 * 5 + 4.0 + (COUNTED ? 4.0 * 5 + 8.0 : 0.0);
+        const double per_key = COUNTED ? 24.0 : 16.0;
+        const double avail = budget - per_u * u_est;
+        R = avail > 0 ? (uint32_t)std::min<double>(std::ceil((double)N * per_key / avail), nb1) : nb1;
+        R = std::max<uint32_t>(R, 2);
+    }
+    R = std::min(R, nb1);
+    const std::vector<uint64_t> bb = balanced_bounds(h1.data(), nb1, (int)R);
+    std::vector<uint64_t> nr(R, 0);
+    uint64_t nmax = 1;
+    for (uint32_t r = 0; r < R; ++r) {
+        for (uint64_t b = bb[r]; b < bb[r + 1]; ++b) nr[r] += h1[b];
+        nmax = std::max(nmax, nr[r]);
+    }
+    K2 *ka = (K2 *)c.ws.get(Workspace::KA, nmax * 8);
+    K2 *kb = (K2 *)c.ws.get(Workspace::KB, nmax * 8);
+    uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nmax * 4) : nullptr;
+    uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nmax * 4) : nullptr;
+    if (c.debug)
+        fprintf(stderr, "[mtg debug] canonical rounds: N=%lu dup=%.2f levels=%u digit1=%u rounds=%u largest=%lu\n",
+                (unsigned long)N, A.dup, plan.levels, b1, R, (unsigned long)nmax);
+    c.timings.n_positions = npos;
+    c.timings.n_extracted = N;
+    c.timings.n_batches = R;
+    c.timings.collect_mode = 2;
+    uint64_t off = 0, cap = 0;
+    *out = nullptr;
+    *outc = nullptr;
+    bool first = true;
+    for (uint32_t r = 0; r < R; ++r) {
+        if (!nr[r]) continue;
+        const uint32_t *dh1 = nullptr;
+        BucketSel sel;
+        sel.add(bb[r], bb[r + 1]);
+        const uint64_t n = fused_pass_b<COUNTED>(c, K, canonical, cmax, in, A, b1, &sel, ka, ca, &dh1);
+        if (n != nr[r]) throw std::runtime_error("a collect round's k-mers differ from its histogram");
+        K2 *xa = ka, *xb = kb;
+        uint32_t *xac = ca, *xbc = cb;
+        c.track_partition = first;  // the roofline's partition pass: the first round's level 2
+        const uint64_t U = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n, 2 * K, cmax, A.dup, dh1, false,
+                                                       nullptr, true, nullptr, &plan);
+        c.track_partition = false;
+        first = false;
+        if (off + U > cap) {
+            // first round: size the canonical set from its distinct ratio (+25 %); later growth keeps
+            // what is already appended
+            const uint64_t want = off == 0 ? (uint64_t)((double)U / (double)n * (double)N * 1.25) + U
+                                           : (off + U) + (off + U) / 4;
+            cap = std::max(want, off + U);
+            *out = (K2 *)c.ws.get(Workspace::CANON, cap * sizeof(K2), off * sizeof(K2), c.stream);
+            if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, cap * 4, off * 4, c.stream);
+        }
+        HIP_CHECK(hipMemcpyAsync(*out + off, xa, U * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+        if (COUNTED) HIP_CHECK(hipMemcpyAsync(*outc + off, xac, U * 4, hipMemcpyDeviceToDevice, c.stream));
+        off += U;
+        if (c.debug)
+            fprintf(stderr, "[mtg debug]   round %u: buckets [%lu, %lu) n=%lu -> %lu distinct\n", r,
+                    (unsigned long)bb[r], (unsigned long)bb[r + 1], (unsigned long)n, (unsigned long)U);
+    }
+    if (!*out) {
+        *out = (K2 *)c.ws.get(Workspace::CANON, sizeof(K2));
+        if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, 4);
+    }
+    // the round buffers the later stages do not reuse (they take KB and SPEC_A again)
+    for (auto sl : {Workspace::KA, Workspace::CA, Workspace::SPEC_B}) c.ws.release(sl);
+    // the fused rc merge reads the canonical keys through their bucket index over the rc sort's final
+    // bits (a one-pass build gets it from its own sort's groups)
+    c.gidx = Ctx::GroupIndex{};
+    if (canonical && off && !COUNTED) {
+        const MsdPlan rp = msd_plan<1>(c, off, 2 * K, 1.0);
+        const unsigned fb = rp.levels ? rp.digit_end[rp.levels] : 0;
+        if (fb && fb <= 26) {
+            const uint64_t nb = 1ull << fb;
+            uint64_t *gi = (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8);
+            bucket_index<1>(c, *out, off, 2 * K - fb, nb, gi);
+            HIP_CHECK(hipMemcpyAsync(gi + nb + 1, gi + nb, 8, hipMemcpyDeviceToDevice, c.stream));
+            c.gidx = Ctx::GroupIndex{*out, off, fb, 2 * K, gi};
+        }
+    }
+    *U_out = off;
+    return true;
 }
 
 // K4: the reverse complements of a sorted canonical set ka[0..U) (add_reverse_complements,
@@ -1878,10 +2067,22 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     }
     uint64_t U = 0, R = 0;
     int ev_extract, ev_sort, ev_unique;
+    bool rounds = false;  // the canonical set collected in rounds of the fused K1 (collect_rounds_fused)
     if (P > 1) {
-        // ---- K1-K4 one key range at a time (both strands in canonical mode): the real edges
         ev_extract = tm.mark();
-        R = U = collect_ranges<L2, COUNTED>(c, K, canonical, cmax, in, P, &ka, &ca);
+        if constexpr (L2 == 1) {
+            rounds = collect_rounds_fused<COUNTED>(c, K, canonical, cmax, in, &ka, &ca, &U);
+            if (rounds) {
+                R = U;
+                kb = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(U, 1) * sizeof(K2));
+                cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(U, 1) * 4) : nullptr;
+            }
+        }
+        if (!rounds) {
+            // ---- K1-K4 one key range at a time (both strands in canonical mode): the real edges
+            R = U = collect_ranges<L2, COUNTED>(c, K, canonical, cmax, in, P, &ka, &ca);
+            T.collect_mode = 1;
+        }
         ev_sort = ev_unique = tm.mark();
         T.n_unique = U;
     } else {
@@ -1907,7 +2108,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     // on its own (no duplicates) and merged with it
     R = U;
     }
-    if (canonical && U && P == 1) {
+    if (canonical && U && (P == 1 || rounds)) {
         K2 *rk;
         uint32_t *rkc;
         // the real edges hold at most 2U keys (the palindromes of even K drop out of the rc set)
@@ -2367,13 +2568,18 @@ static uint64_t collect_ranges_dist(Ctx &c, Dist &d, unsigned K, bool canonical,
 // (8 GPUs) the local dedupe keeps ~2/3 of the k-mers, so nearly every k-mer was sorted twice
 // (DESIGN.md section 8).  Returns false when the fused extraction does not apply (the caller runs
 // the local-collect path).
+// the routed collect needs the fused K1 (u64 keys); MTG_COLLECT=ranges keeps the key-range collect
+static bool routed_applies(const Ctx &c, unsigned K) {
+    return c.fused && !c.use_lsd && K - 1 >= FUSED_HB / 2 && K <= 32 && !c.range_scan;
+}
+
 template <bool COUNTED>
 static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                                 Key<1> **xa_out, uint32_t **xac_out, uint64_t *U_out, std::vector<uint64_t> *bounds,
                                 Tracer &tr, EventTimer &tm, int *ev_extract, int *ev_sort) {
     using K2 = Key<1>;
     // the same on every rank (no input-size test: a rank may hold no reads)
-    if (!c.fused || c.use_lsd || K - 1 < FUSED_HB / 2 || K > 32 || c.force_ranges) return false;
+    if (!routed_applies(c, K)) return false;
     // one-window reads (KMC input) are cheaper through window_reads_kernel and the local collect; the
     // decision must agree on every rank, so a rank's layout is shared by an all-reduce
     {
@@ -2461,102 +2667,207 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     d.shift2 = 2 * K - OB;
     d.nb = NOB;
     tr("route plan", N, Nall);
-    // pass B: this rank's k-mers scattered by their top B1 bits (the single build's fused pass)
     const uint32_t nb1 = 1u << B1;
-    std::vector<uint32_t> h1(nb1, 0);
-    for (uint32_t i = 0; i < NBH; ++i) h1[i >> (FUSED_HB - B1)] += hl[i];
-    std::vector<unsigned long long> cur(2 * nb1);
-    unsigned long long acc = 0;
-    for (uint32_t i = 0; i < nb1; ++i) {
-        cur[i] = acc;
-        acc += h1[i];
-    }
-    for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
-    K2 *ka = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(N, 1) * 8);
-    uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
-    if (nrows) {
-        unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
-        HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
-        auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
-        unsigned long long *send = scur + (size_t)stripes * nb1;
-        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, FUSED_HB, B1, stripes, rps, dcur, scur,
-                                                                     send);
-        HIP_CHECK(hipGetLastError());
-        if (!COUNTED) {
-            extract_partition_fast_kernel<512><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), 0,
-                                                  c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
-                                                              scur, send, ka, &c.small->error);
-        } else {
-            const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
-            extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
-                in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
-                B1, per_stripe, scur, send, ka, ca, &c.small->error);
+    // rounds (configs[3]: 1.5e10 windows per rank): one pass when this rank's keys, the received runs
+    // and their sort buffer fit; else every owner's level-1 buckets are cut into `rounds` sub-intervals
+    // (balanced on the global histogram) and round r collects sub-interval r of every owner -- pass B
+    // keeps only those buckets, exchange 1 and the owner sort run per round, and the owner appends the
+    // rounds' distinct keys in BOSS order.  All ranks agree on the count (an all-gather of the most
+    // any rank needs).  The key-range collect (collect_ranges_dist) re-scanned every read per range
+    // and extracted both strands.
+    uint32_t rounds = 1;
+    {
+        uint64_t want = c.force_ranges;
+        if (!want) {
+            double budget = c.mem_budget;
+            if (budget <= 0) {
+                size_t fr = 0, tot = 0;
+                HIP_CHECK(hipMemGetInfo(&fr, &tot));
+                budget = 0.9 * ((double)fr + (double)c.ws.held());
+            }
+            const double per_key = 8.0 + (COUNTED ? 4.0 : 0.0);
+            // one pass: the rank's keys, the received runs and their ping-pong buffer, plus ~3 N of later
+            // stages (the owned canonical set, its rc keys, the real edges) at low duplication
+            const double need = (double)N * per_key * 3.0;
+            want = need * 2.0 <= budget ? 1 : (uint64_t)std::ceil(need / (0.45 * budget));
         }
-        HIP_CHECK(hipGetLastError());
-        cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
-            scur, send, stripes * nb1, &c.small->error);
-        HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipStreamSynchronize(c.stream));  // cur is a host local
+        uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, (1 + (uint64_t)d.P) * 8);
+        HIP_CHECK(hipMemcpyAsync(dv, &want, 8, hipMemcpyHostToDevice, c.stream));
+        d.comm.allgather_u64(dv, dv + 1, 1, c.stream);
+        std::vector<uint64_t> all(d.P);
+        HIP_CHECK(hipMemcpyAsync(all.data(), dv + 1, (uint64_t)d.P * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // `want` is a host local
+        uint64_t r = 1;
+        for (uint64_t v : all) r = std::max(r, v);
+        rounds = (uint32_t)std::min<uint64_t>(r, 64);
     }
+    // global level-1 counts, and every owner's bucket interval cut into the rounds
+    std::vector<uint64_t> gh1(nb1, 0);
+    for (uint32_t i = 0; i < NBH; ++i) gh1[i >> (FUSED_HB - B1)] += H[i];
+    std::vector<std::vector<uint64_t>> sub(d.P);
+    for (int o = 0; o < d.P; ++o) {
+        const uint64_t o0 = std::min<uint64_t>((*bounds)[o] << (B1 - OB), nb1);
+        const uint64_t o1 = std::min<uint64_t>((*bounds)[o + 1] << (B1 - OB), nb1);
+        sub[o] = balanced_bounds(gh1.data() + o0, o1 - o0, (int)rounds);
+        for (auto &v : sub[o]) v += o0;
+    }
+    const uint64_t ob0 = std::min<uint64_t>((*bounds)[d.me] << (B1 - OB), nb1);
+    const uint64_t ob1 = std::min<uint64_t>((*bounds)[d.me + 1] << (B1 - OB), nb1);
     c.timings.n_extracted = N;
-    *ev_extract = tm.mark();
-    tr("extract + scatter", N);
-    // exchange 1: owner o gets the rank's buckets of its prefixes [bounds[o], bounds[o + 1])
-    std::vector<std::vector<uint64_t>> soff(1, std::vector<uint64_t>(d.P + 1));
-    for (int j = 0; j <= d.P; ++j) {
-        const uint64_t b = (*bounds)[j] << (B1 - OB);  // first level-1 bucket of the prefix
-        soff[0][j] = b >= nb1 ? N : cur[b];
+    c.timings.n_batches = rounds;
+    if (rounds > 1) {
+        c.timings.collect_mode = 2;
+        *ev_extract = tm.mark();
     }
-    K2 *xa = ka;
-    uint32_t *xac = ca;
-    uint64_t n1 = N;
-    if (d.P == 1) {  // one rank: its keys stay where they are (the buffers change slots instead of a copy)
-        c.ws.swap(Workspace::KA, Workspace::XA);
-        if (COUNTED) c.ws.swap(Workspace::CA, Workspace::XAC);
-    } else {
-        const K2 *arrs[1] = {ka};
-        const uint32_t *cnts[1] = {ca};
-        n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA, Workspace::XAC, &xa, &xac);
-    }
-    tr("exchange 1", n1);
-    // the owner's level-1 counts: the global pass-A histogram over its buckets
-    const uint64_t ob0 = (*bounds)[d.me] << (B1 - OB), ob1 = std::min<uint64_t>((*bounds)[d.me + 1] << (B1 - OB), nb1);
-    std::vector<uint32_t> hown(nb1, 0);
-    uint64_t nown = 0;
-    for (uint32_t i = 0; i < NBH; ++i) {
-        const uint32_t b = i >> (FUSED_HB - B1);
-        if (b >= ob0 && b < ob1) {
-            hown[b] += (uint32_t)H[i];
-            nown += H[i];
-        }
-    }
-    if (nown != n1) throw std::runtime_error("received k-mers differ from the global histogram of the owned range");
-    uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
-    HIP_CHECK(hipMemcpyAsync(dh1, hown.data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
-    // plan: the keys fill (ob1 - ob0) of the nb1 level-1 buckets; level 1 is "done" (the buckets are
-    // known from the histogram), level 2 partitions the P runs in one pass (any input order)
+    K2 *acc = nullptr;  // rounds: the owned distinct keys so far
+    uint32_t *accc = nullptr;
+    uint64_t off = 0, cap = 0;
+    K2 *xa = nullptr;
+    uint32_t *xac = nullptr;
     uint64_t U = 0;
-    if (n1) {
-        K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
-        uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
-        const double spread = (double)nb1 / (double)std::max<uint64_t>(1, ob1 - ob0);
-        const double dup = estimate_dup<1>(c, xa, n1, 8.0) / spread;
-        MsdPlan plan = msd_plan<1>(c, n1, 2 * K, dup);
-        unsigned T = plan.levels ? plan.digit_end[plan.levels] : 0;
-        T = std::min(2 * K, std::max(T, B1 + 1));  // at least one partition pass after the routing digit
-        MsdPlan fp{};
-        fp.levels = 1 + (T - B1 + MSD_DBITS - 1) / MSD_DBITS;
-        fp.digit_end[1] = B1;
-        for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
-        c.track_partition = true;
-        c.want_gidx = canonical;
-        U = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup, dh1, false, nullptr, true,
-                                        nullptr, &fp);
-        c.want_gidx = false;
-        c.track_partition = false;
+    for (uint32_t r = 0; r < rounds; ++r) {
+        BucketSel sel;
+        for (int o = 0; o < d.P; ++o) sel.add(sub[o][r], sub[o][r + 1]);
+        const BucketSel *rs = rounds > 1 ? &sel : nullptr;
+        // pass B: this rank's k-mers (of the round's buckets) scattered by their top B1 bits (the single
+        // build's fused pass)
+        std::vector<uint32_t> h1(nb1, 0);
+        for (uint32_t i = 0; i < NBH; ++i) {
+            const uint32_t b = i >> (FUSED_HB - B1);
+            if (!rs || rs->has(b)) h1[b] += hl[i];
+        }
+        std::vector<unsigned long long> cur(2 * nb1);
+        unsigned long long nr = 0;
+        for (uint32_t i = 0; i < nb1; ++i) {
+            cur[i] = nr;
+            nr += h1[i];
+        }
+        for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
+        K2 *ka = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(nr, 1) * 8);
+        uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(nr, 1) * 4) : nullptr;
+        if (nrows) {
+            uint32_t *dsel = nullptr;
+            if (rs) {
+                dsel = (uint32_t *)c.ws.get(Workspace::FUSED_SEL, sizeof(rs->m));
+                HIP_CHECK(hipMemcpyAsync(dsel, rs->m, sizeof(rs->m), hipMemcpyHostToDevice, c.stream));
+            }
+            unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
+            HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
+            auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
+            unsigned long long *send = scur + (size_t)stripes * nb1;
+            stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, FUSED_HB, B1, stripes, rps, dcur,
+                                                                         scur, send, dsel);
+            HIP_CHECK(hipGetLastError());
+            if (!COUNTED) {
+                extract_partition_fast_kernel<512><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), 0,
+                                                      c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
+                                                                  scur, send, ka, &c.small->error, dsel);
+            } else {
+                const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
+                extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+                    in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
+                    B1, per_stripe, scur, send, ka, ca, &c.small->error, dsel);
+            }
+            HIP_CHECK(hipGetLastError());
+            cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
+                scur, send, stripes * nb1, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipStreamSynchronize(c.stream));  // cur / sel are host memory
+        }
+        if (rounds == 1) *ev_extract = tm.mark();
+        tr("extract + scatter", nr);
+        // exchange 1: owner o gets the rank's buckets of its prefixes [bounds[o], bounds[o + 1]) (of
+        // this round: the other buckets are empty)
+        std::vector<std::vector<uint64_t>> soff(1, std::vector<uint64_t>(d.P + 1));
+        for (int j = 0; j <= d.P; ++j) {
+            const uint64_t b = (*bounds)[j] << (B1 - OB);  // first level-1 bucket of the prefix
+            soff[0][j] = b >= nb1 ? nr : cur[b];
+        }
+        xa = ka;
+        xac = ca;
+        uint64_t n1 = nr;
+        if (d.P == 1) {  // one rank: its keys stay where they are (the buffers change slots instead of a copy)
+            c.ws.swap(Workspace::KA, Workspace::XA);
+            if (COUNTED) c.ws.swap(Workspace::CA, Workspace::XAC);
+        } else {
+            const K2 *arrs[1] = {ka};
+            const uint32_t *cnts[1] = {ca};
+            n1 = exchange_runs<K2>(c, d, 1, arrs, COUNTED ? cnts : nullptr, soff, Workspace::XA, Workspace::XAC, &xa,
+                                   &xac);
+        }
+        tr("exchange 1", n1);
+        // the owner's level-1 counts: the global pass-A histogram over its buckets (of this round)
+        const uint64_t rb0 = rs ? sub[d.me][r] : ob0, rb1 = rs ? sub[d.me][r + 1] : ob1;
+        std::vector<uint32_t> hown(nb1, 0);
+        uint64_t nown = 0;
+        for (uint32_t i = 0; i < NBH; ++i) {
+            const uint32_t b = i >> (FUSED_HB - B1);
+            if (b >= rb0 && b < rb1) {
+                hown[b] += (uint32_t)H[i];
+                nown += H[i];
+            }
+        }
+        if (nown != n1) throw std::runtime_error("received k-mers differ from the global histogram of the owned range");
+        uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
+        HIP_CHECK(hipMemcpyAsync(dh1, hown.data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
+        // plan: the keys fill (rb1 - rb0) of the nb1 level-1 buckets; level 1 is "done" (the buckets are
+        // known from the histogram), level 2 partitions the P runs in one pass (any input order)
+        uint64_t Ur = 0;
+        if (n1) {
+            K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
+            uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
+            const double spread = (double)nb1 / (double)std::max<uint64_t>(1, rb1 - rb0);
+            const double dup = estimate_dup<1>(c, xa, n1, 8.0) / spread;
+            MsdPlan plan = msd_plan<1>(c, n1, 2 * K, dup);
+            unsigned T = plan.levels ? plan.digit_end[plan.levels] : 0;
+            T = std::min(2 * K, std::max(T, B1 + 1));  // at least one partition pass after the routing digit
+            MsdPlan fp{};
+            fp.levels = 1 + (T - B1 + MSD_DBITS - 1) / MSD_DBITS;
+            fp.digit_end[1] = B1;
+            for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
+            c.track_partition = r == 0;
+            c.want_gidx = canonical && rounds == 1;
+            Ur = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup, dh1, false, nullptr, true,
+                                             nullptr, &fp);
+            c.want_gidx = false;
+            c.track_partition = false;
+        }
+        tr("owner sort", Ur);
+        if (rounds == 1) {
+            U = Ur;
+            break;
+        }
+        if (off + Ur > cap) {
+            // first filled round: size the owned set from its share of the owner's range (+25 %)
+            uint64_t gr = 0, go = 0;
+            for (uint64_t b = rb0; b < rb1; ++b) gr += gh1[b];
+            for (uint64_t b = ob0; b < ob1; ++b) go += gh1[b];
+            const uint64_t want = off == 0 && gr ? (uint64_t)((double)Ur / (double)gr * (double)go * 1.25) + Ur
+                                                 : (off + Ur) + (off + Ur) / 4;
+            cap = std::max(want, off + Ur);
+            acc = (K2 *)c.ws.get(Workspace::CANON, cap * sizeof(K2), off * sizeof(K2), c.stream);
+            if (COUNTED) accc = (uint32_t *)c.ws.get(Workspace::CANONC, cap * 4, off * 4, c.stream);
+        }
+        if (Ur) {
+            HIP_CHECK(hipMemcpyAsync(acc + off, xa, Ur * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+            if (COUNTED) HIP_CHECK(hipMemcpyAsync(accc + off, xac, Ur * 4, hipMemcpyDeviceToDevice, c.stream));
+        }
+        off += Ur;
+    }
+    if (rounds > 1) {
+        if (!acc) {
+            acc = (K2 *)c.ws.get(Workspace::CANON, sizeof(K2));
+            if (COUNTED) accc = (uint32_t *)c.ws.get(Workspace::CANONC, 4);
+        }
+        xa = acc;
+        xac = accc;
+        U = off;
+        // the round buffers go before the rc exchange and the dummy stage grow theirs
+        for (auto sl : {Workspace::XA, Workspace::XB, Workspace::XAC, Workspace::XBC, Workspace::SPEC_A,
+                        Workspace::SPEC_B})
+            c.ws.release(sl);
     }
     *ev_sort = tm.mark();
-    tr("owner sort", U);
     *xa_out = xa;
     *xac_out = xac;
     *U_out = U;
@@ -2705,8 +3016,12 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     uint32_t *Ec = nullptr;
     uint64_t R = 0;
     std::vector<uint64_t> bounds;
-    const uint32_t rounds = plan_rounds_dist<L2, COUNTED>(c, d, K, canonical, in);
+    // the routed collect plans its own rounds (canonical k-mers of the fused K1); the other collects
+    // batch in key ranges that re-scan the reads
+    const bool routed_try = L2 == 1 && c.dist_collect == 1 && !c.disk && routed_applies(c, K);
+    const uint32_t rounds = routed_try ? 1 : plan_rounds_dist<L2, COUNTED>(c, d, K, canonical, in);
     if (rounds > 1) {
+        T.collect_mode = 1;
         // ---- K1-K4 in rounds of key batches (both strands in canonical mode): the owned real edges
         d.m = RB_CHARS;
         d.shift2 = 2 * K - 2 * d.m;
@@ -3794,7 +4109,7 @@ int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_c
         return MTG_ERR_ARGUMENT;
     }
     try {
-        KmcInput in = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0);
+        KmcInput in = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0, stage_threads(c));
         std::lock_guard<std::mutex> lock(c->kmc_mu);
         if (in.total) c->kmc.push_back(std::move(in));
         return MTG_OK;
@@ -4153,12 +4468,12 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         const auto t_input = std::chrono::steady_clock::now();
         uint64_t seq_base = len, read_base = nr;
         for (const auto &m : c->kmc) {
-            uint64_t *dlut = (uint64_t *)c->ctx.ws.get(Workspace::KMC_LUT, m.lut.size() * 8);
-            uint8_t *drec = (uint8_t *)c->ctx.ws.get(Workspace::KMC_REC, m.records.size() + 1);
-            HIP_CHECK(hipMemcpyAsync(dlut, m.lut.data(), m.lut.size() * 8, hipMemcpyHostToDevice, s));
-            HIP_CHECK(hipMemcpyAsync(drec, m.records.data(), m.records.size(), hipMemcpyHostToDevice, s));
+            uint64_t *dlut = (uint64_t *)c->ctx.ws.get(Workspace::KMC_LUT, m.nlut * 8);
+            uint8_t *drec = (uint8_t *)c->ctx.ws.get(Workspace::KMC_REC, m.record_bytes() + 1);
+            HIP_CHECK(hipMemcpyAsync(dlut, m.lut_bytes(), m.nlut * 8, hipMemcpyHostToDevice, s));
+            HIP_CHECK(hipMemcpyAsync(drec, m.records(), m.record_bytes(), hipMemcpyHostToDevice, s));
             kmc_decode_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m.total, 256), 65536))),
-                                dim3(256), 0, s>>>(drec, dlut, m.lut.size(), m.total, m.k, m.lut_len,
+                                dim3(256), 0, s>>>(drec, dlut, m.nlut, m.total, m.k, m.lut_len,
                                                    m.counter_size, m.min_count, m.max_count, m.both ? 1 : 0,
                                                    dseq, seq_base, dstarts, dcounts, read_base);
             HIP_CHECK(hipGetLastError());
@@ -4293,12 +4608,12 @@ int mtg_kmc_load_device(const char *kmc_path, uint64_t min_count, uint64_t max_c
         HIP_CHECK(hipMalloc(&out->read_starts, std::max<uint64_t>(out->n_reads, 1) * 8));
         HIP_CHECK(hipMalloc(&out->counts, std::max<uint64_t>(out->n_reads, 1) * 4));
         if (m.total) {
-            HIP_CHECK(hipMalloc(&dlut, m.lut.size() * 8));
-            HIP_CHECK(hipMalloc(&drec, m.records.size() + 1));
-            HIP_CHECK(hipMemcpy(dlut, m.lut.data(), m.lut.size() * 8, hipMemcpyHostToDevice));
-            HIP_CHECK(hipMemcpy(drec, m.records.data(), m.records.size(), hipMemcpyHostToDevice));
+            HIP_CHECK(hipMalloc(&dlut, m.nlut * 8));
+            HIP_CHECK(hipMalloc(&drec, m.record_bytes() + 1));
+            HIP_CHECK(hipMemcpy(dlut, m.lut_bytes(), m.nlut * 8, hipMemcpyHostToDevice));
+            HIP_CHECK(hipMemcpy(drec, m.records(), m.record_bytes(), hipMemcpyHostToDevice));
             kmc_decode_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m.total, 256), 65536))),
-                                dim3(256)>>>(drec, dlut, m.lut.size(), m.total, m.k, m.lut_len, m.counter_size,
+                                dim3(256)>>>(drec, dlut, m.nlut, m.total, m.k, m.lut_len, m.counter_size,
                                              m.min_count, m.max_count, m.both ? 1 : 0, out->seq, 0, out->read_starts,
                                              out->counts, 0);
             HIP_CHECK(hipGetLastError());

@@ -18,6 +18,7 @@
 namespace mtg {
 
 constexpr unsigned FUSED_HB = 12;  // histogram bits of pass A (>= any level-1 digit)
+constexpr uint32_t FUSED_SEL_WORDS = 16;  // a level-1 bucket mask of a collect round (<= 512 buckets)
 
 // Stage a tile's read bytes as 2-bit codes (4 = invalid) in LDS: one dword load, four encodes and
 // one dword LDS store per thread step when the bytes are 4-aligned, byte loads for the tail.
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
     const uint64_t *__restrict__ rid_at, uint32_t cmax, unsigned b, uint64_t per_stripe, unsigned long long *__restrict__ cursor,
     const unsigned long long *__restrict__ bend, Key<1> *__restrict__ kout, uint32_t *__restrict__ vout,
-    uint32_t *__restrict__ error) {
+    uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
     using F = FusedTraits<COUNTED, BLOCK_>;
     constexpr int BLOCK = F::BLOCK, PPT = F::PPT, TILE = F::TILE;
     constexpr int NBMAX = 512;
@@ -200,6 +201,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
     __shared__ unsigned long long s_gbase[NBMAX];
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    __shared__ uint32_t s_sel[FUSED_SEL_WORDS];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t nb = 1u << b;
@@ -208,14 +210,22 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint64_t tile = xcd_tile((npos + TILE - 1) / TILE);
     if (tile * TILE >= npos) return;
     for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    if (sel && tid < FUSED_SEL_WORDS) s_sel[tid] = sel[tid];
     const uint64_t base = tile * TILE;
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
     stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
     __syncthreads();
     Key<1> kk[PPT];
     uint32_t cc[PPT];
-    const uint32_t m = slide_windows<1, COUNTED, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos, K,
-                                                            canonical, read_starts, read_counts, n_reads, rid_at, cmax, kk, cc);
+    uint32_t m = slide_windows<1, COUNTED, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos, K,
+                                                      canonical, read_starts, read_counts, n_reads, rid_at, cmax, kk, cc);
+    if (sel) {  // one round of a batched collect: only the level-1 buckets of its mask
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const uint32_t pb = key_prefix(kk[j], 2 * K, b);
+            if (!((s_sel[pb >> 5] >> (pb & 31)) & 1u)) m &= ~(1u << j);
+        }
+    }
     uint32_t r[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j)
@@ -277,7 +287,7 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
-    Key<1> *__restrict__ kout, uint32_t *__restrict__ error) {
+    Key<1> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
     constexpr int NBMAX = 512;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
@@ -287,6 +297,7 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
     __shared__ unsigned long long s_gbase[NBMAX];
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    __shared__ uint32_t s_sel[FUSED_SEL_WORDS];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t nb = 1u << b;
@@ -295,6 +306,7 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     const uint64_t tile = xcd_tile((npos + TILE - 1) / TILE);
     if (tile * TILE >= npos) return;
     for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    if (sel && tid < FUSED_SEL_WORDS) s_sel[tid] = sel[tid];
     const uint64_t base = tile * TILE;
     const bool aligned = (((uintptr_t)(seq + base)) & 15) == 0;
     for (uint32_t w = tid; w < (uint32_t)NW; w += BLOCK) {  // word w = chars base + 16 w ..
@@ -359,6 +371,13 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
         m |= (uint32_t)((uint32_t)j < nwin && ((inv >> j) & maskK) == 0) << j;
     }
     const unsigned bshift = 2 * K - b;
+    if (sel) {  // one round of a batched collect: only the level-1 buckets of its mask
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const uint32_t pb = (uint32_t)(kk[j] >> bshift);
+            if (!((s_sel[pb >> 5] >> (pb & 31)) & 1u)) m &= ~(1u << j);
+        }
+    }
     uint32_t r[PPT];
 #pragma unroll
     for (int j = 0; j < PPT; ++j)
@@ -410,22 +429,25 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
 // nrows = rps S rows, rows rps s .. rps s + rps - 1 count exactly stripe s: stripe s of bucket i
 // starts at the bucket's start plus the stripe counts of stripes < s.  Contiguous stripes keep the
 // runs of neighbouring tiles (which one XCD runs together, xcd_tile) next to each other in a
-// bucket.  One workgroup per bucket, S <= 4 * 256.
+// bucket.  One workgroup per bucket, S <= 4 * 256.  Buckets outside the mask `sel` (not in this
+// round of a batched collect) get empty stripes.
 __global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__restrict__ rows, uint32_t nrows,
                                                             unsigned hb, unsigned b, uint32_t stripes, uint32_t rps,
                                                             const unsigned long long *__restrict__ bstart,
                                                             unsigned long long *__restrict__ cursor,
-                                                            unsigned long long *__restrict__ bend) {
+                                                            unsigned long long *__restrict__ bend,
+                                                            const uint32_t *__restrict__ sel = nullptr) {
     __shared__ uint32_t s_scan[256 / 64 + 1];
     constexpr int PER = 4;
     const uint32_t i = blockIdx.x, nb = 1u << b, f = 1u << (hb - b), nbh = 1u << hb;
+    const bool in = !sel || ((sel[i >> 5] >> (i & 31)) & 1u);
     uint32_t h[PER];
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t st = threadIdx.x * PER + q;
         h[q] = 0;
-        if (st < stripes) {
+        if (st < stripes && in) {
             const uint32_t r1 = stripes == 1 ? nrows : min(rps * st + rps, nrows);  // one stripe: every row
             for (uint32_t r = rps * st; r < r1; ++r)
                 for (uint32_t j = 0; j < f; ++j) h[q] += rows[(size_t)r * nbh + i * f + j];

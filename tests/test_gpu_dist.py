@@ -168,23 +168,31 @@ def test_dist_rccl_single_rank():
 
 # ------------------------------------------------------------ the batched (bounded-memory) collect
 #
-# A rank share too big for one pass (configs[3]: 125 M reads per GPU) is collected in rounds of key
-# batches: owner ranges on the top-char bins of the range kernels, each cut into `rounds` batches; per
-# round every rank extracts both strands of every owner's batch, dedupes, and the owners merge the P
-# runs (boss_pipeline.hip: collect_ranges_dist).  MTG_RANGES forces the rounds on small inputs.
+# A rank share too big for one pass (configs[3]: 125 M reads per GPU) is collected in rounds.  The
+# default for u64 keys (BOSS k 6..31) is the routed collect's rounds: every owner's level-1 buckets
+# cut into `rounds` sub-intervals, pass B of the fused K1 keeping one sub-interval of every owner per
+# round (boss_pipeline.hip: dist_collect_routed), canonical k-mers only.  Otherwise -- and with
+# MTG_COLLECT=ranges -- owner ranges on the top-char bins of the range kernels, each cut into `rounds`
+# batches; per round every rank extracts both strands of every owner's batch, dedupes, and the
+# owners merge the P runs (collect_ranges_dist).  MTG_RANGES forces the rounds on small inputs.
 
+@pytest.mark.parametrize("collect", ["routed", "ranges"])
 @pytest.mark.parametrize("P,rounds", [(1, 2), (2, 2), (2, 5), (3, 3), (4, 7)])
-def test_dist_rounds_random_reads(monkeypatch, P, rounds):
+def test_dist_rounds_random_reads(monkeypatch, P, rounds, collect):
     monkeypatch.setenv("MTG_RANGES", str(rounds))
+    if collect == "ranges":
+        monkeypatch.setenv("MTG_COLLECT", "ranges")
     for k, canonical, bits in ((30, True, 8), (31, False, 0), (45, True, 16), (63, True, 0),
-                               (70, False, 8), (4, True, 8), (5, False, 0), (7, True, 4)):
+                               (70, False, 8), (4, True, 8), (5, False, 0), (7, True, 4), (6, True, 0)):
         reads = _random_reads(200 + k, 600, 150, 6000, n_rate=0.005, lower=True)
         ctors = []
         check_dist(k, reads, P, canonical, bits, ctors_out=ctors)
         # BOSS k >= 5: batched (bins of 4 node chars leave the k - 1 >= 4 chars of every emission
-        # group on one rank)
+        # group on one rank); routed rounds for BOSS k 6..31 (collect_mode 2), else key ranges (1)
         want = rounds if k >= 5 else 1
+        mode = 2 if collect == "routed" and 6 <= k <= 31 else 1 if k >= 5 else 0
         assert all(c.timings().n_batches == want for c in ctors), (k, [c.timings().n_batches for c in ctors])
+        assert all(c.timings().collect_mode == mode for c in ctors), (k, [c.timings().collect_mode for c in ctors])
 
 
 @pytest.mark.parametrize("canonical,nodes", [(False, 591997), (True, 1159851)])
@@ -220,8 +228,12 @@ def test_dist_rounds_planned_from_memory_budget():
     assert all(c.timings().n_batches >= 2 for c in ctors)
 
 
-def test_dist_rounds_large_multi_tile(monkeypatch):
+@pytest.mark.parametrize("collect", ["routed", "ranges"])
+def test_dist_rounds_large_multi_tile(monkeypatch, collect):
+    # (8, True): configs[3]'s shape (canonical, k = 31, 8 ranks) in rounds
     monkeypatch.setenv("MTG_RANGES", "3")
+    if collect == "ranges":
+        monkeypatch.setenv("MTG_COLLECT", "ranges")
     reads = _random_reads(78, 30000, 150, 400000, n_rate=0.0005)
     for P, canonical in ((2, True), (4, False), (8, True)):
         check_dist(30, reads, P, canonical, bits=8)

@@ -1,0 +1,142 @@
+"""Canonical key rounds of the fused K1 (boss_pipeline.hip: collect_rounds_fused): a build too big
+for one pass (BASELINE configs[3]'s per-GPU share) runs pass A of the fused extraction once and
+collects the canonical k-mers in rounds of level-1 buckets of the whole input's MSD plan, then runs
+the one-pass rc, dummy and emit stages on the whole canonical set -- the bounded-memory role of the
+reference's disk container (boss_chunk_construct.cpp:664-933).  Bit-exact against the oracle
+(oracle/, boss_chunk_construct.cpp:54-356 + boss_chunk.cpp:32-133) on the same reads."""
+import importlib
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import bench
+from test_gpu_parity import _random_reads, assert_same
+
+boss = importlib.import_module("projects2014-metagenome_amd.boss")
+
+pytestmark = pytest.mark.gpu
+
+ROUNDS = 2  # timings.collect_mode of collect_rounds_fused (1: key ranges re-scanning the reads)
+
+
+def _build(k, seqs, canonical, bits, counts=None, **kw):
+    ctor = boss.IBOSSChunkConstructor.initialize(k, both_strands=canonical, bits_per_count=bits, **kw)
+    if counts is None:
+        ctor.add_sequences(seqs)
+    else:
+        ctor.add_sequences(list(zip(seqs, counts)))
+    got = ctor.build_chunk()
+    return got, ctor.timings()
+
+
+def _check(k, seqs, canonical, bits, counts=None, **kw):
+    got, t = _build(k, seqs, canonical, bits, counts, **kw)
+    want = O.build_chunk(k, seqs, canonical=canonical, bits_per_count=bits, counts=counts)
+    assert_same(got, want, "k=%d canonical=%s bits=%d" % (k, canonical, bits))
+    return got, t
+
+
+@pytest.fixture
+def small_fused(monkeypatch):
+    # the fused K1 (and so the rounds) on inputs below its default 4 M-window threshold
+    monkeypatch.setenv("MTG_FUSED_MIN", "0")
+    return monkeypatch
+
+
+@pytest.mark.parametrize("rounds", [2, 3, 7])
+@pytest.mark.parametrize("k", [6, 11, 12, 20, 30, 31])
+def test_rounds_random_reads(small_fused, rounds, k):
+    # k = 11 / 31 (even K = k + 1): palindromes drop out of the rc set, doubling their counts
+    small_fused.setenv("MTG_RANGES", str(rounds))
+    reads = _random_reads(2000 + k, 400, 150, 5000, n_rate=0.005, lower=True)
+    for canonical in (False, True):
+        for bits in (0, 8):
+            _, t = _check(k, reads, canonical, bits)
+            assert t.collect_mode == ROUNDS and t.n_batches == rounds, (t.collect_mode, t.n_batches)
+
+
+def test_rounds_counts_saturate(small_fused):
+    small_fused.setenv("MTG_RANGES", "4")
+    rng = np.random.default_rng(18)
+    seqs = _random_reads(19, 300, 60, 2000)
+    counts = rng.integers(1, 400, size=len(seqs)).tolist()
+    for bits in (4, 8, 16, 32):
+        for canonical in (False, True):
+            _, t = _check(15, seqs, canonical, bits, counts)
+            assert t.collect_mode == ROUNDS
+
+
+def test_rounds_transcripts_goldens(small_fused, transcripts_1000):
+    small_fused.setenv("MTG_RANGES", "5")
+    for canonical, nodes in ((False, 591997), (True, 1159851)):
+        got, t = _check(19, transcripts_1000, canonical, 8)
+        assert got.n_real == nodes and t.collect_mode == ROUNDS and t.n_batches == 5
+
+
+def test_rounds_memory_budget_plans(small_fused, transcripts_1000):
+    # a 16 MB budget cannot hold the one-pass build of 1.5 M u64 windows: the build plans its rounds
+    got, t = _check(30, transcripts_1000, True, 0, memory_preallocated=16e6)
+    assert t.collect_mode == ROUNDS and t.n_batches >= 2, (t.collect_mode, t.n_batches)
+    got2, t2 = _check(30, transcripts_1000, True, 0)
+    assert t2.n_batches == 1 and t2.collect_mode == 0 and np.array_equal(got.W, got2.W)
+
+
+def test_range_scan_knob(small_fused, transcripts_1000):
+    # MTG_COLLECT=ranges keeps the key-range collect (both strands, re-scanned reads) for the same input
+    small_fused.setenv("MTG_RANGES", "3")
+    small_fused.setenv("MTG_COLLECT", "ranges")
+    _, t = _check(30, transcripts_1000, True, 8)
+    assert t.collect_mode == 1 and t.n_batches == 3
+
+
+# 2 M genome-sampled reads at k = 31 (the bench generator): a 2-level plan whose speculative final
+# level runs in every round, then the speculative rc level of the fused merge over the whole
+# canonical set; basic mode and counts take the other branches
+@pytest.mark.parametrize("canonical,bits", [(True, 0), (False, 0), (True, 8)])
+def test_rounds_bench_generator_2m(monkeypatch, canonical, bits):
+    monkeypatch.setenv("MTG_RANGES", "3")
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=canonical, bits_per_count=bits, num_threads=8)
+    ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)
+    got = ctor.build_chunk()
+    t = ctor.timings()
+    assert t.collect_mode == ROUNDS and t.n_batches == 3
+    assert t.n_extracted == 2_000_000 * 120
+    if not bits:
+        assert t.spec_levels >= 3 and t.spec_fallbacks == 0, (t.spec_levels, t.spec_fallbacks)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=bits)
+    assert_same(got, want, "2M reads k=31 canonical=%s bits=%d, 3 rounds" % (canonical, bits))
+
+
+# configs[3]'s shape at a size the oracle finishes: 20 M genome-sampled reads (2.4e9 windows) under a
+# memory_preallocated budget that the DEFAULT planner answers with rounds (no MTG_RANGES), the
+# device path's arrays bit for bit against the oracle (~70 s of oracle time on the box's 16 threads)
+@pytest.mark.timeout(900)
+def test_rounds_20m_reads_memory_planned_vs_oracle():
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n_reads, L = 20_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, memory_preallocated=3.5e10)
+    dc = ctor.build_device(seq.data_ptr(), seq.numel())
+    t = ctor.timings()
+    assert t.collect_mode == ROUNDS and t.n_batches >= 2, (t.collect_mode, t.n_batches)
+    assert t.n_extracted == n_reads * (L - 31 + 1)
+    L_ = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    last = np.empty(dc.n, dtype=np.uint8)
+    assert L_.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n) == 0
+    assert L_.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n) == 0
+    F = np.array([int(f) for f in dc.F], dtype=np.uint64)
+    n_real = dc.n_real
+    del ctor
+    host = seq.cpu().numpy()
+    del seq
+    want = O.build_chunk_packed(30, host, np.arange(n_reads + 1, dtype=np.uint64) * (L + 1), canonical=True)
+    assert len(W) == len(want.W)
+    assert np.array_equal(W, want.W) and np.array_equal(last, want.last)
+    assert np.array_equal(F, want.F) and n_real == want.n_real
