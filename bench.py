@@ -267,12 +267,12 @@ def kmc_path(args, kb, boss, kmc_base, steps, n_records):
         dt = time.perf_counter() - t0
         t = ctor.timings()
         if it:
-            rows.append((dt, t1 - t0, t.input_ms, t.total_ms, t.d2h_ms))
+            rows.append((dt, t1 - t0, t.input_ms, t.total_ms, t.d2h_ms, t.host_total_ms))
         del ch
-    m = [sum(r[i] for r in rows) / len(rows) for i in range(5)]
+    m = [sum(r[i] for r in rows) / len(rows) for i in range(6)]
     return {"value": n_records / m[0], "unit": "k-mers/s", "ms_per_step": m[0] * 1e3,
             "stages_ms": {"read_files": m[1] * 1e3, "h2d_and_decode_on_device": m[2],
-                          "device_path": m[3], "d2h_W_last_weights": m[4]},
+                          "device_path": m[3], "d2h_W_last_weights": m[4], "build_chunk_call": m[5]},
             "steps": steps, "what": "add_kmc + build_chunk through the C ABI, host arrays out"}
 
 

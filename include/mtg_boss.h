@@ -145,6 +145,7 @@ typedef struct mtg_boss_timings {
     uint64_t spec_fallbacks;     /* speculative levels that overflowed and reran as the exact level */
     uint64_t collect_mode;       /* how the real k-mers were collected: 0 one pass, 1 key ranges re-scanning
                                     the reads (both strands), 2 canonical rounds of the fused extraction */
+    uint64_t sent_bytes;         /* multi-GPU: bytes this rank sent to the other ranks (every exchange) */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);

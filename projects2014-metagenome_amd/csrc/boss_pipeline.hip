@@ -65,7 +65,7 @@ class Workspace {
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
-        FUSED_SEL, NSLOTS
+        FUSED_SEL, WN, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -191,6 +191,8 @@ struct Ctx {
     bool routed_min = false;       // MTG_ROUTED_CANON=min: the routed collect keeps min(fwd, rc)
     int dist_collect = 1;          // MTG_DIST_COLLECT: 1 routed keys (default), 0 super-k-mers
                                    // (=superkmer), 2 local collect + exchange of sorted runs (=local)
+    unsigned fused_b1 = 0;         // MTG_FUSED_B1=n: the fused K1's level-1 digit forced to n bits (A/B runs)
+    bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
     bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
                                    // that re-scan the reads (both strands) even where the canonical
                                    // rounds of the fused K1 apply (collect_rounds_fused)
@@ -252,6 +254,8 @@ static void load_knobs(Ctx &c) {
     c.fused_emit = !is("MTG_FUSED_EMIT", "0");
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
     c.range_scan = is("MTG_COLLECT", "ranges");
+    c.wide_b1 = !is("MTG_WIDE_B1", "0");
+    if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
     c.spec_final = !is("MTG_SPEC", "0");
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
@@ -1229,6 +1233,26 @@ static bool stage_extract_windows(Ctx &c, unsigned K, bool canonical, uint32_t c
     return true;
 }
 
+// The MSD plan of a fused K1's input.  Its level 1 is pass B's digit, which the VALU-bound pass B
+// can take 10 bits wide (extract_partition_fast_kernel<512, 1024>: 8-key runs, its writes hidden
+// behind the extraction): a plan of 19 bits -- ~2e9 k-mers, 15-20 M reads -- then runs 10 + 9
+// instead of 6 + 6 + 7, one stand-alone partition pass instead of two.  `fast`: the uncounted pass
+// B (the counted one keeps <= 9 bits).
+static MsdPlan fused_plan(const Ctx &c, uint64_t N, unsigned nbits, double dup, bool fast) {
+    MsdPlan p = msd_plan<1>(c, N, nbits, dup);
+    if (!p.levels || !fast) return p;
+    const unsigned T = p.digit_end[p.levels];
+    unsigned b1 = 0;
+    if (c.fused_b1) b1 = std::min(c.fused_b1, T);
+    else if (c.wide_b1 && p.levels == 3 && !c.min_levels && T <= 10 + MSD_DBITS) b1 = 10;
+    if (!b1) return p;
+    MsdPlan q{};
+    q.levels = 1 + (T - b1 + MSD_DBITS - 1) / MSD_DBITS;
+    q.digit_end[1] = b1;
+    for (unsigned l = 2; l <= q.levels; ++l) q.digit_end[l] = b1 + (T - b1) * (l - 1) / (q.levels - 1);
+    return q;
+}
+
 // K1 fused with K2's first partition level (extract_partition.hpp), for 2-bit u64 keys on
 // inputs big enough to have one: pass A (fused_pass_a, the histogram of the top FUSED_HB bits of
 // every k-mer) then pass B (fused_pass_b, the k-mers scattered by their level-1 digit).
@@ -1358,10 +1382,16 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     const bool fast_b = !COUNTED && K <= 32;
     if (fast_b) {
         constexpr int B = 512;
-        extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(A.npos, 16 * B))), dim3(B), 0,
-                                            c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe,
-                                                        scur, send, ka, &c.small->error, dsel);
+        if (b1 > 9)
+            extract_partition_fast_kernel<B, 1024><<<dim3((unsigned)xcd_grid(ceil_div(A.npos, 16 * B))), dim3(B), 0,
+                                                      c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1,
+                                                                  A.per_stripe, scur, send, ka, &c.small->error, dsel);
+        else
+            extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(A.npos, 16 * B))), dim3(B), 0,
+                                                c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe,
+                                                            scur, send, ka, &c.small->error, dsel);
     } else {
+        if (b1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, 512>::TILE);
         extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
             in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
@@ -1383,7 +1413,7 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
 template <int L2, bool COUNTED>
 static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                                 Key<L2> **ka, Key<L2> **kb, uint32_t **ca, uint32_t **cb, uint64_t *N_out,
-                                double *dup_out, const uint32_t **hist1_out) {
+                                double *dup_out, const uint32_t **hist1_out, MsdPlan *plan_out) {
     if constexpr (L2 != 1) {
         return false;
     } else {
@@ -1392,7 +1422,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         FusedA A;
         fused_pass_a(c, K, canonical, in, &A);
         const uint64_t N = A.N;
-        const MsdPlan plan = msd_plan<1>(c, N, 2 * K, A.dup);
+        const MsdPlan plan = fused_plan(c, N, 2 * K, A.dup, !COUNTED && K <= 32);
         if (c.debug)
             fprintf(stderr, "[mtg debug] fused extract N=%lu dup=%.2f levels=%u digit1=%u\n", (unsigned long)N, A.dup,
                     plan.levels, plan.levels ? plan.digit_end[1] : 0);
@@ -1407,6 +1437,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         c.timings.n_extracted = N;
         *N_out = N;
         *dup_out = A.dup;
+        *plan_out = plan;  // the sort runs this plan (its level 1 is pass B's digit)
         return true;
     }
 }
@@ -1416,7 +1447,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
 template <int L2, bool COUNTED>
 static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, Key<L2> **kb,
                               uint32_t **ca, uint32_t **cb, uint64_t N, double dup, bool track,
-                              const uint32_t *hist1 = nullptr) {
+                              const uint32_t *hist1 = nullptr, const MsdPlan *plan = nullptr) {
     // hist1 != nullptr: *ka is already scattered by the level-1 digit (stage_extract_fused)
     uint64_t U = 0;
     if (c.use_lsd) {
@@ -1447,7 +1478,7 @@ static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, K
         c.track_partition = track;
         if (dup <= 0) dup = estimate_dup<L2>(c, *ka, N, 8.0);
         U = msd_sort_unique<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, cmax, dup, hist1, false, nullptr,
-                                         hist1 != nullptr);
+                                         hist1 != nullptr, nullptr, hist1 ? plan : nullptr);
         c.track_partition = false;
     }
     return U;
@@ -1600,7 +1631,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     FusedA A;
     fused_pass_a(c, K, canonical, in, &A);
     const uint64_t N = A.N;
-    const MsdPlan plan = msd_plan<1>(c, N, 2 * K, A.dup);
+    const MsdPlan plan = fused_plan(c, N, 2 * K, A.dup, !COUNTED && K <= 32);
     if (!plan.levels) return false;
     const unsigned b1 = plan.digit_end[1];
     const uint32_t nb1 = 1u << b1;
@@ -2057,6 +2088,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     uint64_t N = 0;
     double dup = 0;
     const uint32_t *hist1 = nullptr;
+    MsdPlan fplan{};
     c.radix_ms = 0;
     c.radix_bytes = 0;
     c.radix_launches = 0;
@@ -2088,14 +2120,15 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     } else {
     if (stage_extract_windows<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N))
         dup = 1.0;  // one k-mer per record: distinct up to a strand
-    else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+    else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb, &N, &dup, &hist1,
+                                                &fplan))
         N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &kb, &ca, &cb);
     ev_extract = tm.mark();
 
     // ---- K2 sort + K3 unique / saturating count merge (ka)
     c.want_gidx = canonical;  // the fused rc merge reads the canonical keys' bucket index
     c.defer_gather_req = canonical;  // ... and may read them in their speculative buckets (Ctx::gap)
-    U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
+    U = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1, &fplan);
     c.defer_gather_req = false;
     c.want_gidx = false;
     ev_sort = tm.mark();
@@ -2573,6 +2606,19 @@ static bool routed_applies(const Ctx &c, unsigned K) {
     return c.fused && !c.use_lsd && K - 1 >= FUSED_HB / 2 && K <= 32 && !c.range_scan;
 }
 
+// one-window reads (KMC input) on every rank: cheaper through window_reads_kernel and the local
+// collect than through the routed one.  Collective: the ranks share their layouts by an all-reduce.
+static bool dist_window_input(Ctx &c, Dist &d, unsigned K, const BuildInput &in) {
+    uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, 8);
+    const uint64_t win = window_layout(c, K, in) || in.seq_len == 0 ? 0 : 1;
+    HIP_CHECK(hipMemcpyAsync(dv, &win, 8, hipMemcpyHostToDevice, c.stream));
+    d.comm.allreduce_sum_u64(dv, 1, c.stream);
+    uint64_t any_other = 0;
+    HIP_CHECK(hipMemcpyAsync(&any_other, dv, 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // `win` is a host local
+    return any_other == 0;
+}
+
 template <bool COUNTED>
 static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                                 Key<1> **xa_out, uint32_t **xac_out, uint64_t *U_out, std::vector<uint64_t> *bounds,
@@ -2580,18 +2626,6 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     using K2 = Key<1>;
     // the same on every rank (no input-size test: a rank may hold no reads)
     if (!routed_applies(c, K)) return false;
-    // one-window reads (KMC input) are cheaper through window_reads_kernel and the local collect; the
-    // decision must agree on every rank, so a rank's layout is shared by an all-reduce
-    {
-        uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, 8);
-        const uint64_t win = window_layout(c, K, in) || in.seq_len == 0 ? 0 : 1;
-        HIP_CHECK(hipMemcpyAsync(dv, &win, 8, hipMemcpyHostToDevice, c.stream));
-        d.comm.allreduce_sum_u64(dv, 1, c.stream);
-        uint64_t any_other = 0;
-        HIP_CHECK(hipMemcpyAsync(&any_other, dv, 8, hipMemcpyDeviceToHost, c.stream));
-        HIP_CHECK(hipStreamSynchronize(c.stream));  // `win` is a host local
-        if (!any_other) return false;
-    }
     constexpr unsigned OB = 8;   // owner-range prefix bits (4 node chars: whole chars for the lifted bounds)
     // canonical windows keep the strand whose key top hashes smaller (boss_kernels.hpp: take_rc): the
     // owners' canonical keys then follow the real edges, and one set of ranges balances both
@@ -2999,6 +3033,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     EventTimer tm(c.stream);
     const int ev_start = tm.mark();
     Dist d{comm, comm.size(), comm.rank(), 0, 0, 1, &tm, {}};
+    const uint64_t sent0 = comm.sent_bytes;
     if (d.P > MAX_RANKS) throw std::runtime_error("more ranks than the routing kernels support");
     T.world = (uint64_t)d.P;
     T.n_batches = 1;
@@ -3018,7 +3053,8 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     std::vector<uint64_t> bounds;
     // the routed collect plans its own rounds (canonical k-mers of the fused K1); the other collects
     // batch in key ranges that re-scan the reads
-    const bool routed_try = L2 == 1 && c.dist_collect == 1 && !c.disk && routed_applies(c, K);
+    bool routed_try = L2 == 1 && c.dist_collect != 2 && !c.disk && routed_applies(c, K);
+    if (routed_try) routed_try = !dist_window_input(c, d, K, in);
     const uint32_t rounds = routed_try ? 1 : plan_rounds_dist<L2, COUNTED>(c, d, K, canonical, in);
     if (rounds > 1) {
         T.collect_mode = 1;
@@ -3040,7 +3076,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         BuildInput sk_in{};
         const bool sk = dist_superkmers(c, d, K, canonical, in, &sk_in, tr);
         if constexpr (L2 == 1)  // the fused extraction routes every k-mer to its owner
-            if (!sk && c.dist_collect != 2)
+            if (!sk && routed_try)
                 routed = dist_collect_routed<COUNTED>(c, d, K, canonical, cmax, in, &xa, &xac, &T.n_unique, &b1, tr, tm,
                                                       &ev_extract, &ev_sort);
         if (!routed) {
@@ -3051,16 +3087,18 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         uint64_t N = 0;
         double dup = 0;
         const uint32_t *hist1 = nullptr;
+        MsdPlan fplan{};
         if (stage_extract_windows<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N))
             dup = 1.0;
-        else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N, &dup, &hist1))
+        else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N, &dup, &hist1,
+                                                    &fplan))
             N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb);
         if (sk) {  // the windows of this rank's reads, not of the received runs
             T.n_positions = in.seq_len >= K ? in.seq_len - K + 1 : 0;
         }
         ev_extract = tm.mark();
         tr("extract", N);
-        const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1);
+        const uint64_t Ul = stage_collect<L2, COUNTED>(c, K, cmax, &ka, &kb, &ca, &cb, N, dup, true, hist1, &fplan);
         ev_sort = tm.mark();
         tr("local collect", Ul);
 
@@ -3320,6 +3358,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     T.emit_ms = tm.ms(ev_merge, ev_emit);
     T.total_ms = tm.ms(ev_start, ev_emit);
     for (auto &p : d.xev) T.exchange_ms += tm.ms(p.first, p.second);
+    T.sent_bytes = comm.sent_bytes - sent0;
     T.radix_launches = c.radix_launches;
     T.radix_pass_ms = c.radix_launches ? c.radix_ms / c.radix_launches : 0;
     T.radix_bytes = c.radix_launches ? c.radix_bytes / c.radix_launches : 0;
@@ -3415,8 +3454,8 @@ class NoComm : public Comm {
     explicit NoComm(int P) : Comm(0, P) {}
     void allreduce_sum_u64(uint64_t *, size_t, hipStream_t) override { fail(); }
     void allgather_u64(const uint64_t *, uint64_t *, size_t, hipStream_t) override { fail(); }
-    void alltoallv(const void *, const uint64_t *, const uint64_t *, void *, const uint64_t *, const uint64_t *,
-                   size_t, hipStream_t) override {
+    void alltoallv_impl(const void *, const uint64_t *, const uint64_t *, void *, const uint64_t *, const uint64_t *,
+                        size_t, hipStream_t) override {
         fail();
     }
 
@@ -3921,9 +3960,12 @@ struct mtg_boss_ctor {
     std::vector<mtg::FastaInput> fasta;  // FASTA / FASTQ files, split into reads on the device
     uint8_t *w4_host = nullptr;          // pinned landing buffer of the 4-bit W copy
     uint64_t w4_cap = 0;
+    uint8_t *wn_host = nullptr;          // pinned landing buffer of the narrowed weights copy
+    uint64_t wn_cap = 0;
     ~mtg_boss_ctor() {
         for (auto &f : fasta) mtg::free_fasta(f);
         if (w4_host) (void)hipHostFree(w4_host);
+        if (wn_host) (void)hipHostFree(wn_host);
     }
 };
 
@@ -4397,6 +4439,94 @@ static void copy_w_to_host(mtg_boss_ctor *c, const uint8_t *dW, uint64_t n, uint
     if (failed) throw std::runtime_error("W copy to the host failed");
 }
 
+// u32 weights (already clamped to the count width) -> `bytes` (1 or 2) per weight, 16 weights a thread
+__global__ void narrow_weights_kernel(const uint32_t *__restrict__ w, uint64_t n, unsigned bytes,
+                                      uint8_t *__restrict__ out) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i0 >= n) return;
+    if (i0 + 16 <= n) {
+        const uint4 *src = (const uint4 *)(w + i0);
+        uint32_t v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 a = src[q];
+            v[4 * q] = a.x, v[4 * q + 1] = a.y, v[4 * q + 2] = a.z, v[4 * q + 3] = a.w;
+        }
+        if (bytes == 1) {
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                o[q] = (v[4 * q] & 0xFF) | (v[4 * q + 1] & 0xFF) << 8 | (v[4 * q + 2] & 0xFF) << 16 | v[4 * q + 3] << 24;
+            *(uint4 *)(out + i0) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            uint32_t o[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = (v[2 * q] & 0xFFFF) | v[2 * q + 1] << 16;
+            *(uint4 *)(out + 2 * i0) = make_uint4(o[0], o[1], o[2], o[3]);
+            *(uint4 *)(out + 2 * i0 + 16) = make_uint4(o[4], o[5], o[6], o[7]);
+        }
+        return;
+    }
+    for (uint64_t i = i0; i < n; ++i) {
+        out[bytes * i] = (uint8_t)w[i];
+        if (bytes == 2) out[2 * i + 1] = (uint8_t)(w[i] >> 8);
+    }
+}
+
+// weights[0..n) (u32) on the device -> the host's u32 array: for count widths <= 16 bits they cross
+// PCIe as 1 or 2 bytes a weight (configs[4]'s 8-bit weights: 1.5 GB -> 0.39 GB), in 16 MiB pieces
+// that the host threads widen as they land
+static void copy_weights_to_host(mtg_boss_ctor *c, const uint32_t *dwt, uint64_t n, unsigned bits, uint32_t *out) {
+    if (!n) return;
+    hipStream_t s = c->ctx.stream;
+    const unsigned bytes = bits <= 8 ? 1 : bits <= 16 ? 2 : 4;
+    if (bytes == 4 || n < (16ull << 20)) {
+        HIP_CHECK(hipMemcpyAsync(out, dwt, n * 4, hipMemcpyDeviceToHost, s));
+        return;
+    }
+    const uint64_t nb = n * bytes;
+    uint8_t *dn = (uint8_t *)c->ctx.ws.get(Workspace::WN, nb + 64);
+    narrow_weights_kernel<<<dim3((unsigned)ceil_div(ceil_div(n, 16), 256)), dim3(256), 0, s>>>(dwt, n, bytes, dn);
+    HIP_CHECK(hipGetLastError());
+    if (c->wn_cap < nb + 64) {  // the ctor's pinned landing buffer, grown on demand
+        if (c->wn_host) (void)hipHostFree(c->wn_host);
+        c->wn_host = nullptr;
+        c->wn_cap = 0;
+        HIP_CHECK(hipHostMalloc((void **)&c->wn_host, nb + nb / 4 + 64, hipHostMallocDefault));
+        c->wn_cap = nb + nb / 4 + 64;
+    }
+    uint8_t *hn = c->wn_host;
+    constexpr uint64_t PIECE = 16ull << 20;  // narrowed bytes per piece (a multiple of 2)
+    const uint64_t np = ceil_div(nb, PIECE);
+    std::vector<hipEvent_t> ev(np);
+    for (uint64_t p = 0; p < np; ++p) {
+        const uint64_t b0 = p * PIECE, len = std::min(PIECE, nb - b0);
+        HIP_CHECK(hipEventCreateWithFlags(&ev[p], hipEventDisableTiming));
+        HIP_CHECK(hipMemcpyAsync(hn + b0, dn + b0, len, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipEventRecord(ev[p], s));
+    }
+    const unsigned T = std::max(1u, std::min<unsigned>(stage_threads(c), (unsigned)np));
+    std::atomic<bool> failed{false};
+    parallel_ranges(T, T, 1, [&](uint64_t t0, uint64_t t1) {
+        DeviceGuard g(c->device);
+        for (uint64_t t = t0; t < t1; ++t)
+            for (uint64_t p = t; p < np; p += T) {
+                if (hipEventSynchronize(ev[p]) != hipSuccess) {
+                    failed = true;
+                    return;
+                }
+                const uint64_t b0 = p * PIECE, len = std::min(PIECE, nb - b0);
+                const uint64_t w0 = b0 / bytes, wn = len / bytes;
+                if (bytes == 1)
+                    for (uint64_t i = 0; i < wn; ++i) out[w0 + i] = hn[b0 + i];
+                else
+                    for (uint64_t i = 0; i < wn; ++i) out[w0 + i] = (uint32_t)hn[b0 + 2 * i] | (uint32_t)hn[b0 + 2 * i + 1] << 8;
+            }
+    });
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (failed) throw std::runtime_error("weights copy to the host failed");
+}
+
 // build_chunk on the staged reads: one H2D copy of the pinned read buffer (+ KMC records), the
 // device path, then W / packed last / weights D2H into pinned blocks the chunk owns
 static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *out) {
@@ -4543,11 +4673,11 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         out->W = (uint8_t *)pool.take(o.n);
         out->last = (uint64_t *)pool.take(std::max<uint64_t>(nwords, 1) * 8);
         HIP_CHECK(hipMemcpyAsync(out->last, dbits, nwords * 8, hipMemcpyDeviceToHost, s));
+        copy_w_to_host(c, o.W, o.n, out->W);
         if (o.weights) {
             out->weights = (uint32_t *)pool.take(o.n * 4);
-            HIP_CHECK(hipMemcpyAsync(out->weights, o.weights, o.n * 4, hipMemcpyDeviceToHost, s));
+            copy_weights_to_host(c, o.weights, o.n, c->params.bits_per_count, out->weights);
         }
-        copy_w_to_host(c, o.W, o.n, out->W);
         HIP_CHECK(hipStreamSynchronize(s));
         mtg_boss_timings &T = c->ctx.timings;
         T.d2h_ms = ms_since(t_d2h);

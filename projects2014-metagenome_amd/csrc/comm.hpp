@@ -44,10 +44,16 @@ class Comm {
     // d_recv[r * n + i] = rank r's d_send[i]
     virtual void allgather_u64(const uint64_t *d_send, uint64_t *d_recv, size_t n, hipStream_t s) = 0;
     // rank j receives scnt[j] elements from d_send + soff[j] (element units, host arrays of P);
-    // the elements from rank i land at d_recv + roff[i]
-    virtual void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff,
-                           void *d_recv, const uint64_t *rcnt, const uint64_t *roff, size_t esz,
-                           hipStream_t s) = 0;
+    // the elements from rank i land at d_recv + roff[i]; counts the bytes that leave this rank
+    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv, const uint64_t *rcnt,
+                   const uint64_t *roff, size_t esz, hipStream_t s) {
+        for (int j = 0; j < size_; ++j)
+            if (j != rank_) sent_bytes += scnt[j] * esz;
+        alltoallv_impl(d_send, scnt, soff, d_recv, rcnt, roff, esz, s);
+    }
+    uint64_t sent_bytes = 0;  // bytes this rank sent to others through alltoallv
+    virtual void alltoallv_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                                const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) = 0;
     // a build's device work starts / ends on stream s (LocalComm's serial mode hands the device over)
     virtual void begin_build(hipStream_t) {}
     virtual void end_build(hipStream_t) {}
@@ -126,7 +132,7 @@ class RcclComm : public Comm {
     void allgather_u64(const uint64_t *d_send, uint64_t *d_recv, size_t n, hipStream_t s) override {
         RCCL_CHECK(RcclApi::get().AllGather(d_send, d_recv, n, ncclUint64, comm_, s));
     }
-    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+    void alltoallv_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
                    const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
         const RcclApi &api = RcclApi::get();
         // messages go out in pieces of at most 1 GiB (counts are size_t, but bounded pieces keep
@@ -191,7 +197,7 @@ class CallbackComm : public Comm {
         COMM_HIP(hipMemcpyAsync(d_recv, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
         COMM_HIP(hipStreamSynchronize(s));
     }
-    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+    void alltoallv_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
                    const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
         std::vector<uint64_t> sb(size_), rb(size_);
         uint64_t st = 0, rt = 0;
@@ -319,7 +325,7 @@ class LocalComm : public Comm {
         COMM_HIP(hipMemcpyAsync(d_recv, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
         COMM_HIP(hipStreamSynchronize(s));
     }
-    void alltoallv(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+    void alltoallv_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
                    const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
         COMM_HIP(hipStreamSynchronize(s));  // the send buffer is complete before peers read it
         auto &slot = g_->slots[rank_];

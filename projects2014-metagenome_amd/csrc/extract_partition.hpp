@@ -18,7 +18,7 @@
 namespace mtg {
 
 constexpr unsigned FUSED_HB = 12;  // histogram bits of pass A (>= any level-1 digit)
-constexpr uint32_t FUSED_SEL_WORDS = 16;  // a level-1 bucket mask of a collect round (<= 512 buckets)
+constexpr uint32_t FUSED_SEL_WORDS = 32;  // a level-1 bucket mask of a collect round (<= 1024 buckets)
 
 // Stage a tile's read bytes as 2-bit codes (4 = invalid) in LDS: one dword load, four encodes and
 // one dword LDS store per thread step when the bytes are 4-aligned, byte loads for the tail.
@@ -283,21 +283,26 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
 // complement by sliding one char a window, validity from the invalid-char mask -- no per-window
 // LDS reads and no per-window branches.  Same k-mers as slide_windows (forward and rc plain words,
 // plain_to_boss, rc < fwd picks rc), so the same output as extract_partition_kernel<false>.
-template <int BLOCK>
+// NB: the widest digit's bucket count (1024: a 10-bit level 1, so that inputs of ~2e9 k-mers keep a
+// 2-level plan).  The bucket counts live in the run-base array until the scan has read them, and the
+// in-tile offsets are u16, so NB = 1024 still fits two workgroups per CU (78 KB of LDS).
+template <int BLOCK, int NB = 512>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
     Key<1> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
-    constexpr int NBMAX = 512;
+    constexpr int NBMAX = NB;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
+    static_assert(TILE <= 65536, "u16 in-tile offsets");
     __shared__ uint32_t s_pack[NW];
     __shared__ uint32_t s_inv[NW];
     __shared__ uint64_t s_keys[TILE];
-    __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
-    __shared__ unsigned long long s_gbase[NBMAX];
+    __shared__ unsigned long long s_gbase[NBMAX];  // the run bases; first the u32 bucket counts (s_cnt)
+    __shared__ uint16_t s_off[NBMAX];              // the buckets' offsets in the tile
     __shared__ uint32_t s_scan[BLOCK / 64 + 1];
     __shared__ uint32_t s_sel[FUSED_SEL_WORDS];
+    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_gbase);
 
     const uint32_t tid = threadIdx.x;
     const uint32_t nb = 1u << b;
@@ -393,12 +398,12 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     }
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
-    __syncthreads();  // every count is read before the offsets overwrite them
+    __syncthreads();  // every count is read before the run bases overwrite them
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
         if (i < nb) {
-            s_cnt[i] = off;
+            s_off[i] = (uint16_t)off;
             const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
             unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
             if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
@@ -412,13 +417,13 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PPT; ++j)
-        if (m & (1u << j)) s_keys[s_cnt[(uint32_t)(kk[j] >> bshift)] + r[j]] = kk[j];
+        if (m & (1u << j)) s_keys[s_off[(uint32_t)(kk[j] >> bshift)] + r[j]] = kk[j];
     __syncthreads();
     for (uint32_t p = tid; p < total; p += BLOCK) {
         const uint64_t key = s_keys[p];
         const uint32_t lb = (uint32_t)(key >> bshift);
         if (s_gbase[lb] == ~0ull) continue;
-        kout[s_gbase[lb] + (p - s_cnt[lb])].w[0] = key;
+        kout[s_gbase[lb] + (p - s_off[lb])].w[0] = key;
     }
 }
 

@@ -51,7 +51,8 @@ def _assert_same(got, want, ctx):
     assert got.n_real == want.n_real, ctx
 
 
-@pytest.mark.parametrize("canonical,bits", [(True, 0), (False, 8)])
+# (the counted builds' ~5e7 weights cross PCIe narrowed to 1 or 2 bytes: copy_weights_to_host)
+@pytest.mark.parametrize("canonical,bits", [(True, 0), (False, 8), (True, 16)])
 def test_bench_generator_2m_reads_k31(canonical, bits):
     asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
     got, t = _gpu_build(30, asc, canonical, bits)
@@ -95,6 +96,19 @@ def test_bench_generator_three_msd_levels(monkeypatch, canonical, spec3):
     reads = [asc[i].tobytes() for i in range(len(asc))]
     want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=0)
     _assert_same(got, want, "2M reads k=31 canonical=%s, 3 MSD levels, MTG_SPEC3=%s" % (canonical, spec3))
+
+
+@pytest.mark.parametrize("canonical", [False, True])
+def test_bench_generator_wide_level1(monkeypatch, canonical):
+    # pass B's 10-bit level-1 digit (extract_partition_fast_kernel<512, 1024>; inputs of ~2e9 k-mers plan
+    # 10 + 9 bits instead of 3 levels), forced on 2 M reads: 10 + 6 bits, the speculative level 2 below it
+    monkeypatch.setenv("MTG_FUSED_B1", "10")
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    got, t = _gpu_build(30, asc, canonical, 0)
+    assert t.spec_levels >= 1 and t.spec_fallbacks == 0, (t.spec_levels, t.spec_fallbacks)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=0)
+    _assert_same(got, want, "2M reads k=31 canonical=%s, 10-bit level 1" % canonical)
 
 
 @pytest.mark.parametrize("levels", ["2", "3"])

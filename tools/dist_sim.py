@@ -32,6 +32,8 @@ def main():
                     help="one rank owns the device at a time (MTG_LOCAL_SERIAL): the step is the SUM of the "
                          "ranks' work, and each rank's device time is measured alone")
     ap.add_argument("--only-single", action="store_true", help="the single build only (its kernel profile)")
+    ap.add_argument("--collect", default=None, choices=["routed", "superkmer", "local"],
+                    help="the multi-GPU collect (MTG_DIST_COLLECT; default: the library's)")
     args = ap.parse_args()
     import torch
     boss = importlib.import_module("projects2014-metagenome_amd.boss")
@@ -59,6 +61,8 @@ def main():
 
     if args.serial:
         os.environ["MTG_LOCAL_SERIAL"] = "1"
+    if args.collect and args.collect != "routed":
+        os.environ["MTG_DIST_COLLECT"] = args.collect
     comms = boss.Comm.local_group(P)
     ctors = [boss.IBOSSChunkConstructor.initialize(kb, both_strands=True) for _ in range(P)]
     res = [None] * P
@@ -98,6 +102,7 @@ def main():
         "single_stages": {k: round(ts[k], 2) for k in keys if k in ts},
         "rank_stages": [{k: round(t[k], 2) for k in keys} for t in per_rank],
         "n_sent": [t["n_sent"] for t in per_rank],
+        "sent_bytes": [t["sent_bytes"] for t in per_rank],
         "n_real": [t["n_real"] for t in per_rank],
     }, indent=1))
 

@@ -1,13 +1,18 @@
 #!/bin/bash
-# Round 4: canonical key rounds (single + routed multi-GPU), pinned KMC reads -- parity tests, the
-# configs[3]-share and configs[4] bench lines, kernel stats of the configs[3] share.
+# Round 4: canonical key rounds (single + routed multi-GPU), pinned KMC reads, the 10-bit level 1 --
+# parity tests, the 20 M-read single build A/B (wide level 1), the configs[3]-share and configs[4]
+# bench lines, kernel stats of the configs[3] share.
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/r4c; mkdir -p $OUT
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 900 --timeout-method thread tests/test_gpu_rounds.py \
-  tests/test_gpu_dist.py -k "rounds or large_multi_tile" > $OUT/pytest.txt 2>&1
+  tests/test_gpu_dist.py tests/test_gpu_scale.py -k "rounds or large_multi_tile or wide_level1" > $OUT/pytest.txt 2>&1
 rc=$?; tail -5 $OUT/pytest.txt; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_kmc.py > $OUT/pytest_kmc.txt 2>&1
 rc=$?; tail -3 $OUT/pytest_kmc.txt; [ $rc -ne 0 ] && exit $rc
+for w in 1 0 1 0; do
+  MTG_WIDE_B1=$w timeout -k 10 300 python -u tools/dist_sim.py --ranks 2 --reads 10000000 --only-single --steps 5 >> $OUT/single20m_wide$w.txt 2>&1 || exit 1
+done
+tail -2 $OUT/single20m_wide1.txt $OUT/single20m_wide0.txt
 timeout -k 10 600 python -u bench.py --config cfg4 --no-cpu-baseline > $OUT/cfg4_bench.json 2> $OUT/cfg4_bench.err
 rc=$?; tail -3 $OUT/cfg4_bench.err; cat $OUT/cfg4_bench.json; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u bench.py --config cfg5 --no-cpu-baseline > $OUT/cfg5_bench.json 2> $OUT/cfg5_bench.err
