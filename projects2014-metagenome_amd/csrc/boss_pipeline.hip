@@ -65,7 +65,7 @@ class Workspace {
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
-        FUSED_SEL, WN, NSLOTS
+        FUSED_SEL, WN, SPEC_AC, SPEC_BC, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -518,12 +518,15 @@ static void ensure_compact(Ctx &c) {
 // one bucket per group, each group's output after the canonical keys before its bucket (cidx, the
 // canonical sort's bucket index) and the rc keys the buckets before it received.
 template <int L, bool COUNTED>
-static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbits, unsigned bp, unsigned bb,
-                                 uint32_t cmax, bool distinct, RcMerge<L> *rm, const Ctx::GroupIndex &cidx,
-                                 bool fine = false) {
-    if constexpr (L != 1 || COUNTED) {
+static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_t n, unsigned nbits, unsigned bp,
+                                 unsigned bb, uint32_t cmax, bool distinct, RcMerge<L> *rm,
+                                 const Ctx::GroupIndex &cidx, bool fine = false) {
+    // COUNTED: the counts travel with their keys (SPEC_AC / SPEC_BC) and add with saturation in the
+    // local pass, as in the exact level (configs[4]'s counted route)
+    if constexpr (L != 1) {
         return ~0ull;
     } else {
+        constexpr double KB = COUNTED ? 12.0 : 8.0;  // bytes of a key and its count
         if (distinct != (rm != nullptr)) return ~0ull;  // the plain unique, or the fused rc merge
         if (rm && !c.spec_rc) return ~0ull;
         if (rm && !(cidx.keys == (const void *)rm->ck && cidx.n == rm->nc && cidx.bits == bb && cidx.nbits == nbits &&
@@ -538,8 +541,10 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         {
             size_t fr = 0, tot = 0;
             HIP_CHECK(hipMemGetInfo(&fr, &tot));
-            if ((double)n * 8.0 * 1.4 * 2.0 > 0.5 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
-                                                   (double)c.ws.held_slot(Workspace::SPEC_B))
+            if ((double)n * KB * 1.4 * 2.0 > 0.5 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
+                                                  (double)c.ws.held_slot(Workspace::SPEC_B) +
+                                                  (double)c.ws.held_slot(Workspace::SPEC_AC) +
+                                                  (double)c.ws.held_slot(Workspace::SPEC_BC))
                 return ~0ull;
         }
         uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nb * 4);
@@ -566,9 +571,11 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         {  // the capacity is known now: both slack-sized buffers (one for the fused rc merge) must fit
             size_t fr = 0, tot = 0;
             HIP_CHECK(hipMemGetInfo(&fr, &tot));
-            const double need = (double)C * sizeof(Key<L>) * (rm ? 1.0 : 2.0);
+            const double need = (double)C * KB * (rm ? 1.0 : 2.0);
             const double have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
-                                (rm ? 0.0 : (double)c.ws.held_slot(Workspace::SPEC_B));
+                                (double)c.ws.held_slot(Workspace::SPEC_AC) +
+                                (rm ? 0.0 : (double)c.ws.held_slot(Workspace::SPEC_B) +
+                                                (double)c.ws.held_slot(Workspace::SPEC_BC));
             if (need > have) {
                 if (c.debug) fprintf(stderr, "[mtg debug] speculative level: capacity %lu does not fit, exact level\n",
                                      (unsigned long)C);
@@ -576,14 +583,15 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             }
         }
         Key<L> *sa = (Key<L> *)c.ws.get(Workspace::SPEC_A, C * sizeof(Key<L>));
+        uint32_t *sac = COUNTED ? (uint32_t *)c.ws.get(Workspace::SPEC_AC, C * 4) : nullptr;
         auto *cur = (unsigned long long *)c.ws.get(Workspace::SPEC_CUR, nb * 8);
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nb * 8, hipMemcpyDeviceToDevice, c.stream));
         HIP_CHECK(hipMemsetAsync(&c.small->spec_ovf, 0, 4, c.stream));
         EventTimer tm(c.stream);
         tm.mark();
-        msd_partition_kernel<L, false><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
-            *keys, sa, nullptr, nullptr, n, nbits, bb, bp, cur, 1, (const unsigned long long *)(bstart + 1),
-            &c.small->spec_ovf);
+        msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, sa, COUNTED ? *vals : nullptr, sac, n, nbits, bb, bp, cur, 1,
+            (const unsigned long long *)(bstart + 1), &c.small->spec_ovf);
         HIP_CHECK(hipGetLastError());
         tm.mark();
         uint32_t povf = 0;
@@ -592,7 +600,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         if (c.track_partition && c.radix_launches == 0) {
             c.radix_ms += tm.ms(0, 1);
             c.radix_launches += 1;
-            c.radix_bytes += 2.0 * n * sizeof(Key<L>);
+            c.radix_bytes += 2.0 * n * KB;
         }
         if (povf) {
             if (c.debug) fprintf(stderr, "[mtg debug] speculative level: a bucket overflowed, exact level\n");
@@ -624,8 +632,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
             const bool gapped = c.gap.valid && c.gap.dst == (const void *)rm->ck;
             const Key<L> *ck = gapped ? (const Key<L> *)c.gap.keys : rm->ck;
             const uint64_t *cgap = gapped ? c.gap.bstart : nullptr;
-            local_merge_kernel<L, false, CAP><<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(
-                sa, nullptr, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+            local_merge_kernel<L, COUNTED, CAP><<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(
+                sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
                 &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
             HIP_CHECK(hipGetLastError());
             uint32_t novf = 0;
@@ -640,8 +648,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
                 uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
                 HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-                local_merge_kernel<L, false, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
-                    sa, nullptr, bstart, nullptr, dlist, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
+                    sa, sac, bstart, nullptr, dlist, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
                     &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
                 HIP_CHECK(hipGetLastError());
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
@@ -670,18 +678,20 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         }
         // every bucket one group: [bstart[b], cur[b])
         Key<L> *sb = (Key<L> *)c.ws.get(Workspace::SPEC_B, C * sizeof(Key<L>));
+        uint32_t *sbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::SPEC_BC, C * 4) : nullptr;
         uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nb + 1) * 4);
         uint32_t *ovf = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);
         HIP_CHECK(hipMemsetAsync(ovf, 0, nb * 4, c.stream));
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
         const bool keycas = nbits < 64;
+        constexpr int WPE = COUNTED ? 1 : 8;  // (the uncounted table fits 8 waves per SIMD at 64 VGPRs)
         if (keycas)
-            local_unique_kernel<1, false, true, 512, LocalTraits<1>::SLOTS / 2, false, 8>
-                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, nullptr, bstart, nullptr, nbits, bb, 0, sb, nullptr,
+            local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE>
+                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc,
                                                                  ucount, ovf, &c.small->counter, cmax, cur);
         else
-            local_unique_kernel<1, false, false, 512, LocalTraits<1>::SLOTS / 2, false, 1>
-                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, nullptr, bstart, nullptr, nbits, bb, 0, sb, nullptr,
+            local_unique_kernel<1, COUNTED, false, 512, LocalTraits<1>::SLOTS / 2, false, 1>
+                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc,
                                                                  ucount, ovf, &c.small->counter, cmax, cur);
         HIP_CHECK(hipGetLastError());
         uint32_t novf = 0;
@@ -703,7 +713,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
                                                                               &c.small->counter, &c.small->error);
             HIP_CHECK(hipGetLastError());
         }
-        if (c.defer_gather_req && c.defer_gather && c.want_gidx) {
+        if (!COUNTED && c.defer_gather_req && c.defer_gather && c.want_gidx) {
             // the fused rc merge follows: leave the distinct keys in their buckets (Ctx::gap); the
             // compact index of bucket g is ustart[g] (one bucket per group)
             uint64_t *gb = (uint64_t *)c.ws.get(Workspace::GAP_BSTART, (nb + 1) * 8);
@@ -724,8 +734,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint64_t n, unsigned nbi
         const bool index = c.want_gidx;
         uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8) : nullptr;
         if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
-        group_gather_kernel<L, false><<<dim3((unsigned)nb), dim3(256), 0, c.stream>>>(
-            sb, nullptr, bstart, ustart, *keys, nullptr, nullptr, nbits - bb, gi, &c.small->gidx_bad);
+        group_gather_kernel<L, COUNTED><<<dim3((unsigned)nb), dim3(256), 0, c.stream>>>(
+            sb, sbc, bstart, ustart, *keys, COUNTED ? *vals : nullptr, nullptr, nbits - bb, gi, &c.small->gidx_bad);
         HIP_CHECK(hipGetLastError());
         uint64_t u = 0;
         uint32_t ibad = 0;
@@ -854,9 +864,14 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     } else {
         for (unsigned lev = 1; lev <= levels; ++lev) {
             // the last of 2 or 3 levels, the ones before it in place (3 levels: inputs over ~1.6e9 keys)
-            if (lev == levels && lev >= 2 && (lev == 2 || c.spec3) && (level1_done || (rm && distinct))) {
-                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, n, nbits, digit_end[lev - 1], digit_end[lev],
-                                                                cmax, distinct, rm, saved_gidx, lev >= 3);
+            // (any plain sort + unique too: configs[4]'s KMC records have no fused level 1)
+            if (lev == levels && lev >= 2 && (lev == 2 || c.spec3) && (level1_done || (rm && distinct) || (!rm && !distinct))) {
+                // the per-tile (fine) sample when the previous level's buckets span few tiles: 3 levels, or
+                // a 10-bit level 1 on a small input (a tile-granular sample of ~30 tiles a bucket missed
+                // by up to ~25 %)
+                const bool fine = lev >= 3 || (n >> digit_end[lev - 1]) < 64ull * MsdTraits<L>::TILE;
+                const uint64_t u = spec_final_level<L, COUNTED>(c, keys, vals, n, nbits, digit_end[lev - 1],
+                                                                digit_end[lev], cmax, distinct, rm, saved_gidx, fine);
                 if (u != ~0ull) return u;
             }
             run_level(lev);

@@ -1,14 +1,11 @@
 #!/bin/bash
-# Round 4: canonical key rounds (single + routed multi-GPU), pinned KMC reads, the 10-bit level 1 --
-# parity tests, the 20 M-read single build A/B (wide level 1), the configs[3]-share and configs[4]
-# bench lines, kernel stats of the configs[3] share.
+# Round 4: the whole -m gpu suite (rounds, wide level 1, counted speculative levels, narrowed weights,
+# pinned KMC reads), the 20 M-read single build A/B (wide level 1), the configs[3]-share and
+# configs[4] bench lines, kernel stats of the configs[3] share.
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/r4c; mkdir -p $OUT
-timeout -k 10 1000 python -u -m pytest -x -v --timeout 900 --timeout-method thread tests/test_gpu_rounds.py \
-  tests/test_gpu_dist.py tests/test_gpu_scale.py -k "rounds or large_multi_tile or wide_level1" > $OUT/pytest.txt 2>&1
-rc=$?; tail -5 $OUT/pytest.txt; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_kmc.py > $OUT/pytest_kmc.txt 2>&1
-rc=$?; tail -3 $OUT/pytest_kmc.txt; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 900 --timeout-method thread tests -m gpu > $OUT/pytest_gpu.txt 2>&1
+rc=$?; tail -5 $OUT/pytest_gpu.txt; [ $rc -ne 0 ] && exit $rc
 for w in 1 0 1 0; do
   MTG_WIDE_B1=$w timeout -k 10 300 python -u tools/dist_sim.py --ranks 2 --reads 10000000 --only-single --steps 5 >> $OUT/single20m_wide$w.txt 2>&1 || exit 1
 done
