@@ -77,7 +77,15 @@ class Workspace {
         if (b.cap < bytes) {
             void *p = nullptr;
             size_t cap = bytes + bytes / 8;
-            HIP_CHECK(hipMalloc(&p, cap));
+            if (hipMalloc(&p, cap) != hipSuccess) {
+                (void)hipGetLastError();
+                size_t fr = 0, tot = 0;
+                (void)hipMemGetInfo(&fr, &tot);
+                throw std::runtime_error("HIP error out of memory: workspace slot " + std::to_string((int)s) + " wants " +
+                                         std::to_string(cap >> 20) + " MiB (held " + std::to_string(held() >> 20) +
+                                         " MiB in all slots, this one " + std::to_string(b.cap >> 20) + " MiB; free " +
+                                         std::to_string(fr >> 20) + " MiB)");
+            }
             if (keep && b.ptr) HIP_CHECK(hipMemcpyAsync(p, b.ptr, keep, hipMemcpyDeviceToDevice, stream));
             if (b.ptr) {
                 if (keep) HIP_CHECK(hipStreamSynchronize(stream));
@@ -503,15 +511,26 @@ __global__ void spec_counts_kernel(const uint64_t *__restrict__ bstart, const un
     if (b < nb) cnt[b] = (uint32_t)(cur[b] - bstart[b]);
 }
 
+// one workgroup per bucket over buckets [lo, hi), in launches of at most 2^22 workgroups (a grid holds
+// fewer than 2^32 work-items: 2^23 buckets of 512 threads do not launch at once)
+template <typename F>
+static void bucket_pieces(uint64_t lo, uint64_t hi, F &&launch) {
+    constexpr uint64_t CH = 1ull << 22;
+    for (uint64_t g0 = lo; g0 < hi; g0 += CH) launch(g0, (unsigned)std::min(CH, hi - g0));
+}
+
 // the deferred gather of a canonical set left in bucket layout (Ctx::gap), for a consumer that reads
 // it compact
 static void ensure_compact(Ctx &c) {
     if (!c.gap.valid) return;
     c.gap.valid = false;
     if (!c.gap.nb) return;
-    group_gather_kernel<1, false><<<dim3((unsigned)c.gap.nb), dim3(256), 0, c.stream>>>(
-        (const Key<1> *)c.gap.keys, nullptr, c.gap.bstart, c.gap.ustart, (Key<1> *)c.gap.dst, nullptr);
-    HIP_CHECK(hipGetLastError());
+    bucket_pieces(0, c.gap.nb, [&](uint64_t g0, unsigned cnt) {
+        group_gather_kernel<1, false><<<dim3(cnt), dim3(256), 0, c.stream>>>(
+            (const Key<1> *)c.gap.keys, nullptr, c.gap.bstart, c.gap.ustart, (Key<1> *)c.gap.dst, nullptr, nullptr, 0,
+            nullptr, nullptr, g0);
+        HIP_CHECK(hipGetLastError());
+    });
 }
 
 // rm (the rc sort fused with the merge, distinct input): the same buckets go to local_merge_kernel,
@@ -632,10 +651,12 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             const bool gapped = c.gap.valid && c.gap.dst == (const void *)rm->ck;
             const Key<L> *ck = gapped ? (const Key<L> *)c.gap.keys : rm->ck;
             const uint64_t *cgap = gapped ? c.gap.bstart : nullptr;
-            local_merge_kernel<L, COUNTED, CAP><<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(
-                sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
-                &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
-            HIP_CHECK(hipGetLastError());
+            bucket_pieces(0, nb, [&](uint64_t g0, unsigned cnt) {
+                local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                    sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, g0);
+                HIP_CHECK(hipGetLastError());
+            });
             uint32_t novf = 0;
             HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
             HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -648,10 +669,12 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
                 uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
                 HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-                local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
-                    sa, sac, bstart, nullptr, dlist, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
-                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
-                HIP_CHECK(hipGetLastError());
+                bucket_pieces(0, list.size(), [&](uint64_t g0, unsigned cnt) {
+                    local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                        sa, sac, bstart, nullptr, dlist + g0, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                        &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
+                    HIP_CHECK(hipGetLastError());
+                });
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
                 HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
             }
@@ -685,15 +708,31 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
         const bool keycas = nbits < 64;
         constexpr int WPE = COUNTED ? 1 : 8;  // (the uncounted table fits 8 waves per SIMD at 64 VGPRs)
-        if (keycas)
-            local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE>
-                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc,
-                                                                 ucount, ovf, &c.small->counter, cmax, cur);
-        else
-            local_unique_kernel<1, COUNTED, false, 512, LocalTraits<1>::SLOTS / 2, false, 1>
-                <<<dim3((unsigned)nb), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc,
-                                                                 ucount, ovf, &c.small->counter, cmax, cur);
-        HIP_CHECK(hipGetLastError());
+        // only the buckets the keys can occupy: those below the previous level's first and last prefix
+        // (a round of the batched collect fills a fraction of them); the others count 0 keys
+        uint64_t blo = 0, bhi = nb;
+        {
+            Key<L> ends[2];
+            HIP_CHECK(hipMemcpyAsync(&ends[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipMemcpyAsync(&ends[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            if (bp) {
+                blo = (ends[0].w[0] >> (nbits - bp)) << (bb - bp);
+                bhi = std::min<uint64_t>(nb, ((ends[1].w[0] >> (nbits - bp)) + 1) << (bb - bp));
+            }
+        }
+        bucket_pieces(blo, bhi, [&](uint64_t g0, unsigned cnt) {
+            if (keycas)
+                local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE>
+                    <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
+                                                            &c.small->counter, cmax, cur, g0);
+            else
+                local_unique_kernel<1, COUNTED, false, 512, LocalTraits<1>::SLOTS / 2, false, 1>
+                    <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
+                                                            &c.small->counter, cmax, cur, g0);
+            HIP_CHECK(hipGetLastError());
+        });
         uint32_t novf = 0;
         HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -734,9 +773,12 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         const bool index = c.want_gidx;
         uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8) : nullptr;
         if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
-        group_gather_kernel<L, COUNTED><<<dim3((unsigned)nb), dim3(256), 0, c.stream>>>(
-            sb, sbc, bstart, ustart, *keys, COUNTED ? *vals : nullptr, nullptr, nbits - bb, gi, &c.small->gidx_bad);
-        HIP_CHECK(hipGetLastError());
+        bucket_pieces(0, nb, [&](uint64_t g0, unsigned cnt) {
+            group_gather_kernel<L, COUNTED><<<dim3(cnt), dim3(256), 0, c.stream>>>(
+                sb, sbc, bstart, ustart, *keys, COUNTED ? *vals : nullptr, nullptr, nbits - bb, gi, &c.small->gidx_bad,
+                g0);
+            HIP_CHECK(hipGetLastError());
+        });
         uint64_t u = 0;
         uint32_t ibad = 0;
         HIP_CHECK(hipMemcpyAsync(&u, ustart + nb, 8, hipMemcpyDeviceToHost, c.stream));
@@ -937,10 +979,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 HIP_CHECK(hipMemsetAsync(gflag, 0, ngroups * 4, c.stream));
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
                 uint64_t *istart = rm->istart && rm->ib >= b ? rm->istart : nullptr;
-                local_merge_kernel<L, COUNTED, CAP><<<dim3((unsigned)ngroups), dim3(512), 0, c.stream>>>(
-                    *keys, COUNTED ? *vals : nullptr, gstart, gbucket, nullptr, rm->ck, rm->cv, cstart, rm->out,
-                    rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart);
-                HIP_CHECK(hipGetLastError());
+                bucket_pieces(0, ngroups, [&](uint64_t g0, unsigned cnt) {
+                    local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                        *keys, COUNTED ? *vals : nullptr, gstart, gbucket, nullptr, rm->ck, rm->cv, cstart, rm->out,
+                        rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr, nullptr, g0);
+                    HIP_CHECK(hipGetLastError());
+                });
                 uint32_t novf = 0;
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
                 HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -953,10 +997,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                     uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
                     HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
                     HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-                    local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3((unsigned)list.size()), dim3(512), 0, c.stream>>>(
-                        *keys, COUNTED ? *vals : nullptr, gstart, gbucket, dlist, rm->ck, rm->cv, cstart, rm->out,
-                        rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart);
-                    HIP_CHECK(hipGetLastError());
+                    bucket_pieces(0, list.size(), [&](uint64_t g0, unsigned cnt) {
+                        local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                            *keys, COUNTED ? *vals : nullptr, gstart, gbucket, dlist + g0, rm->ck, rm->cv, cstart,
+                            rm->out, rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart);
+                        HIP_CHECK(hipGetLastError());
+                    });
                     HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
                     HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
                     if (c.debug) fprintf(stderr, "[mtg debug] rc merge: %zu big groups -> %u left\n", list.size(), novf);
@@ -984,9 +1030,11 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 constexpr int SL = decltype(sl)::value;
                 constexpr bool ND = decltype(nodup)::value;
                 constexpr int WPE = (L == 1 && KC && !ND && !COUNTED) ? 8 : 1;
-                local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE><<<dim3((unsigned)count), dim3(512), 0, c.stream>>>(
-                    *keys, COUNTED ? *vals : nullptr, gstart, glist, nbits, b, sbits, *alt, COUNTED ? *valt : nullptr,
-                    ucount, ovf, &c.small->counter, cmax);
+                bucket_pieces(0, count, [&](uint64_t g0, unsigned cnt) {
+                    local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                        *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits, *alt,
+                        COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax, nullptr, glist ? 0 : g0);
+                });
             };
             using T_ = std::true_type;
             using F_ = std::false_type;
@@ -1088,10 +1136,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         const bool index = c.want_gidx && gbucket_out && b > 0;
         uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nbuckets + 2) * 8) : nullptr;
         if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
-        group_gather_kernel<L, COUNTED><<<dim3((unsigned)ngroups), dim3(256), 0, c.stream>>>(
-            *alt, COUNTED ? *valt : nullptr, gstart, ustart, *keys, COUNTED ? *vals : nullptr, gbucket_out,
-            nbits - b, gi, &c.small->gidx_bad);
-        HIP_CHECK(hipGetLastError());
+        bucket_pieces(0, ngroups, [&](uint64_t g0, unsigned cnt) {
+            group_gather_kernel<L, COUNTED><<<dim3(cnt), dim3(256), 0, c.stream>>>(
+                *alt, COUNTED ? *valt : nullptr, gstart, ustart, *keys, COUNTED ? *vals : nullptr, gbucket_out,
+                nbits - b, gi, &c.small->gidx_bad, g0);
+            HIP_CHECK(hipGetLastError());
+        });
         uint64_t u = 0;
         uint32_t ibad = 0;
         HIP_CHECK(hipMemcpyAsync(&u, ustart + ngroups, 8, hipMemcpyDeviceToHost, c.stream));
@@ -1726,6 +1776,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         *out = (K2 *)c.ws.get(Workspace::CANON, sizeof(K2));
         if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, 4);
     }
+    debug_check_sorted(c, "canonical rounds", *out, off);
     // the round buffers the later stages do not reuse (they take KB and SPEC_A again)
     for (auto sl : {Workspace::KA, Workspace::CA, Workspace::SPEC_B}) c.ws.release(sl);
     // the fused rc merge reads the canonical keys through their bucket index over the rc sort's final
@@ -2645,7 +2696,10 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     // canonical windows keep the strand whose key top hashes smaller (boss_kernels.hpp: take_rc): the
     // owners' canonical keys then follow the real edges, and one set of ranges balances both
     const int cmode = canonical ? (c.routed_min || d.P == 1 ? 1 : 2) : 0;
-    constexpr unsigned B1 = 9;   // pass B's scatter digit
+    // pass B's scatter digit: 10 bits across ranks (extract_partition_fast_kernel<512, 1024>), so that an
+    // owner of 2 ranks' worth of keys at configs[1]'s density (19 planned bits) keeps a 2-level sort;
+    // the counted pass B takes 9
+    const unsigned B1 = c.fused_b1 ? std::max(c.fused_b1, OB) : (!COUNTED && c.wide_b1 && d.P >= 2) ? 10u : 9u;
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     c.timings.n_positions = npos;
     constexpr int TILE = ExtractTraits<1>::TILE;
@@ -2807,11 +2861,16 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
             stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, FUSED_HB, B1, stripes, rps, dcur,
                                                                          scur, send, dsel);
             HIP_CHECK(hipGetLastError());
-            if (!COUNTED) {
+            if (!COUNTED && B1 > 9) {
+                extract_partition_fast_kernel<512, 1024><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512),
+                                                            0, c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
+                                                                           scur, send, ka, &c.small->error, dsel);
+            } else if (!COUNTED) {
                 extract_partition_fast_kernel<512><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), 0,
                                                       c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
                                                                   scur, send, ka, &c.small->error, dsel);
             } else {
+                if (B1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
                 const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
                 extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
                     in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,

@@ -184,6 +184,42 @@ __device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t *sc
     return res;
 }
 
+// The same over 64-bit values (`scratch`: BLOCK / 64 + 1 u64 words): the bucket-count scans, whose
+// tile of 4096 counts can total more than 2^32 keys (a level-1 histogram of > 4.3e9 keys)
+__device__ __forceinline__ uint64_t wave_inclusive_sum_u64(uint64_t v) {
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t o = __shfl_up(v, off, 64);
+        if (lane >= (uint32_t)off) v += o;
+    }
+    return v;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ uint64_t block_exclusive_sum_u64(uint64_t v, uint64_t *scratch, uint64_t *total) {
+    constexpr int NW = BLOCK / 64;
+    const uint32_t lane = __lane_id();
+    const uint32_t wid = threadIdx.x / 64;
+    const uint64_t inc = wave_inclusive_sum_u64(v);
+    if (lane == 63) scratch[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint64_t t = scratch[w];
+            scratch[w] = s;
+            s += t;
+        }
+        scratch[NW] = s;
+    }
+    __syncthreads();
+    const uint64_t res = scratch[wid] + inc - v;
+    *total = scratch[NW];
+    __syncthreads();
+    return res;
+}
+
 // XCD-contiguous tiles for the scatter passes.  The dispatcher hands workgroups to the 8 XCDs
 // round-robin (workgroup b on XCD b % 8), and every XCD has its own L2.  Workgroup b takes tile
 // (b % 8) * per + b / 8, so each XCD walks its own contiguous eighth of the tiles: the tiles it
@@ -207,7 +243,7 @@ __device__ __forceinline__ uint32_t take_tile(uint32_t *tile_counter, uint32_t *
     return *s_tile;
 }
 
-__device__ __forceinline__ void tile_base_lookback(uint64_t *desc, uint32_t tile, uint32_t count,
+__device__ __forceinline__ void tile_base_lookback(uint64_t *desc, uint32_t tile, uint64_t count,
                                                    uint32_t epoch, uint32_t *error,
                                                    uint64_t *s_base) {
     if (threadIdx.x < 64) {

@@ -442,12 +442,12 @@ __global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__re
                                                             unsigned long long *__restrict__ cursor,
                                                             unsigned long long *__restrict__ bend,
                                                             const uint32_t *__restrict__ sel = nullptr) {
-    __shared__ uint32_t s_scan[256 / 64 + 1];
+    __shared__ uint64_t s_scan[256 / 64 + 1];
     constexpr int PER = 4;
     const uint32_t i = blockIdx.x, nb = 1u << b, f = 1u << (hb - b), nbh = 1u << hb;
     const bool in = !sel || ((sel[i >> 5] >> (i & 31)) & 1u);
     uint32_t h[PER];
-    uint32_t sum = 0;
+    uint64_t sum = 0;  // a bucket of a large input may hold more than 2^32 k-mers
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t st = threadIdx.x * PER + q;
@@ -459,8 +459,8 @@ __global__ __launch_bounds__(256) void stripe_cursor_kernel(const uint32_t *__re
         }
         sum += h[q];
     }
-    uint32_t total;
-    uint32_t off = block_exclusive_sum<256>(sum, s_scan, &total);
+    uint64_t total;
+    uint64_t off = block_exclusive_sum_u64<256>(sum, s_scan, &total);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t st = threadIdx.x * PER + q;

@@ -159,20 +159,20 @@ __global__ __launch_bounds__(512) void scan_counts_kernel(const uint32_t *__rest
                                                           uint64_t *desc, uint32_t epoch,
                                                           uint32_t *tile_counter, uint32_t *error) {
     constexpr int ITEMS = 8, TILE = 512 * ITEMS;
-    __shared__ uint32_t s_scan[512 / 64 + 1];
+    __shared__ uint64_t s_scan[512 / 64 + 1];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_base;
     const uint32_t tile = take_tile(tile_counter, &s_tile);
     const uint64_t i0 = (uint64_t)tile * TILE + (uint64_t)threadIdx.x * ITEMS;
     uint32_t v[ITEMS];
-    uint32_t sum = 0;
+    uint64_t sum = 0;  // 64-bit: a tile of bucket counts may hold more than 2^32 keys
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         v[j] = i0 + j < n ? counts[i0 + j] : 0;
         sum += v[j];
     }
-    uint32_t tile_total;
-    const uint32_t off = block_exclusive_sum<512>(sum, s_scan, &tile_total);
+    uint64_t tile_total;
+    const uint64_t off = block_exclusive_sum_u64<512>(sum, s_scan, &tile_total);
     tile_base_lookback(desc, tile, tile_total, epoch, error, &s_base);
     uint64_t s = s_base + off;
 #pragma unroll
@@ -477,8 +477,9 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
     unsigned b, unsigned sbits, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
     uint32_t *__restrict__ ucount, uint32_t *__restrict__ overflow, uint32_t *__restrict__ novf,
-    uint32_t cmax, const unsigned long long *__restrict__ gend = nullptr) {
-    // gend (speculative buckets): group g is [gstart[g], gend[g]), with gaps between groups
+    uint32_t cmax, const unsigned long long *__restrict__ gend = nullptr, uint64_t g_base = 0) {
+    // gend (speculative buckets): group g is [gstart[g], gend[g]), with gaps between groups; g_base: the
+    // first group of this launch (a grid holds < 2^32 work-items, so 2^23+ buckets launch in pieces)
     constexpr int SLOTS = SL;
     constexpr uint32_t LIMIT = SL / 2;
     constexpr uint64_t EMPTY = ~0ull;
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __shared__ uint32_t s_scan[LB / 64 + 1];
     __shared__ int s_hb;
 
-    const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
+    const uint64_t g = glist ? glist[blockIdx.x] : g_base + blockIdx.x;
     const uint64_t g0 = gstart[g], g1 = gend ? (uint64_t)gend[g] : gstart[g + 1];
     const uint32_t tid = threadIdx.x;
     if (g0 >= g1) {
@@ -854,7 +855,7 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf,
     unsigned b, unsigned nbits, unsigned ib, uint64_t *__restrict__ istart,
     const unsigned long long *__restrict__ gend = nullptr, const uint64_t *__restrict__ gbase = nullptr,
-    const uint64_t *__restrict__ cgap = nullptr) {
+    const uint64_t *__restrict__ cgap = nullptr, uint64_t g_base = 0) {
     // cgap (optional, one bucket per group): the canonical keys of bucket g are read at ck[cgap[g] ..)
     // (a set left in its speculative buckets) instead of ck[cstart[g] ..); cstart stays their compact
     // index
@@ -869,7 +870,7 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     __shared__ uint32_t s_hist[256], s_fill[256];
     __shared__ int s_hb;
     const uint32_t tid = threadIdx.x;
-    const uint64_t g = glist ? glist[blockIdx.x] : blockIdx.x;
+    const uint64_t g = glist ? glist[blockIdx.x] : g_base + blockIdx.x;
     const uint64_t g0 = gstart[g], g1 = gend ? (uint64_t)gend[g] : gstart[g + 1];
     const uint64_t gb0 = gbucket ? gbucket[g] : g, gb1 = gbucket ? gbucket[g + 1] : g + 1;
     const uint64_t c0 = cstart[gb0], c1 = cstart[gb1];
@@ -990,11 +991,12 @@ __global__ __launch_bounds__(256) void group_gather_kernel(
     const Key<L> *__restrict__ tmp, const uint32_t *__restrict__ tcnt,
     const uint64_t *__restrict__ gstart, const uint64_t *__restrict__ ustart,
     Key<L> *__restrict__ out, uint32_t *__restrict__ ocnt, const uint64_t *__restrict__ gbucket = nullptr,
-    unsigned ishift = 0, uint64_t *__restrict__ istart = nullptr, uint32_t *__restrict__ ibad = nullptr) {
+    unsigned ishift = 0, uint64_t *__restrict__ istart = nullptr, uint32_t *__restrict__ ibad = nullptr,
+    uint64_t g_base = 0) {
     // a run of more than IRUN empty buckets between two keys would be one thread's serial loop:
     // the index is abandoned (*ibad) and the caller builds it with bucket_index_kernel
     constexpr uint64_t IRUN = 4096;
-    const uint64_t g = blockIdx.x;
+    const uint64_t g = g_base + blockIdx.x;
     const uint64_t src = gstart[g], dst = ustart[g], m = ustart[g + 1] - dst;
     // gbucket == nullptr: one bucket per group (the speculative final level)
     const uint64_t gb0 = istart ? (gbucket ? gbucket[g] : g) : 0;

@@ -110,6 +110,24 @@ def test_rounds_bench_generator_2m(monkeypatch, canonical, bits):
     assert_same(got, want, "2M reads k=31 canonical=%s bits=%d, 3 rounds" % (canonical, bits))
 
 
+# a 3-level plan in every round (configs[3]'s share plans 7 + 8 + 7 bits): forced on 2 M reads
+@pytest.mark.parametrize("spec3", ["0", "1"])
+@pytest.mark.parametrize("canonical", [False, True])
+def test_rounds_three_msd_levels(monkeypatch, canonical, spec3):
+    monkeypatch.setenv("MTG_RANGES", "3")
+    monkeypatch.setenv("MTG_MSD_LEVELS", "3")
+    monkeypatch.setenv("MTG_SPEC3", spec3)
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=canonical, num_threads=8)
+    ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)
+    got = ctor.build_chunk()
+    t = ctor.timings()
+    assert t.collect_mode == ROUNDS and t.n_batches == 3
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=canonical)
+    assert_same(got, want, "2M reads k=31 canonical=%s, 3 rounds of 3 MSD levels, MTG_SPEC3=%s" % (canonical, spec3))
+
+
 # configs[3]'s shape at a size the oracle finishes: 20 M genome-sampled reads (2.4e9 windows) under a
 # memory_preallocated budget that the DEFAULT planner answers with rounds (no MTG_RANGES), the
 # device path's arrays bit for bit against the oracle (~70 s of oracle time on the box's 16 threads)
