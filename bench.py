@@ -622,6 +622,8 @@ def main():
                                            "n_rows", "radix_launches", "n_sent", "n_batches",
                                            "peak_bytes")},
         "exchange_ms": last["exchange_ms"],
+        "sent_bytes": last["sent_bytes"],  # rank 0's bytes to the other ranks in the last step
+        "collect_mode": last["collect_mode"],  # 0 one pass, 1 key ranges, 2 canonical rounds
     }
     if args.kmc:
         result["kmc_input"] = {"records_per_gpu": kmers_per_rank, "write_s": kmc_write_s,

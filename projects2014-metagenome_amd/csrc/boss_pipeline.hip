@@ -97,6 +97,15 @@ class Workspace {
         return b.ptr;
     }
     void swap(Slot a, Slot b) { std::swap(bufs_[a], bufs_[b]); }
+    // the buffers a build's sort, rc, dummy and emit stages hold (not its input, look-back descriptors
+    // or pass-A histograms): a build in rounds frees the previous build's before sizing its rounds
+    void release_stage_buffers() {
+        for (Slot sl : {KA, KB, CA, CB, SUMS, BUCKETS, FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, FB_K, FB_V,
+                        RC_ALT, RC_ALTC, REAL, REALC, INFLAG, XA, XAC, XB, XBC, QSEND, QRECV, QFLAG, DSRC, DSEND,
+                        DRECV, RC_SENDC, LAST_BITS, W4, WN, DPOS, DWL, CANON, CANONC, CANON_IDX, SPEC_A, SPEC_B,
+                        SPEC_AC, SPEC_BC})
+            release(sl);
+    }
     // frees a slot's buffer (batched builds drop their round buffers before the later stages grow)
     void release(Slot s) {
         Buf &b = bufs_[s];
@@ -490,11 +499,15 @@ struct RcMerge {
 
 // bucket capacities of the speculative final level: the sampled count scaled up, 20 % + 512 keys
 // of slack (a bucket of ~4600 keys overflows with probability ~1e-10 at a 1/8 sample)
+// (buckets outside [blo, bhi) -- below the input's first or above its last previous-level prefix --
+// hold no key and get no slack: a round of a batched collect fills a fraction of the buckets)
 __global__ void spec_caps_kernel(const uint32_t *__restrict__ sample, uint64_t nb, uint32_t stride,
-                                 uint32_t *__restrict__ cap, bool tiny) {
+                                 uint32_t *__restrict__ cap, bool tiny, uint64_t blo, uint64_t bhi) {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) cap[b] = tiny ? (uint32_t)(((uint64_t)sample[b] * stride) / 2)
-                              : (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
+    if (b >= nb) return;
+    if (b < blo || b >= bhi) cap[b] = 0;
+    else cap[b] = tiny ? (uint32_t)(((uint64_t)sample[b] * stride) / 2)
+                       : (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
 }
 
 // The final MSD level of the main sort (level 2 after the fused K1's level 1) without its exact
@@ -573,8 +586,19 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         msd_hist_kernel<L><<<dim3((unsigned)(fine ? tiles : ceil_div(tiles, SS))), dim3(MSD_BLOCK), 0, c.stream>>>(
             *keys, n, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1);
         HIP_CHECK(hipGetLastError());
+        // the buckets the keys can occupy: those under the previous level's first and last prefix
+        uint64_t blo = 0, bhi = nb;
+        if (bp) {
+            Key<L> ends[2];
+            HIP_CHECK(hipMemcpyAsync(&ends[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipMemcpyAsync(&ends[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));
+            blo = (ends[0].w[0] >> (nbits - bp)) << (bb - bp);
+            bhi = std::min<uint64_t>(nb, ((ends[1].w[0] >> (nbits - bp)) + 1) << (bb - bp));
+        }
         uint32_t *cap = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
-        spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap, c.spec_tiny);
+        spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap, c.spec_tiny,
+                                                                                        blo, bhi);
         HIP_CHECK(hipGetLastError());
         uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nb + 1) * 8);
         {
@@ -708,20 +732,9 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
         const bool keycas = nbits < 64;
         constexpr int WPE = COUNTED ? 1 : 8;  // (the uncounted table fits 8 waves per SIMD at 64 VGPRs)
-        // only the buckets the keys can occupy: those below the previous level's first and last prefix
-        // (a round of the batched collect fills a fraction of them); the others count 0 keys
-        uint64_t blo = 0, bhi = nb;
-        {
-            Key<L> ends[2];
-            HIP_CHECK(hipMemcpyAsync(&ends[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
-            HIP_CHECK(hipMemcpyAsync(&ends[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
-            HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
-            HIP_CHECK(hipStreamSynchronize(c.stream));
-            if (bp) {
-                blo = (ends[0].w[0] >> (nbits - bp)) << (bb - bp);
-                bhi = std::min<uint64_t>(nb, ((ends[1].w[0] >> (nbits - bp)) + 1) << (bb - bp));
-            }
-        }
+        // only the buckets the keys can occupy (blo, bhi above; a round of the batched collect fills a
+        // fraction of them); the others count 0 keys
+        HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
         bucket_pieces(blo, bhi, [&](uint64_t g0, unsigned cnt) {
             if (keycas)
                 local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE>
@@ -1693,6 +1706,9 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     using K2 = Key<1>;
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     if (c.range_scan || c.disk || !fused_applies(c, K, npos)) return false;
+    // a previous build's stage buffers would crowd out this build's rounds: they go now (and are
+    // allocated again at the sizes this build needs)
+    c.ws.release_stage_buffers();
     FusedA A;
     fused_pass_a(c, K, canonical, in, &A);
     const uint64_t N = A.N;
@@ -1777,8 +1793,10 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, 4);
     }
     debug_check_sorted(c, "canonical rounds", *out, off);
-    // the round buffers the later stages do not reuse (they take KB and SPEC_A again)
-    for (auto sl : {Workspace::KA, Workspace::CA, Workspace::SPEC_B}) c.ws.release(sl);
+    // the round buffers (sized for the largest round) go; the rc stage takes KB and SPEC_A again at
+    // its own size
+    for (auto sl : {Workspace::KA, Workspace::CA, Workspace::KB, Workspace::CB, Workspace::SPEC_A, Workspace::SPEC_B})
+        c.ws.release(sl);
     // the fused rc merge reads the canonical keys through their bucket index over the rc sort's final
     // bits (a one-pass build gets it from its own sort's groups)
     c.gidx = Ctx::GroupIndex{};
@@ -2820,6 +2838,7 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     c.timings.n_batches = rounds;
     if (rounds > 1) {
         c.timings.collect_mode = 2;
+        c.ws.release_stage_buffers();  // a previous build's would crowd out the rounds' buffers
         *ev_extract = tm.mark();
     }
     K2 *acc = nullptr;  // rounds: the owned distinct keys so far
