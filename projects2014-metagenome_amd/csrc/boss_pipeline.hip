@@ -70,26 +70,35 @@ class Workspace {
     ~Workspace() {
         for (auto &b : bufs_)
             if (b.ptr) (void)hipFree(b.ptr);
+        for (auto &b : cache_) (void)hipFree(b.ptr);
     }
     void *get(Slot s, size_t bytes, size_t keep = 0, hipStream_t stream = nullptr) {
         Buf &b = bufs_[s];
         bytes = std::max<size_t>(bytes, 256);
         if (b.cap < bytes) {
-            void *p = nullptr;
-            size_t cap = bytes + bytes / 8;
-            if (hipMalloc(&p, cap) != hipSuccess) {
-                (void)hipGetLastError();
-                size_t fr = 0, tot = 0;
-                (void)hipMemGetInfo(&fr, &tot);
-                throw std::runtime_error("HIP error out of memory: workspace slot " + std::to_string((int)s) + " wants " +
-                                         std::to_string(cap >> 20) + " MiB (held " + std::to_string(held() >> 20) +
-                                         " MiB in all slots, this one " + std::to_string(b.cap >> 20) + " MiB; free " +
-                                         std::to_string(fr >> 20) + " MiB)");
+            size_t cap = 0;
+            void *p = take_cached(bytes, &cap);
+            if (!p) {
+                cap = bytes + bytes / 8;
+                if (hipMalloc(&p, cap) != hipSuccess) {
+                    (void)hipGetLastError();
+                    drop_cache();
+                    if (hipMalloc(&p, cap) != hipSuccess) {
+                        (void)hipGetLastError();
+                        size_t fr = 0, tot = 0;
+                        (void)hipMemGetInfo(&fr, &tot);
+                        throw std::runtime_error("HIP error out of memory: workspace slot " + std::to_string((int)s) +
+                                                 " wants " + std::to_string(cap >> 20) + " MiB (held " +
+                                                 std::to_string(held() >> 20) + " MiB in all slots, this one " +
+                                                 std::to_string(b.cap >> 20) + " MiB; free " + std::to_string(fr >> 20) +
+                                                 " MiB)");
+                    }
+                }
             }
             if (keep && b.ptr) HIP_CHECK(hipMemcpyAsync(p, b.ptr, keep, hipMemcpyDeviceToDevice, stream));
             if (b.ptr) {
-                if (keep) HIP_CHECK(hipStreamSynchronize(stream));
-                HIP_CHECK(hipFree(b.ptr));
+                HIP_CHECK(hipDeviceSynchronize());
+                cache_.push_back(b);
             }
             b.ptr = p;
             b.cap = cap;
@@ -106,20 +115,42 @@ class Workspace {
                         SPEC_AC, SPEC_BC})
             release(sl);
     }
-    // frees a slot's buffer (batched builds drop their round buffers before the later stages grow)
+    // a slot gives its buffer back (batched builds drop their round buffers before the later stages
+    // grow).  The block is kept for the next get() of about its size rather than freed: freeing and
+    // mapping again the ~200 GB of a configs[3] share cost seconds per build while the driver clears
+    // the pages (and slowed the kernels running meanwhile).  A hipMalloc that fails frees the kept
+    // blocks and tries again.
     void release(Slot s) {
         Buf &b = bufs_[s];
         if (b.ptr) {
             HIP_CHECK(hipDeviceSynchronize());
-            (void)hipFree(b.ptr);
+            cache_.push_back(b);
         }
         b.ptr = nullptr;
         b.cap = 0;
     }
+    // every byte the workspace holds, in slots and kept blocks
     uint64_t held() const {
-        uint64_t t = 0;
+        uint64_t t = cached();
         for (const auto &b : bufs_) t += b.cap;
         return t;
+    }
+    uint64_t cached() const {
+        uint64_t t = 0;
+        for (const auto &b : cache_) t += b.cap;
+        return t;
+    }
+    // free HBM for new buffers: the device's free memory plus the kept blocks
+    uint64_t free_bytes() const {
+        size_t fr = 0, tot = 0;
+        HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        return (uint64_t)fr + cached();
+    }
+    void drop_cache() {
+        if (cache_.empty()) return;
+        HIP_CHECK(hipDeviceSynchronize());
+        for (auto &b : cache_) (void)hipFree(b.ptr);
+        cache_.clear();
     }
     uint64_t held_slot(Slot s) const { return bufs_[s].cap; }
 
@@ -128,7 +159,22 @@ class Workspace {
         void *ptr = nullptr;
         size_t cap = 0;
     };
+    // the smallest kept block of at least `bytes` and at most about twice that (a far bigger block
+    // stays for the request it was made for)
+    void *take_cached(size_t bytes, size_t *cap) {
+        size_t best = cache_.size();
+        for (size_t i = 0; i < cache_.size(); ++i)
+            if (cache_[i].cap >= bytes && cache_[i].cap <= 2 * bytes + (64u << 20) &&
+                (best == cache_.size() || cache_[i].cap < cache_[best].cap))
+                best = i;
+        if (best == cache_.size()) return nullptr;
+        void *p = cache_[best].ptr;
+        *cap = cache_[best].cap;
+        cache_.erase(cache_.begin() + (long)best);
+        return p;
+    }
     Buf bufs_[NSLOTS];
+    std::vector<Buf> cache_;
 };
 
 struct Small {  // one device word block, zeroed per use
@@ -210,7 +256,9 @@ struct Ctx {
                                    // (=superkmer), 2 local collect + exchange of sorted runs (=local)
     unsigned fused_b1 = 0;         // MTG_FUSED_B1=n: the fused K1's level-1 digit forced to n bits (A/B runs)
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
+    bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's earlier probe loop (A/B)
     bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
+    bool kmc_mirror = true;  // add_kmc copies the first database to the device while reading it
                                    // that re-scan the reads (both strands) even where the canonical
                                    // rounds of the fused K1 apply (collect_rounds_fused)
     bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
@@ -272,6 +320,8 @@ static void load_knobs(Ctx &c) {
     c.dummy_ranks = !is("MTG_DUMMY_SORT", "lifted");
     c.range_scan = is("MTG_COLLECT", "ranges");
     c.wide_b1 = !is("MTG_WIDE_B1", "0");
+    c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
+    c.lu_fast = !is("MTG_LU_FAST", "0");
     if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
     c.spec_final = !is("MTG_SPEC", "0");
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
@@ -571,8 +621,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         const uint64_t nb = 1ull << bb;
         // the two slack-sized buffers must fit next to everything else
         {
-            size_t fr = 0, tot = 0;
-            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            const uint64_t fr = c.ws.free_bytes();
             if ((double)n * KB * 1.4 * 2.0 > 0.5 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
                                                   (double)c.ws.held_slot(Workspace::SPEC_B) +
                                                   (double)c.ws.held_slot(Workspace::SPEC_AC) +
@@ -612,8 +661,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         }
         const uint64_t C = read_u64(c, (const unsigned long long *)(bstart + nb));
         {  // the capacity is known now: both slack-sized buffers (one for the fused rc merge) must fit
-            size_t fr = 0, tot = 0;
-            HIP_CHECK(hipMemGetInfo(&fr, &tot));
+            const uint64_t fr = c.ws.free_bytes();
             const double need = (double)C * KB * (rm ? 1.0 : 2.0);
             const double have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
                                 (double)c.ws.held_slot(Workspace::SPEC_AC) +
@@ -736,7 +784,11 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // fraction of them); the others count 0 keys
         HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
         bucket_pieces(blo, bhi, [&](uint64_t g0, unsigned cnt) {
-            if (keycas)
+            if (keycas && c.lu_fast)
+                local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE, true>
+                    <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
+                                                            &c.small->counter, cmax, cur, g0);
+            else if (keycas)
                 local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE>
                     <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
                                                             &c.small->counter, cmax, cur, g0);
@@ -1044,6 +1096,15 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 constexpr bool ND = decltype(nodup)::value;
                 constexpr int WPE = (L == 1 && KC && !ND && !COUNTED) ? 8 : 1;
                 bucket_pieces(0, count, [&](uint64_t g0, unsigned cnt) {
+                    if constexpr (KC && !ND) {
+                        if (c.lu_fast) {
+                            local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE, true><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                                *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits,
+                                *alt, COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax, nullptr,
+                                glist ? 0 : g0);
+                            return;
+                        }
+                    }
                     local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                         *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits, *alt,
                         COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax, nullptr, glist ? 0 : g0);
@@ -4244,8 +4305,20 @@ int mtg_boss_ctor_add_kmc(mtg_boss_ctor *c, const char *kmc_path, uint64_t min_c
         return MTG_ERR_ARGUMENT;
     }
     try {
-        KmcInput in = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0, stage_threads(c));
-        std::lock_guard<std::mutex> lock(c->kmc_mu);
+        // the first database of a batch is copied to the device while its files are read (the
+        // workspace's KMC slots; a later database is copied by build_chunk, the slots being taken)
+        std::unique_lock<std::mutex> lock(c->kmc_mu, std::defer_lock);
+        if (c->ctx.kmc_mirror) lock.lock();
+        const bool mirror = c->ctx.kmc_mirror && c->kmc.empty();
+        DeviceGuard g(c->device);
+        DeviceMirror mpre, msuf;
+        mpre.stream = msuf.stream = c->ctx.stream;
+        mpre.device = msuf.device = c->device;
+        mpre.alloc = [&](uint64_t b) { return (uint8_t *)c->ctx.ws.get(Workspace::KMC_LUT, b); };
+        msuf.alloc = [&](uint64_t b) { return (uint8_t *)c->ctx.ws.get(Workspace::KMC_REC, b); };
+        KmcInput in = kmc_open(kmc_path, min_count, max_count, call_both_from_canonical != 0, stage_threads(c),
+                               mirror ? &mpre : nullptr, mirror ? &msuf : nullptr);
+        if (!lock.owns_lock()) lock.lock();
         if (in.total) c->kmc.push_back(std::move(in));
         return MTG_OK;
     } catch (const std::exception &e) {
@@ -4691,10 +4764,19 @@ static int build_chunk_impl(mtg_boss_ctor *c, mtg::Comm *comm, mtg_boss_chunk *o
         const auto t_input = std::chrono::steady_clock::now();
         uint64_t seq_base = len, read_base = nr;
         for (const auto &m : c->kmc) {
-            uint64_t *dlut = (uint64_t *)c->ctx.ws.get(Workspace::KMC_LUT, m.nlut * 8);
-            uint8_t *drec = (uint8_t *)c->ctx.ws.get(Workspace::KMC_REC, m.record_bytes() + 1);
-            HIP_CHECK(hipMemcpyAsync(dlut, m.lut_bytes(), m.nlut * 8, hipMemcpyHostToDevice, s));
-            HIP_CHECK(hipMemcpyAsync(drec, m.records(), m.record_bytes(), hipMemcpyHostToDevice, s));
+            const uint64_t *dlut;
+            const uint8_t *drec;
+            if (m.dpre) {  // copied while add_kmc read the files (same stream)
+                dlut = (const uint64_t *)(m.dpre + 8);
+                drec = m.dsuf + 8;
+            } else {
+                uint64_t *l = (uint64_t *)c->ctx.ws.get(Workspace::KMC_LUT, m.nlut * 8);
+                uint8_t *r = (uint8_t *)c->ctx.ws.get(Workspace::KMC_REC, m.record_bytes() + 1);
+                HIP_CHECK(hipMemcpyAsync(l, m.lut_bytes(), m.nlut * 8, hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(r, m.records(), m.record_bytes(), hipMemcpyHostToDevice, s));
+                dlut = l;
+                drec = r;
+            }
             kmc_decode_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(m.total, 256), 65536))),
                                 dim3(256), 0, s>>>(drec, dlut, m.nlut, m.total, m.k, m.lut_len,
                                                    m.counter_size, m.min_count, m.max_count, m.both ? 1 : 0,

@@ -27,6 +27,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <functional>
 #include <vector>
 
 #include <fcntl.h>
@@ -68,6 +69,7 @@ struct KmcInput {
     uint64_t total = 0;
     uint64_t nlut = 0;                     // prefix-table entries (4^lut_len)
     PinnedFile pre, suf;                   // the two files as read
+    const uint8_t *dpre = nullptr, *dsuf = nullptr;  // their device mirrors (DeviceMirror) or null
     const uint8_t *lut_bytes() const { return pre.data + 4; }  // u64 lut[nlut] after "KMCP"
     const uint8_t *records() const { return suf.data + 4; }    // after "KMCS"
     uint64_t record_bytes() const { return suf.size >= 8 ? suf.size - 8 : 0; }
@@ -81,11 +83,21 @@ static std::string kmc_strip(const std::string &p) {
     return p;
 }
 
+// optional device copy of a file made while it is read: file byte j lands at device byte j + 4 (so
+// the 8-byte prefix table after the 4-byte "KMCP" marker is 8-byte aligned), piece by piece on
+// `stream` as each piece is read, so the host-to-device copy runs under the reading
+struct DeviceMirror {
+    std::function<uint8_t *(uint64_t bytes)> alloc;  // device buffer of `bytes` (file size + 8)
+    hipStream_t stream = nullptr;
+    int device = 0;
+    uint8_t *out = nullptr;                           // the buffer, once read
+};
+
 // a file into a pinned pool block: large preads from several threads at once (a single reader
 // copies out of the page cache at ~3.5 GB/s: 316 of the 561 ms of configs[4]'s file route went
 // to reading the 1.1 GB suffix file into pageable memory, and its host-to-device copy then ran
 // from pageable memory too)
-static PinnedFile read_file_pinned(const std::string &path, unsigned threads) {
+static PinnedFile read_file_pinned(const std::string &path, unsigned threads, DeviceMirror *dm = nullptr) {
     const int fd = ::open(path.c_str(), O_RDONLY);
     if (fd < 0) throw std::runtime_error("cannot open " + path);
     const off_t end = ::lseek(fd, 0, SEEK_END);
@@ -98,11 +110,21 @@ static PinnedFile read_file_pinned(const std::string &path, unsigned threads) {
         throw;
     }
     f.size = n;
+    uint8_t *dst = nullptr;
+    if (dm) {
+        try {
+            dst = dm->alloc(n + 8);
+        } catch (...) {
+            ::close(fd);
+            throw;
+        }
+    }
     constexpr uint64_t PIECE = 64ull << 20;
     const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads, (n + PIECE - 1) / PIECE));
     std::atomic<uint64_t> next{0};
     std::atomic<bool> bad{false};
     auto work = [&]() {
+        if (dst) (void)hipSetDevice(dm->device);
         while (!bad) {
             const uint64_t p0 = next.fetch_add(PIECE);
             if (p0 >= n) return;
@@ -115,6 +137,10 @@ static PinnedFile read_file_pinned(const std::string &path, unsigned threads) {
                 }
                 p += (uint64_t)got;
             }
+            if (dst && hipMemcpyAsync(dst + 4 + p0, f.data + p0, p1 - p0, hipMemcpyHostToDevice, dm->stream) != hipSuccess) {
+                bad = true;
+                return;
+            }
         }
     };
     std::vector<std::thread> pool;
@@ -123,23 +149,29 @@ static PinnedFile read_file_pinned(const std::string &path, unsigned threads) {
     for (auto &t : pool) t.join();
     ::close(fd);
     if (bad) throw std::runtime_error("cannot read " + path);
+    if (dm) dm->out = dst;
     return f;
 }
 
 // seq_io::read_kmers (kmc_parser.cpp:27-62): min/max as the reference passes them (max
 // exclusive), combined with the database's own cut-offs as CKMCFile::SetMin/MaxCount do
 static KmcInput kmc_open(const std::string &path, uint64_t min_count, uint64_t max_count,
-                         bool call_both_from_canonical, unsigned threads = 8) {
+                         bool call_both_from_canonical, unsigned threads = 8, DeviceMirror *dpre = nullptr,
+                         DeviceMirror *dsuf = nullptr) {
     const std::string base = kmc_strip(path);
     auto bad = [&](const char *why) {
         return std::runtime_error("Error: Can't open KMC database " + base + " (" + why + ")");
     };
     KmcInput in;
     try {
-        in.pre = read_file_pinned(base + ".kmc_pre", threads);
-        in.suf = read_file_pinned(base + ".kmc_suf", threads);
+        in.pre = read_file_pinned(base + ".kmc_pre", threads, dpre);
+        in.suf = read_file_pinned(base + ".kmc_suf", threads, dsuf);
     } catch (const std::exception &) {
         throw bad("missing file");
+    }
+    if (dpre && dsuf) {
+        in.dpre = dpre->out;
+        in.dsuf = dsuf->out;
     }
     const PinnedFile &pre = in.pre, &suf = in.suf;
     if (pre.size < 16 || memcmp(pre.data, "KMCP", 4) || memcmp(pre.data + pre.size - 4, "KMCP", 4))

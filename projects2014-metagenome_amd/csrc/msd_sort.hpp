@@ -471,7 +471,7 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
 template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
-          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1>
+          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1, bool FAST = false>
 __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
@@ -488,6 +488,12 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     constexpr bool LIST = KEYCAS && !NODUP;
     __shared__ Key<L> s_key[SLOTS];
     __shared__ uint16_t s_slot[LIST ? LIMIT : 1];
+    // FAST (LIST only): a batch's loads without per-key bounds when the whole batch lies in the
+    // group, a probe loop without unrolled exit chains, and the batch's new keys take their list
+    // positions with one wave scan + one LDS atomic per wave and batch.  The kernel issues about as
+    // many SALU (divergence masks) as VALU instructions, and both pipes issue ~1 instruction per cycle
+    // per CU, so the loop's scalar bookkeeping is cut along with its vector work.
+    static_assert(!FAST || (LIST && (SL & (SL - 1)) == 0), "FAST is the LIST path, power-of-two tables");
     __shared__ uint32_t s_state[KEYCAS ? 1 : SLOTS];
     __shared__ uint32_t s_sum[COUNTED ? SLOTS : 1];
     __shared__ uint32_t s_hist[256];
@@ -539,10 +545,34 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         constexpr int PAIR = L == 1 ? 2 : 1;
         constexpr int BATCH = (LB >= 1024 ? 12 : WPE >= 8 ? 6 : 8) / PAIR;  // 6 at 64 VGPRs: 4.47 -> 4.19 ms
         const uint64_t a0 = PAIR == 2 ? (g0 & ~1ull) : g0;
-        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += (uint64_t)LB * BATCH * PAIR) {
+        // (FAST: the loop runs while any lane of the wave has keys, so the per-batch wave scan sees
+        // every lane; the lanes past the group's end load nothing)
+        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; FAST ? __ballot(ib < g1 && !ovf) != 0 : (ib < g1 && !ovf);
+             ib += (uint64_t)LB * BATCH * PAIR) {
             Key<L> kb[BATCH * PAIR];
             uint32_t vb[BATCH * PAIR];
             bool hv[BATCH * PAIR];
+            if (FAST && ib >= g0 && ib + (uint64_t)(BATCH - 1) * LB * PAIR + PAIR <= g1) {
+#pragma unroll
+                for (int q = 0; q < BATCH; ++q) {
+                    const uint64_t i = ib + (uint64_t)q * LB * PAIR;
+                    if constexpr (PAIR == 2) {
+                        const ulonglong2 kv = *(const ulonglong2 *)(keys + i);
+                        kb[2 * q] = Key<L>::from(kv.x);
+                        kb[2 * q + 1] = Key<L>::from(kv.y);
+                        hv[2 * q] = hv[2 * q + 1] = true;
+                        if (COUNTED) {
+                            const uint2 vv = *(const uint2 *)(vals + i);
+                            vb[2 * q] = vv.x;
+                            vb[2 * q + 1] = vv.y;
+                        }
+                    } else {
+                        kb[q] = keys[i];
+                        hv[q] = true;
+                        if (COUNTED) vb[q] = vals[i];
+                    }
+                }
+            } else
 #pragma unroll
             for (int q = 0; q < BATCH; ++q) {
                 const uint64_t i = ib + (uint64_t)q * LB * PAIR;
@@ -598,6 +628,67 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             // batch instead of a chain per key, measured slower: 11.4 vs 10.5 ms sort stage, the
             // in-flight results spill at 64 VGPRs; 10.6 ms with 4-key batches)
             constexpr int NQ = BATCH * PAIR;
+            if constexpr (FAST) {
+                uint32_t insm = 0;  // bit q: key q was new (inserted at insh[q])
+                uint16_t insh[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const bool act = hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice);
+                    uint32_t h = slot_of<SLOTS>(key_hash(kb[q]));
+                    // st: 0 probing, 1 found, 2 inserted, 3 no key.  The loop runs while any lane of the
+                    // wave probes (a wave-uniform loop with one masked CAS block: few lane-mask merges)
+                    uint32_t st = act ? 0u : 3u;
+                    for (uint32_t probes = 0; __ballot(st == 0) != 0; ++probes) {
+                        if (probes >= SLOTS) {
+                            ovf = ovf || st == 0;
+                            break;
+                        }
+                        if (st == 0) {
+                            const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
+                                                           (unsigned long long)EMPTY, (unsigned long long)kb[q].w[0]);
+                            st = old == EMPTY ? 2u : old == kb[q].w[0] ? 1u : 0u;
+                            h = st ? h : (h + 1) & (SLOTS - 1);
+                        }
+                    }
+                    const bool isnew = st == 2;
+                    if (act && st != 0) {
+                        if (COUNTED) {
+                            const uint32_t add = vb[q];
+                            if (cmax <= 0xFFFFu) {
+                                const uint32_t o = atomicAdd(&s_sum[h], add);
+                                if (o + add > 0x40000000u) atomicMin(&s_sum[h], cmax);
+                            } else {
+                                uint32_t old = s_sum[h], assumed;
+                                do {
+                                    assumed = old;
+                                    const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
+                                    old = atomicCAS(&s_sum[h], assumed, nv);
+                                } while (old != assumed);
+                            }
+                        }
+                    }
+                    insh[q] = (uint16_t)h;
+                    insm |= (uint32_t)isnew << q;
+                }
+                // list positions: a wave scan of the new-key counts, one LDS atomic per wave
+                const uint32_t nins = (uint32_t)__popc(insm);
+                const uint32_t incl = wave_inclusive_sum(nins);
+                const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                if (wtot) {
+                    uint32_t wb = 0;
+                    if (__lane_id() == 63) wb = atomicAdd(&s_distinct, wtot);
+                    uint32_t pos = (uint32_t)__builtin_amdgcn_readlane((int)wb, 63) + incl - nins;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        if ((insm >> q) & 1u) {
+                            if (pos < LIMIT) s_slot[pos] = insh[q];
+                            else ovf = true;
+                            ++pos;
+                        }
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // LIST: the new keys of a wave take their list positions by ballot after the probe
