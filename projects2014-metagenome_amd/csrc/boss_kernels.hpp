@@ -607,7 +607,10 @@ struct DummyTraits {
  * (8 edges per thread instead of 4: 2.59 ms).
  * A range that does not fit falls back to bucketed searches in global memory.
  */
-template <int L>
+// ABL (timing ablations for tools/stage_bench only; 0 in the product): bit 0 = no in_flag stores,
+// bit 1 = no flags stores, bit 2 = no staging and no search (every edge a sink), bit 3 = staging
+// but no search
+template <int L, int ABL = 0>
 __global__ __launch_bounds__(256) void dummy_sink_kernel(
     const Key<L> *__restrict__ keys, uint64_t n, unsigned K, const uint64_t *__restrict__ start,
     unsigned bshift, uint8_t *__restrict__ flags, uint8_t *__restrict__ in_flag) {
@@ -660,6 +663,7 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+        if (ABL & 4) break;
         if (s_off[c] == ~0u) continue;
         const uint64_t a = s_lo[c];
         const uint32_t off = s_off[c];
@@ -669,6 +673,10 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (j0 + q >= tn) continue;
+        if (ABL & 12) {
+            if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)(1u | (((first >> q) & 1u) << 1)) ^ (uint8_t)s_r[q & 7].w[0];
+            continue;
+        }
         const uint32_t c = (uint32_t)(x[q].w[0] & 3);
         // to_next(x, K, 0): node a_2..a_K, label 0 (kmer_boss.hpp:147-169)
         const Key<L> p = (shr(x[q], 2) | shl(Key<L>::from(c), 2 * (K - 1))) & ~m3;
@@ -686,8 +694,9 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
             const uint64_t i = lower_bound_bucketed(keys, start, bshift, p);
             if (i < n && shr(keys[i], 2) == shr(p, 2)) hit = i;
         }
-        if (hit != ~0ull) in_flag[hit] = 1;
-        flags[base + j0 + q] = (uint8_t)((hit == ~0ull ? 1u : 0u) | (((first >> q) & 1u) << 1));
+        if (!(ABL & 1) && hit != ~0ull) in_flag[hit] = 1;
+        if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)((hit == ~0ull ? 1u : 0u) | (((first >> q) & 1u) << 1));
+        else if (hit == 12345) flags[0] = 1;  // keep the search
     }
 }
 

@@ -256,7 +256,8 @@ struct Ctx {
                                    // (=superkmer), 2 local collect + exchange of sorted runs (=local)
     unsigned fused_b1 = 0;         // MTG_FUSED_B1=n: the fused K1's level-1 digit forced to n bits (A/B runs)
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
-    bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's earlier probe loop (A/B)
+    bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
+    uint32_t merge_it = 1;         // MTG_MERGE_IT: local_merge_kernel's least outputs per thread (A/B)
     bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
     bool kmc_mirror = true;  // add_kmc copies the first database to the device while reading it
                                    // that re-scan the reads (both strands) even where the canonical
@@ -322,6 +323,7 @@ static void load_knobs(Ctx &c) {
     c.wide_b1 = !is("MTG_WIDE_B1", "0");
     c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
     c.lu_fast = !is("MTG_LU_FAST", "0");
+    if (const char *e = getenv("MTG_MERGE_IT")) c.merge_it = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
     c.spec_final = !is("MTG_SPEC", "0");
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
@@ -632,8 +634,9 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         HIP_CHECK(hipMemsetAsync(h, 0, nb * 4, c.stream));
         // 2 levels: every 8th tile (level-1 buckets span hundreds of tiles); 3 levels: the first 1/8 of every
         // tile (level-2 buckets can be only a few tiles long, and a tile-granular sample missed them)
-        msd_hist_kernel<L><<<dim3((unsigned)(fine ? tiles : ceil_div(tiles, SS))), dim3(MSD_BLOCK), 0, c.stream>>>(
-            *keys, n, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1);
+        constexpr uint32_t GT = 8;  // fine sample: tiles per workgroup (one LDS window flush)
+        msd_hist_kernel<L><<<dim3((unsigned)(fine ? ceil_div(tiles, GT) : ceil_div(tiles, SS))), dim3(MSD_BLOCK), 0,
+                             c.stream>>>(*keys, n, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1, fine ? GT : 1);
         HIP_CHECK(hipGetLastError());
         // the buckets the keys can occupy: those under the previous level's first and last prefix
         uint64_t blo = 0, bhi = nb;
@@ -726,7 +729,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             bucket_pieces(0, nb, [&](uint64_t g0, unsigned cnt) {
                 local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                     sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
-                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, g0);
+                    &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, g0, c.merge_it);
                 HIP_CHECK(hipGetLastError());
             });
             uint32_t novf = 0;
@@ -744,7 +747,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
                 bucket_pieces(0, list.size(), [&](uint64_t g0, unsigned cnt) {
                     local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                         sa, sac, bstart, nullptr, dlist + g0, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
-                        &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap);
+                        &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, 0, c.merge_it);
                     HIP_CHECK(hipGetLastError());
                 });
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
@@ -1047,7 +1050,8 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 bucket_pieces(0, ngroups, [&](uint64_t g0, unsigned cnt) {
                     local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                         *keys, COUNTED ? *vals : nullptr, gstart, gbucket, nullptr, rm->ck, rm->cv, cstart, rm->out,
-                        rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr, nullptr, g0);
+                        rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr, nullptr, g0,
+                        c.merge_it);
                     HIP_CHECK(hipGetLastError());
                 });
                 uint32_t novf = 0;
@@ -1065,7 +1069,8 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                     bucket_pieces(0, list.size(), [&](uint64_t g0, unsigned cnt) {
                         local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                             *keys, COUNTED ? *vals : nullptr, gstart, gbucket, dlist + g0, rm->ck, rm->cv, cstart,
-                            rm->out, rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart);
+                            rm->out, rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr,
+                            nullptr, 0, c.merge_it);
                         HIP_CHECK(hipGetLastError());
                     });
                     HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -234,6 +235,33 @@ class CallbackComm : public Comm {
 };
 
 // ------------------------------------------------------------------- in-process rank threads
+// the received slices of one local all-to-all in one launch (one workgroup row per source rank)
+// instead of one copy per peer: a P = 8 build made ~270 copies per rank, each a launch
+constexpr int kLocalCopyMax = 64;
+struct LocalCopyBatch {
+    const char *src[kLocalCopyMax];
+    char *dst[kLocalCopyMax];
+    uint64_t bytes[kLocalCopyMax];
+};
+
+__global__ __launch_bounds__(256) void local_copy_kernel(LocalCopyBatch b) {
+    const int seg = blockIdx.y;
+    const char *src = b.src[seg];
+    char *dst = b.dst[seg];
+    const uint64_t n = b.bytes[seg];
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t al = ((uint64_t)(uintptr_t)src | (uint64_t)(uintptr_t)dst | n);
+    if ((al & 15) == 0) {
+        for (uint64_t i = t; i < n / 16; i += T) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+    } else if ((al & 7) == 0) {
+        for (uint64_t i = t; i < n / 8; i += T) ((uint64_t *)dst)[i] = ((const uint64_t *)src)[i];
+    } else if ((al & 3) == 0) {
+        for (uint64_t i = t; i < n / 4; i += T) ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
+    } else {
+        for (uint64_t i = t; i < n; i += T) dst[i] = src[i];
+    }
+}
+
 struct LocalGroup {
     explicit LocalGroup(int n) : size(n), slots(n), host(n), held_ms(n, 0.0) {}
     int size;
@@ -342,12 +370,29 @@ class LocalComm : public Comm {
                 throw std::runtime_error(msg);
             }
         hold();
-        for (int i = 0; i < size_; ++i) {
-            const auto &src = g_->slots[i];
-            if (rcnt[i])
-                COMM_HIP(hipMemcpyAsync((char *)d_recv + roff[i] * esz,
-                                        (const char *)src.ptr + src.soff[rank_] * esz, rcnt[i] * esz,
-                                        hipMemcpyDeviceToDevice, s));
+        if (size_ <= kLocalCopyMax) {
+            LocalCopyBatch batch{};
+            uint64_t most = 0;
+            for (int i = 0; i < size_; ++i) {
+                const auto &src = g_->slots[i];
+                batch.src[i] = (const char *)src.ptr + src.soff[rank_] * esz;
+                batch.dst[i] = (char *)d_recv + roff[i] * esz;
+                batch.bytes[i] = rcnt[i] * esz;
+                most = std::max<uint64_t>(most, rcnt[i] * esz);
+            }
+            if (most) {
+                const unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((most + 16383) / 16384, 2048));
+                local_copy_kernel<<<dim3(gx, (unsigned)size_), dim3(256), 0, s>>>(batch);
+                COMM_HIP(hipGetLastError());
+            }
+        } else {
+            for (int i = 0; i < size_; ++i) {
+                const auto &src = g_->slots[i];
+                if (rcnt[i])
+                    COMM_HIP(hipMemcpyAsync((char *)d_recv + roff[i] * esz,
+                                            (const char *)src.ptr + src.soff[rank_] * esz, rcnt[i] * esz,
+                                            hipMemcpyDeviceToDevice, s));
+            }
         }
         COMM_HIP(hipStreamSynchronize(s));
         wait();  // nobody reuses its send buffer while a peer still copies from it

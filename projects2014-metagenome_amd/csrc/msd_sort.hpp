@@ -48,15 +48,18 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
                                                              uint64_t n, unsigned nbits,
                                                              unsigned b, unsigned bp,
                                                              uint32_t *__restrict__ counts,
-                                                             uint32_t tstride = 1, uint32_t slice = 1) {
+                                                             uint32_t tstride = 1, uint32_t slice = 1,
+                                                             uint32_t gtiles = 1) {
     // tstride > 1: a sample -- workgroup i counts tile i * tstride (msd_sort_unique's speculative
     // final level sizes its buckets from it); slice > 1: a finer sample -- workgroup i counts 1/slice
-    // of tile i, one line of every 8 * slice keys (previous-level buckets only a few tiles long, or
-    // a fraction of one, are still sampled evenly)
+    // of tiles i * gtiles .. + gtiles - 1, one line of every 8 * slice keys (previous-level buckets only
+    // a few tiles long, or a fraction of one, are still sampled evenly).  gtiles tiles share one LDS
+    // window flush: a sample of 1/8 of every tile flushing per tile cost as much as the full histogram
+    // (a 3-level round of configs[3]'s share: 9.7 vs 10.4 ms, its global atomics)
     constexpr int TILE = MsdTraits<L>::TILE;
     constexpr int WMAX = MSD_WIN << 8;
     __shared__ uint32_t s_cnt[WMAX];
-    const uint64_t base = (uint64_t)blockIdx.x * tstride * TILE;
+    const uint64_t base = (uint64_t)blockIdx.x * tstride * (slice > 1 ? gtiles : 1u) * TILE;
     const unsigned sub = b - bp;
     const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
     for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
@@ -74,16 +77,20 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
         // the finer sample spread over the whole tile: the first 64-byte line (8 keys) of every
         // 8 * slice keys, four lanes per line (a contiguous 1/slice prefix would miss previous-level
         // buckets that start late in the tile)
-        const uint64_t tend = min(n, base + TILE);
         const uint32_t lines = TILE / (8 * slice);
-        for (uint32_t j = threadIdx.x; j < 4 * lines; j += MSD_BLOCK) {
-            const uint64_t i = base + (uint64_t)(j >> 2) * (8 * slice) + 2 * (j & 3);
-            if (i + 1 < tend) {
-                const ulonglong2 v = *(const ulonglong2 *)(keys + i);
-                add(Key<L>::from(v.x));
-                add(Key<L>::from(v.y));
-            } else if (i < tend) {
-                add(keys[i]);
+        for (uint32_t t = 0; t < gtiles; ++t) {
+            const uint64_t tb = base + (uint64_t)t * TILE;
+            if (tb >= n) break;
+            const uint64_t tend = min(n, tb + TILE);
+            for (uint32_t j = threadIdx.x; j < 4 * lines; j += MSD_BLOCK) {
+                const uint64_t i = tb + (uint64_t)(j >> 2) * (8 * slice) + 2 * (j & 3);
+                if (i + 1 < tend) {
+                    const ulonglong2 v = *(const ulonglong2 *)(keys + i);
+                    add(Key<L>::from(v.x));
+                    add(Key<L>::from(v.y));
+                } else if (i < tend) {
+                    add(keys[i]);
+                }
             }
         }
       } else {  // 16-byte loads: two keys per lane
@@ -489,10 +496,10 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __shared__ Key<L> s_key[SLOTS];
     __shared__ uint16_t s_slot[LIST ? LIMIT : 1];
     // FAST (LIST only): a batch's loads without per-key bounds when the whole batch lies in the
-    // group, a probe loop without unrolled exit chains, and the batch's new keys take their list
-    // positions with one wave scan + one LDS atomic per wave and batch.  The kernel issues about as
-    // many SALU (divergence masks) as VALU instructions, and both pipes issue ~1 instruction per cycle
-    // per CU, so the loop's scalar bookkeeping is cut along with its vector work.
+    // group, and the batch's new keys take their list positions from the wave's ballots (no LDS) with
+    // one LDS atomic per wave and batch, instead of an LDS atomic + an LDS broadcast (ds_bpermute) per
+    // key slot.  The kernel's LDS pipe is its busiest (SQ_ACTIVE_INST_LDS ~ one wave per CU at all
+    // times at configs[1]), so LDS instructions are what this variant removes.
     static_assert(!FAST || (LIST && (SL & (SL - 1)) == 0), "FAST is the LIST path, power-of-two tables");
     __shared__ uint32_t s_state[KEYCAS ? 1 : SLOTS];
     __shared__ uint32_t s_sum[COUNTED ? SLOTS : 1];
@@ -545,10 +552,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         constexpr int PAIR = L == 1 ? 2 : 1;
         constexpr int BATCH = (LB >= 1024 ? 12 : WPE >= 8 ? 6 : 8) / PAIR;  // 6 at 64 VGPRs: 4.47 -> 4.19 ms
         const uint64_t a0 = PAIR == 2 ? (g0 & ~1ull) : g0;
-        // (FAST: the loop runs while any lane of the wave has keys, so the per-batch wave scan sees
-        // every lane; the lanes past the group's end load nothing)
-        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; FAST ? __ballot(ib < g1 && !ovf) != 0 : (ib < g1 && !ovf);
-             ib += (uint64_t)LB * BATCH * PAIR) {
+        for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += (uint64_t)LB * BATCH * PAIR) {
             Key<L> kb[BATCH * PAIR];
             uint32_t vb[BATCH * PAIR];
             bool hv[BATCH * PAIR];
@@ -628,67 +632,8 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             // batch instead of a chain per key, measured slower: 11.4 vs 10.5 ms sort stage, the
             // in-flight results spill at 64 VGPRs; 10.6 ms with 4-key batches)
             constexpr int NQ = BATCH * PAIR;
-            if constexpr (FAST) {
-                uint32_t insm = 0;  // bit q: key q was new (inserted at insh[q])
-                uint16_t insh[NQ];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const bool act = hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice);
-                    uint32_t h = slot_of<SLOTS>(key_hash(kb[q]));
-                    // st: 0 probing, 1 found, 2 inserted, 3 no key.  The loop runs while any lane of the
-                    // wave probes (a wave-uniform loop with one masked CAS block: few lane-mask merges)
-                    uint32_t st = act ? 0u : 3u;
-                    for (uint32_t probes = 0; __ballot(st == 0) != 0; ++probes) {
-                        if (probes >= SLOTS) {
-                            ovf = ovf || st == 0;
-                            break;
-                        }
-                        if (st == 0) {
-                            const uint64_t old = atomicCAS((unsigned long long *)&s_key[h].w[0],
-                                                           (unsigned long long)EMPTY, (unsigned long long)kb[q].w[0]);
-                            st = old == EMPTY ? 2u : old == kb[q].w[0] ? 1u : 0u;
-                            h = st ? h : (h + 1) & (SLOTS - 1);
-                        }
-                    }
-                    const bool isnew = st == 2;
-                    if (act && st != 0) {
-                        if (COUNTED) {
-                            const uint32_t add = vb[q];
-                            if (cmax <= 0xFFFFu) {
-                                const uint32_t o = atomicAdd(&s_sum[h], add);
-                                if (o + add > 0x40000000u) atomicMin(&s_sum[h], cmax);
-                            } else {
-                                uint32_t old = s_sum[h], assumed;
-                                do {
-                                    assumed = old;
-                                    const uint32_t nv = assumed > cmax - add ? cmax : assumed + add;
-                                    old = atomicCAS(&s_sum[h], assumed, nv);
-                                } while (old != assumed);
-                            }
-                        }
-                    }
-                    insh[q] = (uint16_t)h;
-                    insm |= (uint32_t)isnew << q;
-                }
-                // list positions: a wave scan of the new-key counts, one LDS atomic per wave
-                const uint32_t nins = (uint32_t)__popc(insm);
-                const uint32_t incl = wave_inclusive_sum(nins);
-                const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                if (wtot) {
-                    uint32_t wb = 0;
-                    if (__lane_id() == 63) wb = atomicAdd(&s_distinct, wtot);
-                    uint32_t pos = (uint32_t)__builtin_amdgcn_readlane((int)wb, 63) + incl - nins;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        if ((insm >> q) & 1u) {
-                            if (pos < LIMIT) s_slot[pos] = insh[q];
-                            else ovf = true;
-                            ++pos;
-                        }
-                    }
-                }
-                continue;
-            }
+            uint32_t dpos[FAST ? NQ : 1];  // FAST: (position in the batch << 16 | slot), ~0 = not new
+            uint32_t wnew = 0;             // FAST: new keys of the wave in this batch so far (uniform)
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 // LIST: the new keys of a wave take their list positions by ballot after the probe
@@ -745,7 +690,13 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                     }
                 }
                 }
-                if constexpr (LIST) {
+                if constexpr (FAST) {
+                    // deferred list positions: this key's rank among the batch's new keys of the wave
+                    // (ballots and popcounts, no LDS); one LDS atomic per wave and batch below
+                    const uint64_t m = __ballot(ins >= 0);
+                    dpos[q] = ins >= 0 ? ((wnew + (uint32_t)__popcll(m & lanemask_lt())) << 16 | (uint32_t)ins) : ~0u;
+                    wnew += (uint32_t)__popcll(m);
+                } else if constexpr (LIST) {
                     const uint64_t m = __ballot(ins >= 0);
                     if (m) {
                         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
@@ -755,6 +706,22 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                         const uint32_t pos = wb + (uint32_t)__popcll(m & lanemask_lt());
                         if (ins >= 0) {
                             if (pos < LIMIT) s_slot[pos] = (uint16_t)ins;
+                            else ovf = true;
+                        }
+                    }
+                }
+            }
+            if constexpr (FAST) {
+                if (wnew) {  // the batch's new keys of the wave: one LDS atomic, positions known
+                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1;
+                    uint32_t wb = 0;
+                    if (__lane_id() == leader) wb = atomicAdd(&s_distinct, wnew);
+                    wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, (int)leader);
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        if (dpos[q] != ~0u) {
+                            const uint32_t pos = wb + (dpos[q] >> 16);
+                            if (pos < LIMIT) s_slot[pos] = (uint16_t)(dpos[q] & 0xFFFFu);
                             else ovf = true;
                         }
                     }
@@ -946,7 +913,7 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     uint32_t *__restrict__ outc, uint32_t *__restrict__ gflag, uint32_t *__restrict__ ovf,
     unsigned b, unsigned nbits, unsigned ib, uint64_t *__restrict__ istart,
     const unsigned long long *__restrict__ gend = nullptr, const uint64_t *__restrict__ gbase = nullptr,
-    const uint64_t *__restrict__ cgap = nullptr, uint64_t g_base = 0) {
+    const uint64_t *__restrict__ cgap = nullptr, uint64_t g_base = 0, uint32_t it_min = 1) {
     // cgap (optional, one bucket per group): the canonical keys of bucket g are read at ck[cgap[g] ..)
     // (a set left in its speculative buckets) instead of ck[cstart[g] ..); cstart stays their compact
     // index
@@ -1031,9 +998,10 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         if (COUNTED) s_rv[b0 + rank] = s_sv[p];
     }
     __syncthreads();
-    // merge path over (s_r[0..nr), s_c[0..nc)): thread t writes outputs [t * IT, (t + 1) * IT)
+    // merge path over (s_r[0..nr), s_c[0..nc)): thread t writes outputs [t * IT, (t + 1) * IT).  it_min:
+    // at least that many outputs a thread (fewer diagonal searches of ~11 LDS steps, longer serial runs)
     const uint32_t n = nr + nc;
-    const uint32_t IT = (n + LB - 1) / LB;
+    const uint32_t IT = max((n + LB - 1) / LB, it_min);
     const uint32_t o0 = min(tid * IT, n), o1 = min(o0 + IT, n);
     uint32_t lo = o0 > nc ? o0 - nc : 0, hi = min(o0, nr);
     while (lo < hi) {

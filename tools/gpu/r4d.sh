@@ -2,7 +2,7 @@
 # Round 4: multi-GPU cost model per collect mode (serial dist_sim: per-rank device time alone, and the
 # bytes every rank sends), P = 2 (10 M reads per rank) and P = 8 (2.5 M reads per rank); P = 2 also with
 # the 9-bit routing digit (MTG_WIDE_B1=0).
-R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/r4d"; mkdir -p "$OUT"; cd "$R"
+R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/${TAG:-r4d}"; mkdir -p "$OUT"; cd "$R"
 run() {  # tag P N collect [env]
   env $5 timeout -k 10 300 python3 -u tools/dist_sim.py --ranks $2 --reads $3 --serial --collect $4 > "$OUT/$1.json" 2> "$OUT/$1.err" || { echo "$1 failed"; tail -5 "$OUT/$1.err"; exit 1; }
   python3 - "$OUT/$1.json" <<'PY'
