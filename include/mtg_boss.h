@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 5
+#define MTG_BOSS_ABI_VERSION 6
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -146,6 +146,8 @@ typedef struct mtg_boss_timings {
     uint64_t collect_mode;       /* how the real k-mers were collected: 0 one pass, 1 key ranges re-scanning
                                     the reads (both strands), 2 canonical rounds of the fused extraction */
     uint64_t sent_bytes;         /* multi-GPU: bytes this rank sent to the other ranks (every exchange) */
+    uint64_t spec_l1;            /* 1: the fused extraction scattered into the speculative level-1 layout
+                                    (a sampled histogram pass) */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);

@@ -87,7 +87,7 @@ class Timings(ctypes.Structure):
                [("n_batches", ctypes.c_uint64), ("peak_bytes", ctypes.c_uint64),
                 ("input_ms", ctypes.c_double), ("spilled_bytes", ctypes.c_uint64)] + \
                [(name, ctypes.c_uint64) for name in ("spec_levels", "spec_fine_levels", "spec_fallbacks",
-                                                      "collect_mode", "sent_bytes")]
+                                                      "collect_mode", "sent_bytes", "spec_l1")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -610,11 +610,17 @@ struct DummyTraits {
 // ABL (timing ablations for tools/stage_bench only; 0 in the product): bit 0 = no in_flag stores,
 // bit 1 = no flags stores, bit 2 = no staging and no search (every edge a sink), bit 3 = staging
 // but no search
+// q (the multi-GPU build, run_pipeline_dist): the probes look up a separate sorted array q[0..nq) --
+// the edges of other ranks whose nodes this rank's edges target -- whose bucket index is `start`;
+// in_flag then marks q's edges.  Without q the probes look up keys itself.
 template <int L, int ABL = 0>
 __global__ __launch_bounds__(256) void dummy_sink_kernel(
     const Key<L> *__restrict__ keys, uint64_t n, unsigned K, const uint64_t *__restrict__ start,
-    unsigned bshift, uint8_t *__restrict__ flags, uint8_t *__restrict__ in_flag) {
+    unsigned bshift, uint8_t *__restrict__ flags, uint8_t *__restrict__ in_flag,
+    const Key<L> *__restrict__ q = nullptr, uint64_t nq = 0) {
     using T = DummyTraits<L>;
+    const Key<L> *__restrict__ look = q ? q : keys;
+    const uint64_t nl = q ? nq : n;
     constexpr int PER = T::PER;
     __shared__ Key<L> s_r[T::CAP];
     __shared__ uint64_t s_lo[4];
@@ -667,7 +673,7 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         if (s_off[c] == ~0u) continue;
         const uint64_t a = s_lo[c];
         const uint32_t off = s_off[c];
-        for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = keys[a + j];
+        for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = look[a + j];
     }
     __syncthreads();
 #pragma unroll
@@ -691,8 +697,8 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
             }
             if (lo < cnt && shr(s_r[off + lo], 2) == shr(p, 2)) hit = s_lo[c] + lo;
         } else {
-            const uint64_t i = lower_bound_bucketed(keys, start, bshift, p);
-            if (i < n && shr(keys[i], 2) == shr(p, 2)) hit = i;
+            const uint64_t i = lower_bound_bucketed(look, start, bshift, p);
+            if (i < nl && shr(look[i], 2) == shr(p, 2)) hit = i;
         }
         if (!(ABL & 1) && hit != ~0ull) in_flag[hit] = 1;
         if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)((hit == ~0ull ? 1u : 0u) | (((first >> q) & 1u) << 1));

@@ -65,7 +65,7 @@ class Workspace {
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
-        FUSED_SEL, WN, SPEC_AC, SPEC_BC, NSLOTS
+        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -262,6 +262,9 @@ struct Ctx {
     bool kmc_mirror = true;  // add_kmc copies the first database to the device while reading it
                                    // that re-scan the reads (both strands) even where the canonical
                                    // rounds of the fused K1 apply (collect_rounds_fused)
+    bool kspec = true;             // MTG_KSPEC=0: the fused K1 passes with K a runtime argument at K = 31 too
+    bool dist_pull = true;         // MTG_DIST_SINKS=query: the multi-GPU sink join by routed queries
+                                   // (target_split + query_join) instead of the pulled edge slices
     bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
                                    // dense u64 ranks (dummy_encode_kernel)
     // bucket index of the last msd_sort_unique's output over its final bucket bits, when every group
@@ -297,6 +300,17 @@ struct Ctx {
                              // sample-sized one (spec_final_level)
     bool spec_tiny = false;  // MTG_SPEC_CAPS=tiny: speculative buckets without slack (tests force the
                              // overflow fallback with it)
+    // MTG_SPEC_L1=0: the exact fused pass A (a histogram of every window) instead of the sampled one
+    // and the speculative level-1 layout (fused_pass_b_spec), used from MTG_SPEC_L1_MIN windows on;
+    // MTG_SPEC_L1_SAMPLE: pass A counts every n-th tile
+    bool spec_l1 = true;
+    bool spec_l1_tiny = false;  // MTG_SPEC_L1_CAPS=tiny: segments without slack (tests force its fallback)
+    uint64_t spec_l1_min = 1ull << 28;
+    uint32_t spec_l1_sample = 8;
+    // the speculative level-1 layout of the last fused K1 until the level-2 pass has read it: gap1_n
+    // positions, tile t of the level-2 tiling holding keys in its first gap1_tv[t] positions
+    uint64_t gap1_n = 0;
+    const uint32_t *gap1_tv = nullptr;
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
     const void *bidx_keys = nullptr;
     uint64_t bidx_n = 0;
@@ -330,6 +344,12 @@ static void load_knobs(Ctx &c) {
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
     c.spec_tiny = is("MTG_SPEC_CAPS", "tiny");
+    c.spec_l1 = !is("MTG_SPEC_L1", "0");
+    c.dist_pull = !is("MTG_DIST_SINKS", "query");
+    c.kspec = !is("MTG_KSPEC", "0");
+    c.spec_l1_tiny = is("MTG_SPEC_L1_CAPS", "tiny");
+    if (const char *e = getenv("MTG_SPEC_L1_MIN")) c.spec_l1_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("MTG_SPEC_L1_SAMPLE")) c.spec_l1_sample = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_MSD_LEVELS")) c.min_levels = (unsigned)std::min(3, std::max(0, atoi(v)));
     c.dist_collect = is("MTG_DIST_COLLECT", "superkmer") ? 0 : is("MTG_DIST_COLLECT", "local") ? 2 : 1;
     c.routed_min = is("MTG_ROUTED_CANON", "min");
@@ -618,8 +638,15 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             return ~0ull;
         constexpr uint32_t SS = 8;
         constexpr int TILE = MsdTraits<L>::TILE;
-        const uint64_t tiles = ceil_div(n, TILE);
+        // after a speculative level-1 layout the input is the padded array (Ctx::gap1_n)
+        const bool g1 = bp && c.gap1_n && !rm;
+        const uint64_t npos = g1 ? c.gap1_n : n;
+        const uint32_t *tv = g1 ? c.gap1_tv : nullptr;
+        const uint64_t tiles = ceil_div(npos, TILE);
         if (c.use_lsd || !c.spec_final || tiles < 64 * SS || bb - bp > 9 || bb > 24) return ~0ull;
+        // a padded input samples every tile: its tiles' fills differ (segment tails, empty tiles), so a
+        // tile-granular sample sized the buckets badly (overflow at 2 M reads)
+        if (g1) fine = true;
         const uint64_t nb = 1ull << bb;
         // the two slack-sized buffers must fit next to everything else
         {
@@ -636,11 +663,12 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // tile (level-2 buckets can be only a few tiles long, and a tile-granular sample missed them)
         constexpr uint32_t GT = 8;  // fine sample: tiles per workgroup (one LDS window flush)
         msd_hist_kernel<L><<<dim3((unsigned)(fine ? ceil_div(tiles, GT) : ceil_div(tiles, SS))), dim3(MSD_BLOCK), 0,
-                             c.stream>>>(*keys, n, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1, fine ? GT : 1);
+                             c.stream>>>(*keys, npos, nbits, bb, bp, h, fine ? 1 : SS, fine ? SS : 1, fine ? GT : 1, tv);
         HIP_CHECK(hipGetLastError());
         // the buckets the keys can occupy: those under the previous level's first and last prefix
+        // (a padded input's ends are not keys: every bucket)
         uint64_t blo = 0, bhi = nb;
-        if (bp) {
+        if (bp && !g1) {
             Key<L> ends[2];
             HIP_CHECK(hipMemcpyAsync(&ends[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
             HIP_CHECK(hipMemcpyAsync(&ends[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
@@ -684,8 +712,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         EventTimer tm(c.stream);
         tm.mark();
         msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
-            *keys, sa, COUNTED ? *vals : nullptr, sac, n, nbits, bb, bp, cur, 1,
-            (const unsigned long long *)(bstart + 1), &c.small->spec_ovf);
+            *keys, sa, COUNTED ? *vals : nullptr, sac, npos, nbits, bb, bp, cur, 1,
+            (const unsigned long long *)(bstart + 1), &c.small->spec_ovf, tv);
         HIP_CHECK(hipGetLastError());
         tm.mark();
         uint32_t povf = 0;
@@ -702,6 +730,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             ++c.timings.spec_fallbacks;
             return ~0ull;
         }
+        if (g1) c.gap1_n = 0, c.gap1_tv = nullptr;  // read: the buckets below are compact per bucket
         if (rm) {  // the fused rc merge over the speculative buckets
             uint32_t *cnt = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
             spec_counts_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(bstart, cur, nb, cnt);
@@ -896,6 +925,10 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         const unsigned bb = digit_end[lev], bp = digit_end[lev - 1];
         nbuckets = 1ull << bb;
         const uint32_t *cnt = hist1;
+        // level 2 after a speculative level-1 layout reads the padded array (c.gap1_n positions)
+        const bool g1 = lev == 2 && level1_done && c.gap1_n;
+        const uint64_t npos = g1 ? c.gap1_n : n, ltiles = g1 ? ceil_div(npos, TILE) : tiles;
+        const uint32_t *tv = g1 ? c.gap1_tv : nullptr;
         if (lev != 1 || !hist1) {
             uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nbuckets * 4);
             HIP_CHECK(hipMemsetAsync(h, 0, nbuckets * 4, c.stream));
@@ -907,7 +940,8 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbuckets, 256)),
                                           dim3(256), 0, c.stream>>>(rows, nrows, (uint32_t)nbuckets, h);
             } else {
-                msd_hist_kernel<L><<<dim3((unsigned)tiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, h);
+                msd_hist_kernel<L><<<dim3((unsigned)ltiles), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, npos, nbits, bb, bp,
+                                                                                             h, 1, 1, 1, tv);
             }
             HIP_CHECK(hipGetLastError());
             cnt = h;
@@ -932,9 +966,11 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         // cfg2 level-2 pass vs 4.09 with 1024-thread tiles (16 K keys, one per CU) -- before the XCD
         // mapping the longer runs of the big tiles won (4.65 vs 5.3 ms); nontemporal access measured
         // the same (tools/part_bench.hip)
-        msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
-            *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, n, nbits, bb, bp, cur);
+        msd_partition_kernel<L, COUNTED><<<dim3((unsigned)xcd_grid(ltiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, npos, nbits, bb, bp, cur, 1, nullptr,
+            nullptr, tv);
         HIP_CHECK(hipGetLastError());
+        if (g1) c.gap1_n = 0, c.gap1_tv = nullptr;  // compact from here on
         tm.mark();
         if (c.track_partition && c.radix_launches == 0) {  // first partition launch of the sort
             HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -1406,6 +1442,7 @@ struct FusedA {
     uint32_t nrows = 0, rps = 0, stripes = 0;
     uint64_t per_stripe = 0;
     uint32_t *rows = nullptr;  // per-row histograms (device), rps rows per stripe of pass-B tiles
+    double sample_factor = 1.0;  // tiles per sampled tile of pass A (fused_pass_a with sample > 1)
     std::vector<uint32_t> h;   // their sum over the 2^FUSED_HB top-bit bins (host)
 };
 
@@ -1415,7 +1452,22 @@ static bool fused_applies(const Ctx &c, unsigned K, uint64_t npos) {
 
 // pass A over every window, and the duplication estimate from a sample of windows (on a side stream
 // it overlapped pass A but measured no faster: 26.3 vs 26.2 ms per step)
-static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &in, FusedA *A) {
+// the fused passes with K = 31 compiled in (KC, extract_partition.hpp) unless MTG_KSPEC=0
+template <bool OTHER, typename... A>
+static void launch_hist_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, A... a) {
+    if (K == 31 && c.kspec) extract_hist_fast_kernel<OTHER, 31><<<g, b, 0, c.stream>>>(a...);
+    else extract_hist_fast_kernel<OTHER, 0><<<g, b, 0, c.stream>>>(a...);
+}
+template <int BLOCK, int NB, typename... A>
+static void launch_part_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, A... a) {
+    if (K == 31 && c.kspec) extract_partition_fast_kernel<BLOCK, NB, 31><<<g, b, 0, c.stream>>>(a...);
+    else extract_partition_fast_kernel<BLOCK, NB, 0><<<g, b, 0, c.stream>>>(a...);
+}
+
+// sample > 1 (fused_pass_b_spec): every row counts every sample-th of its tiles, and the rows form
+// kSpecStripes stripes of kSpecRps rows each (A->h, A->N are then estimates)
+constexpr uint32_t kSpecStripes = 16, kSpecRps = 128;
+static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &in, FusedA *A, uint32_t sample = 1) {
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
     unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
@@ -1444,11 +1496,23 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
     // [r per_row, (r + 1) per_row), so rows rps s .. rps s + rps - 1 cover stripe s.  One stripe
     // (fewer rows than rps) takes every row, each an equal share of the tiles.
     const uint64_t tiles_b = ceil_div(npos, (uint64_t)16 * fbk);
-    const uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
-    const uint64_t per_stripe = ceil_div(tiles_b, stripes);
-    const uint64_t per_row = stripes == 1 ? ceil_div(tiles_b * rps, nrows) : per_stripe;
-    extract_hist_fast_kernel<<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
-                                                                   tiles, per_row, rows);
+    uint32_t stripes = std::max<uint32_t>(1, nrows / rps);
+    uint64_t per_stripe = ceil_div(tiles_b, stripes);
+    uint64_t per_row = stripes == 1 ? ceil_div(tiles_b * rps, nrows) : per_stripe;
+    uint32_t rps_out = rps;
+    if (sample > 1) {
+        // kSpecStripes stripes of kSpecRps rows: row r counts the pass-A tiles [r per_row, (r + 1) per_row),
+        // so stripe s (pass-B tiles [s per_stripe, (s + 1) per_stripe), 2 pass-A tiles each) is rows
+        // s kSpecRps .. + kSpecRps - 1
+        nrows = kSpecStripes * kSpecRps;
+        rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
+        per_row = ceil_div(tiles, nrows);
+        per_stripe = kSpecRps * per_row / 2;  // kSpecRps is even
+        stripes = (uint32_t)ceil_div(tiles_b, per_stripe);
+        rps_out = kSpecRps;
+    }
+    launch_hist_fast<false>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, canonical ? 1 : 0, tiles, per_row, rows,
+                            (uint32_t *)nullptr, sample);
     HIP_CHECK(hipGetLastError());
     hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
                               c.stream>>>(rows, nrows, nbh, h12);
@@ -1460,13 +1524,16 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
     HIP_CHECK(hipStreamSynchronize(c.stream));
     uint64_t N = 0;
     for (uint32_t v : A->h) N += v;
+    // a row samples ceil(per_row / sample) of its per_row tiles
+    A->sample_factor = sample > 1 ? (double)per_row / (double)ceil_div(per_row, sample) : 1.0;
+    N = (uint64_t)((double)N * A->sample_factor);
     const double mv = (double)std::max<unsigned long long>(st[1], 1);
     const double ew = 2.0 * (double)N * (double)st[0] / (mv * mv);
     A->npos = npos;
     A->N = N;
     A->dup = N >= 16ull * M ? std::max(1.0, ew / 1.2) : 8.0;
     A->nrows = nrows;
-    A->rps = rps;
+    A->rps = rps_out;
     A->stripes = stripes;
     A->per_stripe = per_stripe;
     A->rows = rows;
@@ -1526,14 +1593,13 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     const bool fast_b = !COUNTED && K <= 32;
     if (fast_b) {
         constexpr int B = 512;
+        const dim3 g((unsigned)xcd_grid(ceil_div(A.npos, 16 * B)));
         if (b1 > 9)
-            extract_partition_fast_kernel<B, 1024><<<dim3((unsigned)xcd_grid(ceil_div(A.npos, 16 * B))), dim3(B), 0,
-                                                      c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1,
-                                                                  A.per_stripe, scur, send, ka, &c.small->error, dsel);
+            launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur,
+                                      send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr);
         else
-            extract_partition_fast_kernel<B><<<dim3((unsigned)xcd_grid(ceil_div(A.npos, 16 * B))), dim3(B), 0,
-                                                c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe,
-                                                            scur, send, ka, &c.small->error, dsel);
+            launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur,
+                                     send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr);
     } else {
         if (b1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, 512>::TILE);
@@ -1552,6 +1618,88 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     return acc;
 }
 
+// Pass B into the speculative level-1 layout (extract_partition.hpp: spec_l1_caps_kernel) after a
+// sampled pass A (fused_pass_a with sample > 1): no exact histogram pass over every window (pass A:
+// 1.29 ms at configs[1]).  Segments of (bucket, stripe) sized from the sample with slack, each a whole
+// number of level-2 tiles; the level-2 pass reads the padded array through tvalid (c.gap1).  Returns
+// the k-mer count with the exact level-1 counts in *dh1_out, or ~0 when a segment overflowed (nothing
+// the caller needs was touched: it runs the exact passes).
+static uint64_t fused_pass_b_spec(Ctx &c, unsigned K, bool canonical, const BuildInput &in, const FusedA &A,
+                                  unsigned b1, Key<1> **ka, Key<1> **kb, const uint32_t **dh1_out) {
+    const uint32_t nb1 = 1u << b1, S = A.stripes;
+    constexpr uint32_t T2 = MsdTraits<1>::TILE;
+    const uint64_t nseg = (uint64_t)nb1 * S;
+    uint32_t *caps = (uint32_t *)c.ws.get(Workspace::SPEC1_CAPS, (nseg + 1) * 4);
+    uint64_t *sst = (uint64_t *)c.ws.get(Workspace::SPEC1_START, (nseg + 1) * 8);
+    spec_l1_caps_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(A.rows, A.nrows, FUSED_HB, b1, S, A.rps,
+                                                               (float)A.sample_factor, T2, caps, c.spec_l1_tiny);
+    HIP_CHECK(hipGetLastError());
+    {
+        uint32_t ep;
+        const uint64_t st = ceil_div(nseg, 4096);
+        uint64_t *desc = acquire_desc(c, st, &ep);
+        HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+        scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(caps, nseg, sst, desc, ep, &c.small->counter,
+                                                                          &c.small->error);
+        HIP_CHECK(hipGetLastError());
+    }
+    const uint64_t C1 = read_u64(c, (const unsigned long long *)(sst + nseg));
+    if (C1 % T2) throw std::logic_error("spec level 1: segments not tile-aligned");
+    {  // the padded array and its ping-pong buffer must fit next to everything else
+        const uint64_t fr = c.ws.free_bytes();
+        const double need = 16.0 * (double)C1, have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::KA) +
+                                                       (double)c.ws.held_slot(Workspace::KB);
+        if (need > have) return ~0ull;
+    }
+    *ka = (Key<1> *)c.ws.get(Workspace::KA, std::max<uint64_t>(C1, 1) * 8);
+    *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(C1, 1) * 8);
+    auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, nseg * 16);
+    unsigned long long *send = scur + nseg;
+    spec_l1_cursor_kernel<<<dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, c.stream>>>(sst, caps, nb1, S, scur,
+                                                                                          send);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemsetAsync(&c.small->spec_ovf, 0, 4, c.stream));
+    EventTimer tm(c.stream);
+    tm.mark();
+    constexpr int B = 512;
+    const dim3 g((unsigned)xcd_grid(ceil_div(A.npos, 16 * B)));
+    if (b1 > 9)
+        launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send,
+                                  *ka, &c.small->error, (const uint32_t *)nullptr, &c.small->spec_ovf);
+    else
+        launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send,
+                                 *ka, &c.small->error, (const uint32_t *)nullptr, &c.small->spec_ovf);
+    HIP_CHECK(hipGetLastError());
+    tm.mark();
+    const uint64_t ntile2 = C1 / T2;
+    uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
+    uint32_t *tv = (uint32_t *)c.ws.get(Workspace::SPEC1_TV, std::max<uint64_t>(ntile2, 1) * 4);
+    HIP_CHECK(hipMemsetAsync(dh1, 0, nb1 * 4, c.stream));
+    HIP_CHECK(hipMemsetAsync(&c.small->total, 0, 8, c.stream));
+    spec_l1_finish_kernel<<<dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, c.stream>>>(sst, caps, scur, nb1, S, T2,
+                                                                                          dh1, tv, &c.small->total);
+    HIP_CHECK(hipGetLastError());
+    uint32_t povf = 0;
+    uint64_t N = 0;
+    HIP_CHECK(hipMemcpyAsync(&povf, &c.small->spec_ovf, 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipMemcpyAsync(&N, &c.small->total, 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.fused_ms = tm.ms(0, 1);
+    if (povf) {
+        if (c.debug) fprintf(stderr, "[mtg debug] speculative level 1: a segment overflowed, exact passes\n");
+        ++c.timings.spec_fallbacks;
+        return ~0ull;
+    }
+    c.gap1_n = C1;
+    c.gap1_tv = tv;
+    c.timings.spec_l1 = 1;
+    if (c.debug)
+        fprintf(stderr, "[mtg debug] speculative level 1: N=%lu (sample %lu) padded %lu (%.3fx), %u stripes\n",
+                (unsigned long)N, (unsigned long)A.N, (unsigned long)C1, (double)C1 / (double)std::max<uint64_t>(N, 1), S);
+    *dh1_out = dh1;
+    return N;
+}
+
 // Returns false (nothing done) when the fused path does not apply; else N, the duplication
 // estimate, and the level-1 counts in *hist1 (device) with *ka scattered.
 template <int L2, bool COUNTED>
@@ -1564,6 +1712,31 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
         if (!fused_applies(c, K, npos)) return false;
         FusedA A;
+        // the speculative level-1 layout: uncounted single builds big enough that a sample sizes the
+        // segments well (the rounds and the multi-GPU collect keep the exact passes)
+        const bool spec1 = !COUNTED && K <= 32 && c.spec_l1 && npos >= c.spec_l1_min;
+        c.gap1_n = 0;
+        c.gap1_tv = nullptr;
+        if (spec1) {
+            fused_pass_a(c, K, canonical, in, &A, c.spec_l1_sample);
+            const MsdPlan plan = fused_plan(c, A.N, 2 * K, A.dup, true);
+            if (plan.levels == 2) {
+                const uint64_t N = fused_pass_b_spec(c, K, canonical, in, A, plan.digit_end[1], ka, kb, hist1_out);
+                if (c.debug)
+                    fprintf(stderr, "[mtg debug] fused extract (sampled) N=%lu dup=%.2f levels=%u digit1=%u\n",
+                            (unsigned long)A.N, A.dup, plan.levels, plan.digit_end[1]);
+                if (N != ~0ull) {
+                    c.timings.n_positions = npos;
+                    c.timings.n_extracted = N;
+                    *ca = *cb = nullptr;
+                    *N_out = N;
+                    *dup_out = A.dup;
+                    *plan_out = plan;
+                    return true;
+                }
+            }
+            A = FusedA{};
+        }
         fused_pass_a(c, K, canonical, in, &A);
         const uint64_t N = A.N;
         const MsdPlan plan = fused_plan(c, N, 2 * K, A.dup, !COUNTED && K <= 32);
@@ -1594,6 +1767,7 @@ static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, K
                               const uint32_t *hist1 = nullptr, const MsdPlan *plan = nullptr) {
     // hist1 != nullptr: *ka is already scattered by the level-1 digit (stage_extract_fused)
     uint64_t U = 0;
+    if (!hist1) c.gap1_n = 0, c.gap1_tv = nullptr;
     if (c.use_lsd) {
         radix_sort<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, track);
         reset_small(c);
@@ -2805,8 +2979,8 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     uint32_t *h12 = (uint32_t *)c.ws.get(Workspace::FUSED_HIST, 2 * NBH * 4);
     HIP_CHECK(hipMemsetAsync(h12, 0, 2 * NBH * 4, c.stream));
     if (nrows) {
-        extract_hist_fast_kernel<true><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, cmode,
-                                                                             tiles, per_row, rows, rows_o);
+        launch_hist_fast<true>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, cmode, tiles, per_row, rows, rows_o,
+                               1u);
         HIP_CHECK(hipGetLastError());
         hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(NBH, 256)), dim3(256), 0,
                                   c.stream>>>(rows, nrows, NBH, h12);
@@ -2947,13 +3121,13 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
                                                                          scur, send, dsel);
             HIP_CHECK(hipGetLastError());
             if (!COUNTED && B1 > 9) {
-                extract_partition_fast_kernel<512, 1024><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512),
-                                                            0, c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
-                                                                           scur, send, ka, &c.small->error, dsel);
+                launch_part_fast<512, 1024>(c, K, dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), in.seq,
+                                            in.seq_len, K, cmode, B1, per_stripe, scur, send, ka, &c.small->error,
+                                            (const uint32_t *)dsel, (uint32_t *)nullptr);
             } else if (!COUNTED) {
-                extract_partition_fast_kernel<512><<<dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), 0,
-                                                      c.stream>>>(in.seq, in.seq_len, K, cmode, B1, per_stripe,
-                                                                  scur, send, ka, &c.small->error, dsel);
+                launch_part_fast<512, 512>(c, K, dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), in.seq,
+                                           in.seq_len, K, cmode, B1, per_stripe, scur, send, ka, &c.small->error,
+                                           (const uint32_t *)dsel, (uint32_t *)nullptr);
             } else {
                 if (B1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
                 const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
@@ -3337,6 +3511,10 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
             K2 *ralt = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(nrc, 1) * sizeof(K2));
             uint32_t *rcalt = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(nrc, 1) * 4) : nullptr;
             RcMerge<L2> rm{xa, xac, U, out, outc};
+            // the dummy stage's and the split emit's bucket index of the owned edges comes out of the
+            // fused merge (as in the single build), sized for R = U + nrc
+            rm.ib = bucket_bits<L2>(U + nrc, 2 * K);
+            rm.istart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << rm.ib) + 2) * 8);
             const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + U)) : 1.0;
             uint64_t nr = 0;
             if (nrc)
@@ -3360,6 +3538,118 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     if (d.P == 1) {  // one rank owns every target node: the single build's local join
         D = stage_dummies_local<L2, L3>(c, K, E, R, &dk);
         tr("dummies (local)", D);
+    } else if (c.dist_pull && d.m + 1 <= k_b) {
+        // the pulled sink join (dist_kernels.hpp: pull_bounds_kernel): every rank sends each owner the
+        // slices of its edges whose nodes the owner's edges target, the owner runs the single build's
+        // join (dummy_sink_kernel) of its edges against them and returns an in-edge byte per received
+        // edge; sinks and sources are then written like the single build's and routed to their owners
+        uint8_t *flags = (uint8_t *)c.ws.get(Workspace::FLAGS, R + 1);
+        std::vector<std::vector<uint64_t>> qoff(4, std::vector<uint64_t>(d.P + 1, 0));
+        std::vector<uint64_t> cstart(5, R);
+        cstart[0] = 0;
+        if (R) {
+            uint64_t *db = (uint64_t *)c.ws.get(Workspace::BOUNDS, (d.P + 1) * 8);
+            uint64_t *g = (uint64_t *)c.ws.get(Workspace::XGATHER, 4 * (d.P + 1) * 8);
+            HIP_CHECK(hipMemcpyAsync(db, bounds.data(), (d.P + 1) * 8, hipMemcpyHostToDevice, c.stream));
+            pull_bounds_kernel<L2><<<dim3((unsigned)ceil_div(4 * (d.P + 1), 256)), dim3(256), 0, c.stream>>>(
+                E, R, db, (uint32_t)d.P, K, d.m, g);
+            HIP_CHECK(hipGetLastError());
+            std::vector<uint64_t> pos(4 * (d.P + 1));
+            HIP_CHECK(hipMemcpyAsync(pos.data(), g, pos.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));  // bounds / pos are host locals
+            for (int cl = 0; cl < 4; ++cl) {
+                cstart[cl] = pos[cl * (d.P + 1)];
+                for (int j = 0; j <= d.P; ++j) qoff[cl][j] = pos[cl * (d.P + 1) + j] - cstart[cl];
+            }
+            if (cstart[0] != 0 || pos[3 * (d.P + 1) + d.P] != R)
+                throw std::logic_error("pulled join: the class slices do not cover the edges");
+        }
+        tr("pull bounds", R);
+        K2 *qr;
+        uint32_t *unused_c = nullptr;
+        const K2 *qarr[4] = {E + cstart[0], E + cstart[1], E + cstart[2], E + cstart[3]};
+        std::vector<uint64_t> qruns;
+        const uint64_t nq = exchange_runs<K2>(c, d, 4, qarr, nullptr, qoff, Workspace::QRECV, Workspace::XAC, &qr,
+                                              &unused_c, &qruns);
+        tr("exchange pulled edges", nq);
+        // the received edges are sorted (array-major = by top char, then by source rank = key order)
+        const unsigned QB = bucket_bits<L2>(nq, 2 * K);
+        const unsigned qshift = 2 * K - QB;
+        uint64_t *qstart = (uint64_t *)c.ws.get(Workspace::QINDEX, ((1ull << QB) + 2) * 8);
+        bucket_index<L2>(c, qr, nq, qshift, 1ull << QB, qstart);
+        uint8_t *qin = (uint8_t *)c.ws.get(Workspace::QFLAG, nq + 1);
+        if (nq) HIP_CHECK(hipMemsetAsync(qin, 0, nq, c.stream));
+        if (R) {
+            dummy_sink_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0, c.stream>>>(
+                E, R, K, qstart, qshift, flags, qin, qr, nq);
+            HIP_CHECK(hipGetLastError());
+        }
+        tr("pulled join", nq);
+        // exchange back: the in-edge byte of every received edge to its sender, where the 4 x P pieces
+        // land aligned with the sender's edge array (its classes in order, each by owner)
+        std::vector<std::vector<uint64_t>> boff(4, std::vector<uint64_t>(d.P + 1, 0));
+        const uint8_t *barr[4];
+        for (int cl = 0; cl < 4; ++cl) {
+            const uint64_t b0 = qruns[cl * d.P];
+            barr[cl] = qin + b0;
+            for (int i = 0; i < d.P; ++i) boff[cl][i] = qruns[cl * d.P + i] - b0;
+            boff[cl][d.P] = qruns[(cl + 1) * d.P] - b0;  // the next class's first run (or the total)
+        }
+        uint8_t *in_flag;
+        uint32_t *unused_b = nullptr;
+        const uint64_t nback = exchange_runs<uint8_t>(c, d, 4, barr, nullptr, boff, Workspace::INFLAG, Workspace::XAC,
+                                                      &in_flag, &unused_b);
+        if (nback != R) throw std::logic_error("pulled join: in-edge bytes do not match the edges");
+        tr("exchange in-edge bytes", nback);
+        // the bucket index of the owned edges, for the split emit's dummy ranks (unless the fused rc
+        // merge wrote it)
+        if (!(c.bidx_keys == (const void *)E && c.bidx_n == R)) {
+            const unsigned B = bucket_bits<L2>(R, 2 * K);
+            const unsigned bshift = 2 * K - B;
+            uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << B) + 2) * 8);
+            bucket_index<L2>(c, E, R, bshift, 1ull << B, bstart);
+            note_bucket_index(c, E, R, bstart, bshift);
+        }
+        // sinks (lift(to_next(x, 0)) with label $) and sources of every level, as the single build writes
+        // them, routed to the owners of their lifted prefixes
+        const uint64_t wtiles = ceil_div(R, DummyTraits<L2>::WTILE);
+        uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
+        uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (wtiles + 1) * 8);
+        uint64_t nraw = 0;
+        if (R) {
+            dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, k_b, tcnt);
+            HIP_CHECK(hipGetLastError());
+            uint32_t ep;
+            const uint64_t st = ceil_div(wtiles, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(tcnt, wtiles, toff, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+            nraw = read_u64(c, (const unsigned long long *)(toff + wtiles));
+        }
+        K3 *src = (K3 *)c.ws.get(Workspace::DSRC, std::max<uint64_t>(nraw, 1) * sizeof(K3));
+        if (nraw) {
+            dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(E, flags, in_flag, R, K,
+                                                                                            toff, src);
+            HIP_CHECK(hipGetLastError());
+        }
+        tr("sinks + sources", nraw);
+        K3 *ssend = (K3 *)c.ws.get(Workspace::DSEND, std::max<uint64_t>(nraw, 1) * sizeof(K3));
+        std::vector<std::vector<uint64_t>> doff(1);
+        doff[0] = route<L3, 1>(c, d, src, nraw, K, 3 * K - 3 * d.m, 3 * d.m, lifted_bounds(bounds, d.m), ssend);
+        K3 *drecv;
+        const K3 *darr[1] = {ssend};
+        const uint64_t Draw = exchange_runs<K3>(c, d, 1, darr, nullptr, doff, Workspace::DRECV, Workspace::XAC, &drecv,
+                                                &unused_c);
+        tr("route + exchange dummies", Draw);
+        if (Draw) {
+            K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
+            K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));
+            HIP_CHECK(hipMemcpyAsync(da, drecv, Draw * sizeof(K3), hipMemcpyDeviceToDevice, c.stream));
+            D = sort_unique_dummies<L3>(c, K, da, db, Draw, &dk);
+            tr("dummy sort", D);
+        }
     } else {
         const unsigned B = bucket_bits<L2>(R, 2 * K);
         const unsigned bshift = 2 * K - B;

@@ -445,6 +445,35 @@ __global__ __launch_bounds__(256) void query_join_kernel(const Key<L> *__restric
     }
 }
 
+/*
+ * The pulled sink join (run_pipeline_dist): instead of sending every edge's query to the owner of its
+ * target node, every rank sends each owner j the edges y whose NODE some edge of j targets: x = (a_1
+ * .. a_k; label c) targets node (a_2 .. a_k, c), whose edges y have top char c and then a_k, a_(k-1),
+ * .. -- so y goes to the owner of the m-char prefix below y's top char, i.e. of y's (m+1)-char prefix
+ * minus c 4^m.  Within one top char c that prefix is monotone along the sorted edges, so every
+ * (class c, owner j) share is a contiguous slice: out[c * (P + 1) + j] = the first edge with top char
+ * c whose (m+1)-char prefix is >= c 4^m + bounds[j] (bounds[0] = 0, bounds[P] = 4^m).  Each edge is
+ * sent once, unchanged (no split pass, no to_next transform); the owner receives its 4 classes' slices
+ * from every rank sorted (array-major, then by source rank), probes them with its own edges
+ * (dummy_sink_kernel with q), and returns one in-edge byte per received edge, which arrives aligned
+ * with the sender's edge array.
+ */
+template <int L>
+__global__ void pull_bounds_kernel(const Key<L> *__restrict__ e, uint64_t n, const uint64_t *__restrict__ bounds,
+                                   uint32_t P, unsigned K, unsigned m, uint64_t *__restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 4 * (P + 1)) return;
+    const uint32_t c = t / (P + 1), j = t % (P + 1);
+    const uint64_t v = ((uint64_t)c << (2 * m)) + bounds[j];
+    const unsigned sh = 2 * K - 2 * (m + 1);  // (m+1)-char prefix = key >> sh
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (bits_at(shr(e[mid], sh), 0, 2 * (m + 1)) < v) lo = mid + 1; else hi = mid;
+    }
+    out[t] = lo;
+}
+
 // first query index of every owner in every class: out[c * (P + 1) + j] = lower bound of the prefix
 // bounds[j] in the sorted class array [cstart[c], cstart[c + 1])
 template <int L>

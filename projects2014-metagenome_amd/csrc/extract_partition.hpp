@@ -91,11 +91,18 @@ __device__ __forceinline__ uint32_t rc_word(uint32_t w) {
 // OTHER (the multi-GPU build): also rows_other, the histogram of the top bits of the other strand's
 // key of every canonical window (its reverse complement: max(fwd, rc)), so the owner ranges can be
 // balanced on the real edges (both strands) as well as on the canonical k-mers.
-template <bool OTHER = false>
+// KC (both fused passes): the window length K as a compile-time constant (0 = the runtime argument);
+// the host instantiates KC = 31, the k = 30 BOSS build of BASELINE configs[1] / [3], so the 64-bit masks
+// and shifts of the window loop fold into immediates
+template <bool OTHER = false, int KC = 0>
 __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
-                                                                unsigned K, int canonical, uint64_t ntiles,
+                                                                unsigned K_, int canonical, uint64_t ntiles,
                                                                 uint64_t per_row, uint32_t *__restrict__ rows,
-                                                                uint32_t *__restrict__ rows_other = nullptr) {
+                                                                uint32_t *__restrict__ rows_other = nullptr,
+                                                                uint32_t tstride = 1) {
+    // tstride > 1: a sample -- row r counts every tstride-th of its tiles (the speculative level-1
+    // layout of fused_pass_b_spec sizes its segments from it)
+    const unsigned K = KC ? (unsigned)KC : K_;
     constexpr int BLOCK = 256, PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;
     constexpr uint32_t NB = 1u << FUSED_HB;
     static_assert(FUSED_HB == 12, "6-char tops");
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
     };
     const uint64_t t0 = (uint64_t)blockIdx.x * per_row, t1 = min(ntiles, t0 + per_row);
     fetch(t0);
-    for (uint64_t tile = t0; tile < t1; ++tile) {
+    for (uint64_t tile = t0; tile < t1; tile += tstride) {
         const uint64_t base = tile * TILE;
         uint32_t pk, iv;
         if (have) pack16(pre, pk, iv);
@@ -136,7 +143,7 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
             s_inv[BLOCK + tid] = b;
         }
         __syncthreads();
-        if (tile + 1 < t1) fetch(tile + 1);
+        if (tile + tstride < t1) fetch(tile + tstride);
         else have = false;
         const uint64_t p0 = base + 16ull * tid;
         if (p0 >= npos) continue;
@@ -286,11 +293,15 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
 // NB: the widest digit's bucket count (1024: a 10-bit level 1, so that inputs of ~2e9 k-mers keep a
 // 2-level plan).  The bucket counts live in the run-base array until the scan has read them, and the
 // in-tile offsets are u16, so NB = 1024 still fits two workgroups per CU (78 KB of LDS).
-template <int BLOCK, int NB = 512>
+template <int BLOCK, int NB = 512, int KC = 0>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
-    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical, unsigned b,
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
-    Key<1> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
+    Key<1> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr,
+    uint32_t *__restrict__ povf = nullptr) {
+    // povf (the speculative level-1 layout): a reservation past its segment's end writes nothing and
+    // raises *povf instead of the error word -- the caller then runs the exact passes A and B
+    const unsigned K = KC ? (unsigned)KC : K_;
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
     constexpr int NBMAX = NB;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
@@ -407,7 +418,7 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
             const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
             unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
             if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
-                atomicOr(error, 2u);            // write past its range (the host raises)
+                atomicOr(povf ? povf : error, povf ? 1u : 2u);  // write past its range
                 g = ~0ull;
             }
             s_gbase[i] = g;
@@ -479,6 +490,62 @@ __global__ void cursor_check_kernel(const unsigned long long *__restrict__ curso
                                     uint32_t *__restrict__ error) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nb && cursor[i] != bend[i]) atomicOr(error, 2u);
+}
+
+/*
+ * The speculative level-1 layout (fused_pass_b_spec): pass A counts only every SA-th tile of each
+ * row, and pass B scatters into segments sized from that sample, one per (bucket, stripe), bucket-
+ * major, each rounded up to whole level-2 tiles (TILE2 keys) so that every level-2 tile lies inside
+ * one segment: its keys are a prefix of the tile (tvalid[tile] of them) and the level-2 pass
+ * (msd_hist_kernel / msd_partition_kernel with tvalid) reads the padded array without compaction.
+ * caps[i * S + s] = the segment of bucket i, stripe s: the sampled count times SA with 1/16 + 3
+ * sigma + 1024 of slack.  One workgroup per bucket, one thread per stripe (S <= 256).
+ */
+__global__ __launch_bounds__(256) void spec_l1_caps_kernel(const uint32_t *__restrict__ rows, uint32_t nrows,
+                                                           unsigned hb, unsigned b, uint32_t stripes, uint32_t rps,
+                                                           float sa, uint32_t tile2, uint32_t *__restrict__ caps,
+                                                           bool tiny = false) {
+    // tiny (tests): half the sampled count, rounded down -- every populated stripe overflows
+    const uint32_t i = blockIdx.x, s = threadIdx.x, f = 1u << (hb - b), nbh = 1u << hb;
+    if (s >= stripes) return;
+    uint64_t cnt = 0;
+    const uint32_t r1 = min(rps * s + rps, nrows);
+    for (uint32_t r = rps * s; r < r1; ++r)
+        for (uint32_t j = 0; j < f; ++j) cnt += rows[(size_t)r * nbh + i * f + j];
+    const double est = (double)cnt * (double)sa;  // sa: tiles per sampled tile
+    uint64_t cap = (uint64_t)(est + est / 16.0 + 3.0 * sqrt(est * sa) + 1024.0);
+    cap = tiny ? (uint64_t)(est / 2) / tile2 * tile2 : (cap + tile2 - 1) / tile2 * tile2;
+    caps[(size_t)i * stripes + s] = (uint32_t)min(cap, (uint64_t)0xFFFFFFFFu / tile2 * tile2);
+}
+
+// segment starts (scan of caps, bucket-major) -> pass B's per-stripe cursors and ends (stripe-major)
+__global__ void spec_l1_cursor_kernel(const uint64_t *__restrict__ start, const uint32_t *__restrict__ caps,
+                                      uint32_t nb, uint32_t stripes, unsigned long long *__restrict__ cursor,
+                                      unsigned long long *__restrict__ bend) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nb * stripes) return;
+    const uint32_t i = (uint32_t)(t / stripes), s = (uint32_t)(t % stripes);
+    cursor[(size_t)s * nb + i] = start[t];
+    bend[(size_t)s * nb + i] = start[t] + caps[t];
+}
+
+// after the speculative pass B: every segment's fill (its cursor minus its start), the exact level-1
+// counts h1 (zeroed by the caller), the total in *total, and tvalid of the segment's level-2 tiles
+__global__ void spec_l1_finish_kernel(const uint64_t *__restrict__ start, const uint32_t *__restrict__ caps,
+                                      const unsigned long long *__restrict__ cursor, uint32_t nb, uint32_t stripes,
+                                      uint32_t tile2, uint32_t *__restrict__ h1, uint32_t *__restrict__ tvalid,
+                                      unsigned long long *__restrict__ total) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nb * stripes) return;
+    const uint32_t i = (uint32_t)(t / stripes), s = (uint32_t)(t % stripes);
+    const uint64_t st = start[t], cap = caps[t];
+    const uint64_t fill = min((uint64_t)cursor[(size_t)s * nb + i] - st, cap);  // past cap: overflow, flagged
+    if (fill) {
+        atomicAdd(&h1[i], (uint32_t)fill);
+        atomicAdd(total, (unsigned long long)fill);
+    }
+    for (uint64_t o = 0; o < cap; o += tile2)
+        tvalid[(st + o) / tile2] = (uint32_t)(fill > o ? min(fill - o, (uint64_t)tile2) : 0);
 }
 
 // duplication estimate straight from the read bytes (the keys do not exist yet): the k-mer at

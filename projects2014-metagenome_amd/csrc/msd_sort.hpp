@@ -49,7 +49,10 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
                                                              unsigned b, unsigned bp,
                                                              uint32_t *__restrict__ counts,
                                                              uint32_t tstride = 1, uint32_t slice = 1,
-                                                             uint32_t gtiles = 1) {
+                                                             uint32_t gtiles = 1,
+                                                             const uint32_t *__restrict__ tvalid = nullptr) {
+    // tvalid (the speculative level-1 layout, extract_partition.hpp: spec_l1_caps_kernel): tile t holds
+    // keys only in its first tvalid[t] positions
     // tstride > 1: a sample -- workgroup i counts tile i * tstride (msd_sort_unique's speculative
     // final level sizes its buckets from it); slice > 1: a finer sample -- workgroup i counts 1/slice
     // of tiles i * gtiles .. + gtiles - 1, one line of every 8 * slice keys (previous-level buckets only
@@ -59,13 +62,27 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
     constexpr int TILE = MsdTraits<L>::TILE;
     constexpr int WMAX = MSD_WIN << 8;
     __shared__ uint32_t s_cnt[WMAX];
-    const uint64_t base = (uint64_t)blockIdx.x * tstride * (slice > 1 ? gtiles : 1u) * TILE;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * tstride * (slice > 1 ? gtiles : 1u);
+    const uint64_t base = tile0 * TILE;
+    if (base >= n) return;
+    auto tile_end = [&](uint64_t t) {  // end of tile t's keys
+        return min(n, t * TILE + (tvalid ? (uint64_t)tvalid[t] : (uint64_t)TILE));
+    };
+    // the LDS window starts at the first key of the workgroup's first non-empty tile
+    uint64_t wkey = base;
+    if (tvalid) {
+        const uint32_t ng = slice > 1 ? gtiles : 1u;
+        uint32_t t = 0;
+        while (t < ng && (tile0 + t) * TILE < n && tvalid[tile0 + t] == 0) ++t;
+        if (t == ng || (tile0 + t) * TILE >= n) return;
+        wkey = (tile0 + t) * TILE;
+    }
     const unsigned sub = b - bp;
     const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
     for (int i = threadIdx.x; i < (int)wsize; i += MSD_BLOCK) s_cnt[i] = 0;
-    const uint32_t wbase = key_prefix(keys[base], nbits, bp) << sub;
+    const uint32_t wbase = key_prefix(keys[wkey], nbits, bp) << sub;
     __syncthreads();
-    const uint64_t end = min(n, base + TILE / slice);
+    const uint64_t end = min(tile_end(tile0), base + TILE / slice);
     auto add = [&](const Key<L> &key) {
         const uint32_t bucket = key_prefix(key, nbits, b);
         const uint32_t lb = bucket - wbase;
@@ -81,7 +98,7 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
         for (uint32_t t = 0; t < gtiles; ++t) {
             const uint64_t tb = base + (uint64_t)t * TILE;
             if (tb >= n) break;
-            const uint64_t tend = min(n, tb + TILE);
+            const uint64_t tend = tile_end(tile0 + t);
             for (uint32_t j = threadIdx.x; j < 4 * lines; j += MSD_BLOCK) {
                 const uint64_t i = tb + (uint64_t)(j >> 2) * (8 * slice) + 2 * (j & 3);
                 if (i + 1 < tend) {
@@ -221,7 +238,9 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     const Key<L> *__restrict__ kin, Key<L> *__restrict__ kout, const uint32_t *__restrict__ vin,
     uint32_t *__restrict__ vout, uint64_t n, unsigned nbits, unsigned b, unsigned bp,
     unsigned long long *__restrict__ cursor, unsigned cstride = 1,
-    const unsigned long long *__restrict__ bend = nullptr, uint32_t *__restrict__ povf = nullptr) {
+    const unsigned long long *__restrict__ bend = nullptr, uint32_t *__restrict__ povf = nullptr,
+    const uint32_t *__restrict__ tvalid = nullptr) {
+    // tvalid (the speculative level-1 layout): tile t holds keys only in its first tvalid[t] positions
     // NT: nontemporal loads and stores (the streaming wide-digit pass: nothing it touches is
     // re-read from L2; measured 4.65 vs 4.67 ms on the cfg2 pass)
     // bend (speculative buckets, sized from a sample): a reservation past its bucket's end writes
@@ -239,6 +258,8 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     const uint32_t tid = threadIdx.x;
     const uint64_t tile = xcd_tile((n + TILE - 1) / TILE);  // grid = xcd_grid(tiles)
     if (tile * TILE >= n) return;
+    const uint32_t tv = tvalid ? tvalid[tile] : (uint32_t)TILE;
+    if (tv == 0) return;
     const uint64_t base = tile * TILE;
     const unsigned sub = b - bp;
     const uint32_t wsize = min((uint32_t)WMAX, (uint32_t)MSD_WIN << sub);  // 9-bit digits: one segment
@@ -253,8 +274,8 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint64_t i = base + (uint64_t)j * BLOCK + tid;
-        have[j] = i < n;
-        if (i < n) {
+        have[j] = i < n && (uint32_t)j * BLOCK + tid < tv;
+        if (have[j]) {
             k[j] = load_key(kin + i, NT);
             if (HAS_VAL) v[j] = vin[i];
         }
@@ -477,8 +498,12 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  *   3. Keys (and counts) go to tmp[gstart[g] + slot]; ucount[g] = D.
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
+#ifndef MTG_LU_PEEL
+#define MTG_LU_PEEL 1
+#endif
 template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
-          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1, bool FAST = false>
+          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1, bool FAST = false,
+          bool PEEL = MTG_LU_PEEL>
 __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
@@ -640,6 +665,33 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 // loop, one LDS atomic per wave (an atomicAdd on s_distinct from the inserting lanes
                 // is the atomic optimizer's lane-by-lane loop: ~5 SALU per new key)
                 int32_t ins = -1;
+                if constexpr (FAST && KEYCAS && !COUNTED && PEEL) {
+                    // the first probe straight-line: a repeat finds itself and a new key its empty slot
+                    // there, so only the lanes whose slot held another key enter the probing loop
+                    const bool act = hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice);
+                    const uint64_t key = kb[q].w[0];
+                    uint32_t h = slot_of<SLOTS>(key_hash(kb[q]));
+                    uint64_t old = 0;
+                    if (act) old = atomicCAS((unsigned long long *)&s_key[h].w[0], (unsigned long long)EMPTY,
+                                             (unsigned long long)key);
+                    if (act && old == EMPTY) ins = (int32_t)h;
+                    if (act && old != EMPTY && old != key) {
+                        for (uint32_t probes = 1;; ++probes) {
+                            if (probes >= SLOTS) {
+                                ovf = true;
+                                break;
+                            }
+                            h = h + 1 == SLOTS ? 0 : h + 1;
+                            old = atomicCAS((unsigned long long *)&s_key[h].w[0], (unsigned long long)EMPTY,
+                                            (unsigned long long)key);
+                            if (old == EMPTY) {
+                                ins = (int32_t)h;
+                                break;
+                            }
+                            if (old == key) break;
+                        }
+                    }
+                } else
                 if (hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice)) {
                 const Key<L> key = kb[q];
                 uint32_t h = slot_of<SLOTS>(key_hash(key));

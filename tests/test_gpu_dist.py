@@ -111,10 +111,12 @@ def test_dist_superkmer_read_counts(monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"MTG_DIST_COLLECT": "superkmer"}, {"MTG_DIST_COLLECT": "local"},
-                                 {"MTG_ROUTED_CANON": "min"}])
+                                 {"MTG_ROUTED_CANON": "min"}, {"MTG_DIST_SINKS": "query"},
+                                 {"MTG_DIST_SINKS": "query", "MTG_DIST_COLLECT": "superkmer"}])
 def test_dist_collect_modes(monkeypatch, env):
     # every collect of the multi-GPU build (MTG_DIST_COLLECT; the routed default with min(fwd, rc)
-    # canonical keys instead of the hashed-top choice) is exact
+    # canonical keys instead of the hashed-top choice) is exact, and so is the sink join by routed
+    # queries (MTG_DIST_SINKS=query) that the pulled edge slices replaced
     for name, v in env.items():
         monkeypatch.setenv(name, v)
     reads = _random_reads(21, 2000, 150, 20000, n_rate=0.005, lower=True)
@@ -131,8 +133,11 @@ def test_dist_empty_and_lopsided_ranks():
     check_dist(1, CONSTRUCT_SEQS, 4, True, 8)
 
 
-def test_dist_large_multi_tile():
-    # (8, True) is configs[3]'s shape: canonical, BOSS k = 30 (k = 31), the default routed collect on 8 ranks
+@pytest.mark.parametrize("sinks", ["pull", "query"])
+def test_dist_large_multi_tile(monkeypatch, sinks):
+    # (8, True) is configs[3]'s shape: canonical, BOSS k = 30 (k = 31), the default routed collect on 8
+    # ranks; the default pulled sink join and the routed queries it replaced
+    monkeypatch.setenv("MTG_DIST_SINKS", sinks)
     reads = _random_reads(77, 30000, 150, 400000, n_rate=0.0005)
     for P, canonical in ((2, True), (4, True), (8, False), (8, True)):
         check_dist(30, reads, P, canonical, bits=8)

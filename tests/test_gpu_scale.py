@@ -125,6 +125,30 @@ def test_bench_generator_speculative_overflow(monkeypatch, levels):
     _assert_same(got, want, "2M reads k=31 canonical, tiny speculative buckets, %s levels" % levels)
 
 
+@pytest.mark.parametrize("canonical,knobs", [(False, {}), (True, {}), (True, {"MTG_SPEC": "0"}),
+                                             (True, {"MTG_SPEC_L1_CAPS": "tiny"})])
+def test_bench_generator_speculative_level1(monkeypatch, canonical, knobs):
+    # the fused K1's sampled pass A and speculative level-1 layout (fused_pass_b_spec; on by default
+    # from 2^28 windows), forced on 2 M reads: the level-2 pass reads the padded segments through
+    # tvalid -- speculative (default), exact (MTG_SPEC=0), or never reached because the segments were
+    # sized without slack and overflowed into the exact passes A and B (MTG_SPEC_L1_CAPS=tiny)
+    monkeypatch.setenv("MTG_SPEC_L1_MIN", "0")
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
+    got, t = _gpu_build(30, asc, canonical, 0)
+    assert t.n_extracted == 2_000_000 * 120
+    if "MTG_SPEC_L1_CAPS" in knobs:
+        assert t.spec_l1 == 0 and t.spec_fallbacks >= 1, (t.spec_l1, t.spec_fallbacks)
+    else:
+        assert t.spec_l1 == 1, t.spec_l1
+        if "MTG_SPEC" not in knobs:
+            assert t.spec_fallbacks == 0 and t.spec_levels >= 1, (t.spec_levels, t.spec_fallbacks)
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    want = O.build_chunk(30, reads, canonical=canonical, bits_per_count=0)
+    _assert_same(got, want, "2M reads k=31 canonical=%s, speculative level 1, %s" % (canonical, knobs))
+
+
 @pytest.mark.parametrize("canonical", [False, True])
 def test_config0_k12_full_transcripts(transcripts_1000, canonical):
     for bits in (0, 8):
