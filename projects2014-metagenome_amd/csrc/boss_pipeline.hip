@@ -307,6 +307,8 @@ struct Ctx {
     bool spec_l1_tiny = false;  // MTG_SPEC_L1_CAPS=tiny: segments without slack (tests force its fallback)
     uint64_t spec_l1_min = 1ull << 28;
     uint32_t spec_l1_sample = 8;
+    uint32_t spec_l1_stripes = 16;  // MTG_SPEC_L1_STRIPES: segments per level-1 bucket (a power of two <= 256)
+    uint32_t spec_l1_slack = 16;    // MTG_SPEC_L1_SLACK: segment slack 1/n of the estimate (+ 3 sigma + 1024)
     // the speculative level-1 layout of the last fused K1 until the level-2 pass has read it: gap1_n
     // positions, tile t of the level-2 tiling holding keys in its first gap1_tv[t] positions
     uint64_t gap1_n = 0;
@@ -348,6 +350,11 @@ static void load_knobs(Ctx &c) {
     c.dist_pull = !is("MTG_DIST_SINKS", "query");
     c.kspec = !is("MTG_KSPEC", "0");
     c.spec_l1_tiny = is("MTG_SPEC_L1_CAPS", "tiny");
+    if (const char *e = getenv("MTG_SPEC_L1_STRIPES")) {
+        const long v = atol(e);
+        if (v >= 1 && v <= 256 && (v & (v - 1)) == 0) c.spec_l1_stripes = (uint32_t)v;
+    }
+    if (const char *e = getenv("MTG_SPEC_L1_SLACK")) c.spec_l1_slack = (uint32_t)std::max(2L, std::min(1024L, atol(e)));
     if (const char *e = getenv("MTG_SPEC_L1_MIN")) c.spec_l1_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("MTG_SPEC_L1_SAMPLE")) c.spec_l1_sample = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_MSD_LEVELS")) c.min_levels = (unsigned)std::min(3, std::max(0, atoi(v)));
@@ -1464,9 +1471,9 @@ static void launch_part_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, A... a) {
     else extract_partition_fast_kernel<BLOCK, NB, 0><<<g, b, 0, c.stream>>>(a...);
 }
 
-// sample > 1 (fused_pass_b_spec): every row counts every sample-th of its tiles, and the rows form
-// kSpecStripes stripes of kSpecRps rows each (A->h, A->N are then estimates)
-constexpr uint32_t kSpecStripes = 16, kSpecRps = 128;
+// sample > 1 (fused_pass_b_spec): every row counts every sample-th of its tiles, and the 2048 rows form
+// c.spec_l1_stripes stripes (A->h, A->N are then estimates)
+constexpr uint32_t kSpecRows = 2048;
 static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &in, FusedA *A, uint32_t sample = 1) {
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
@@ -1501,15 +1508,16 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
     uint64_t per_row = stripes == 1 ? ceil_div(tiles_b * rps, nrows) : per_stripe;
     uint32_t rps_out = rps;
     if (sample > 1) {
-        // kSpecStripes stripes of kSpecRps rows: row r counts the pass-A tiles [r per_row, (r + 1) per_row),
+        // S stripes of kSpecRows / S rows: row r counts the pass-A tiles [r per_row, (r + 1) per_row),
         // so stripe s (pass-B tiles [s per_stripe, (s + 1) per_stripe), 2 pass-A tiles each) is rows
-        // s kSpecRps .. + kSpecRps - 1
-        nrows = kSpecStripes * kSpecRps;
+        // s rps .. + rps - 1
+        const uint32_t S = c.spec_l1_stripes, srps = kSpecRows / S;
+        nrows = kSpecRows;
         rows = (uint32_t *)c.ws.get(Workspace::HIST_ROWS, (uint64_t)nrows * nbh * 4);
         per_row = ceil_div(tiles, nrows);
-        per_stripe = kSpecRps * per_row / 2;  // kSpecRps is even
+        per_stripe = srps * per_row / 2;  // srps is even (S <= 256)
         stripes = (uint32_t)ceil_div(tiles_b, per_stripe);
-        rps_out = kSpecRps;
+        rps_out = srps;
     }
     launch_hist_fast<false>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, canonical ? 1 : 0, tiles, per_row, rows,
                             (uint32_t *)nullptr, sample);
@@ -1632,7 +1640,8 @@ static uint64_t fused_pass_b_spec(Ctx &c, unsigned K, bool canonical, const Buil
     uint32_t *caps = (uint32_t *)c.ws.get(Workspace::SPEC1_CAPS, (nseg + 1) * 4);
     uint64_t *sst = (uint64_t *)c.ws.get(Workspace::SPEC1_START, (nseg + 1) * 8);
     spec_l1_caps_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(A.rows, A.nrows, FUSED_HB, b1, S, A.rps,
-                                                               (float)A.sample_factor, T2, caps, c.spec_l1_tiny);
+                                                               (float)A.sample_factor, T2, caps, c.spec_l1_tiny,
+                                                               c.spec_l1_slack);
     HIP_CHECK(hipGetLastError());
     {
         uint32_t ep;

@@ -498,13 +498,13 @@ __global__ void cursor_check_kernel(const unsigned long long *__restrict__ curso
  * major, each rounded up to whole level-2 tiles (TILE2 keys) so that every level-2 tile lies inside
  * one segment: its keys are a prefix of the tile (tvalid[tile] of them) and the level-2 pass
  * (msd_hist_kernel / msd_partition_kernel with tvalid) reads the padded array without compaction.
- * caps[i * S + s] = the segment of bucket i, stripe s: the sampled count times SA with 1/16 + 3
+ * caps[i * S + s] = the segment of bucket i, stripe s: the sampled count times SA with 1/slack + 3
  * sigma + 1024 of slack.  One workgroup per bucket, one thread per stripe (S <= 256).
  */
 __global__ __launch_bounds__(256) void spec_l1_caps_kernel(const uint32_t *__restrict__ rows, uint32_t nrows,
                                                            unsigned hb, unsigned b, uint32_t stripes, uint32_t rps,
                                                            float sa, uint32_t tile2, uint32_t *__restrict__ caps,
-                                                           bool tiny = false) {
+                                                           bool tiny = false, uint32_t slack = 16) {
     // tiny (tests): half the sampled count, rounded down -- every populated stripe overflows
     const uint32_t i = blockIdx.x, s = threadIdx.x, f = 1u << (hb - b), nbh = 1u << hb;
     if (s >= stripes) return;
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(256) void spec_l1_caps_kernel(const uint32_t *__res
     for (uint32_t r = rps * s; r < r1; ++r)
         for (uint32_t j = 0; j < f; ++j) cnt += rows[(size_t)r * nbh + i * f + j];
     const double est = (double)cnt * (double)sa;  // sa: tiles per sampled tile
-    uint64_t cap = (uint64_t)(est + est / 16.0 + 3.0 * sqrt(est * sa) + 1024.0);
+    uint64_t cap = (uint64_t)(est + est / slack + 3.0 * sqrt(est * sa) + 1024.0);
     cap = tiny ? (uint64_t)(est / 2) / tile2 * tile2 : (cap + tile2 - 1) / tile2 * tile2;
     caps[(size_t)i * stripes + s] = (uint32_t)min(cap, (uint64_t)0xFFFFFFFFu / tile2 * tile2);
 }

@@ -498,12 +498,8 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  *   3. Keys (and counts) go to tmp[gstart[g] + slot]; ucount[g] = D.
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
-#ifndef MTG_LU_PEEL
-#define MTG_LU_PEEL 1
-#endif
 template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
-          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1, bool FAST = false,
-          bool PEEL = MTG_LU_PEEL>
+          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1, bool FAST = false>
 __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
@@ -665,33 +661,6 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 // loop, one LDS atomic per wave (an atomicAdd on s_distinct from the inserting lanes
                 // is the atomic optimizer's lane-by-lane loop: ~5 SALU per new key)
                 int32_t ins = -1;
-                if constexpr (FAST && KEYCAS && !COUNTED && PEEL) {
-                    // the first probe straight-line: a repeat finds itself and a new key its empty slot
-                    // there, so only the lanes whose slot held another key enter the probing loop
-                    const bool act = hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice);
-                    const uint64_t key = kb[q].w[0];
-                    uint32_t h = slot_of<SLOTS>(key_hash(kb[q]));
-                    uint64_t old = 0;
-                    if (act) old = atomicCAS((unsigned long long *)&s_key[h].w[0], (unsigned long long)EMPTY,
-                                             (unsigned long long)key);
-                    if (act && old == EMPTY) ins = (int32_t)h;
-                    if (act && old != EMPTY && old != key) {
-                        for (uint32_t probes = 1;; ++probes) {
-                            if (probes >= SLOTS) {
-                                ovf = true;
-                                break;
-                            }
-                            h = h + 1 == SLOTS ? 0 : h + 1;
-                            old = atomicCAS((unsigned long long *)&s_key[h].w[0], (unsigned long long)EMPTY,
-                                            (unsigned long long)key);
-                            if (old == EMPTY) {
-                                ins = (int32_t)h;
-                                break;
-                            }
-                            if (old == key) break;
-                        }
-                    }
-                } else
                 if (hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice)) {
                 const Key<L> key = kb[q];
                 uint32_t h = slot_of<SLOTS>(key_hash(key));
