@@ -818,7 +818,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         HIP_CHECK(hipMemsetAsync(ovf, 0, nb * 4, c.stream));
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
         const bool keycas = nbits < 64;
-        constexpr int WPE = COUNTED ? 1 : 8;  // (the uncounted table fits 8 waves per SIMD at 64 VGPRs)
+        constexpr int WPE = COUNTED ? 1 : MTG_LU_WPE;  // (the uncounted table fits 8 waves per SIMD at 64 VGPRs)
         // only the buckets the keys can occupy (blo, bhi above; a round of the batched collect fills a
         // fraction of them); the others count 0 keys
         HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
@@ -1142,7 +1142,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 constexpr bool KC = decltype(keycas)::value;
                 constexpr int SL = decltype(sl)::value;
                 constexpr bool ND = decltype(nodup)::value;
-                constexpr int WPE = (L == 1 && KC && !ND && !COUNTED) ? 8 : 1;
+                constexpr int WPE = (L == 1 && KC && !ND && !COUNTED) ? MTG_LU_WPE : 1;
                 bucket_pieces(0, count, [&](uint64_t g0, unsigned cnt) {
                     if constexpr (KC && !ND) {
                         if (c.lu_fast) {

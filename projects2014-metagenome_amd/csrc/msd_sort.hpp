@@ -498,8 +498,12 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
  *   3. Keys (and counts) go to tmp[gstart[g] + slot]; ucount[g] = D.
  * More than LIMIT distinct keys -> overflow[g] = 1 (the host finishes the group otherwise).
  */
+// waves per SIMD the uncounted local_unique_kernel is compiled for (its VGPR budget: 512 / MTG_LU_WPE)
+#ifndef MTG_LU_WPE
+#define MTG_LU_WPE 8
+#endif
 template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
-          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? 8 : 1, bool FAST = false>
+          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? MTG_LU_WPE : 1, bool FAST = false>
 __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
@@ -571,7 +575,14 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         // keys are loaded BATCH at a time per thread so the global loads overlap; 8-byte keys
         // as 16-byte pairs from the even index at or below g0
         constexpr int PAIR = L == 1 ? 2 : 1;
-        constexpr int BATCH = (LB >= 1024 ? 12 : WPE >= 8 ? 6 : 8) / PAIR;  // 6 at 64 VGPRs: 4.47 -> 4.19 ms
+        // keys per thread and load batch: 4 at 64 VGPRs (6: 4.47 -> 4.19 ms in round 3; 4: sort stage
+        // 8.56 -> 8.29-8.38 ms in round 4, the 6-key batch spilled 16-20 bytes per lane to scratch);
+        // MTG_LU_BATCH overrides it at build time for A/B runs
+#ifdef MTG_LU_BATCH
+        constexpr int BATCH = (KEYCAS && !COUNTED && !NODUP ? MTG_LU_BATCH : (LB >= 1024 ? 12 : WPE >= 8 ? 4 : 8)) / PAIR;
+#else
+        constexpr int BATCH = (LB >= 1024 ? 12 : WPE >= 8 ? 4 : 8) / PAIR;
+#endif
         const uint64_t a0 = PAIR == 2 ? (g0 & ~1ull) : g0;
         for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += (uint64_t)LB * BATCH * PAIR) {
             Key<L> kb[BATCH * PAIR];
