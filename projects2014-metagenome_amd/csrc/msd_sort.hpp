@@ -91,16 +91,16 @@ __global__ __launch_bounds__(MSD_BLOCK) void msd_hist_kernel(const Key<L> *__res
     };
     if constexpr (L == 1) {
       if (slice > 1) {
-        // the finer sample spread over the whole tile: the first 64-byte line (8 keys) of every
-        // 8 * slice keys, four lanes per line (a contiguous 1/slice prefix would miss previous-level
-        // buckets that start late in the tile)
-        const uint32_t lines = TILE / (8 * slice);
+        // the finer sample spread over the whole tile: the first 128-byte line (16 keys) of every
+        // 16 * slice keys, eight lanes per line (a contiguous 1/slice prefix would miss previous-level
+        // buckets that start late in the tile; 64-byte lines fetched twice the bytes they counted)
+        const uint32_t lines = TILE / (16 * slice);
         for (uint32_t t = 0; t < gtiles; ++t) {
             const uint64_t tb = base + (uint64_t)t * TILE;
             if (tb >= n) break;
             const uint64_t tend = tile_end(tile0 + t);
-            for (uint32_t j = threadIdx.x; j < 4 * lines; j += MSD_BLOCK) {
-                const uint64_t i = tb + (uint64_t)(j >> 2) * (8 * slice) + 2 * (j & 3);
+            for (uint32_t j = threadIdx.x; j < 8 * lines; j += MSD_BLOCK) {
+                const uint64_t i = tb + (uint64_t)(j >> 3) * (16 * slice) + 2 * (j & 7);
                 if (i + 1 < tend) {
                     const ulonglong2 v = *(const ulonglong2 *)(keys + i);
                     add(Key<L>::from(v.x));
