@@ -815,14 +815,29 @@ __device__ __forceinline__ uint64_t dummy_rank(uint64_t W, unsigned m, unsigned 
     return 4ull * m + (7 * W - 4 * char_sum2(W)) / 3 + (m < k ? (uint64_t)c : 0ull);
 }
 
+// The source levels with few real chars (m <= DUMMY_BITMAP_M: levels k - m) repeat: a level-(k - m)
+// dummy is fixed by the source node's first m + 1 chars, so ~S sources share at most 4^(m+1) of them.
+// In the dense-rank path they are not written one per (source, level) but set one bit each in a bitmap
+// over (m, first m chars, next char) -- (4^(DUMMY_BITMAP_M + 2) - 4) / 3 bits, 175 KB -- whose set
+// bits dummy_bitmap_ranks_kernel appends as ranks: the sort takes ~S (k - DUMMY_BITMAP_M - 1) + the
+// distinct few instead of S k keys.
+constexpr unsigned DUMMY_BITMAP_M = 9;
+constexpr unsigned DUMMY_BITMAP_LDS = 6;  // levels with <= 6 real chars: 21844 bits, an LDS copy per tile
+__host__ __device__ constexpr uint64_t dummy_bitmap_base(unsigned m) {  // bits of the levels with < m real chars
+    return ((1ull << (2 * (m + 1))) - 4) / 3;
+}
+
 // RANKS (k <= 30): the dummies as their dense u64 ranks (dummy_rank, below) straight from the 2-bit
 // edge -- a sink's real chars are the edge's target node (x >> 2 with the label moved on top), a
-// level-l source's are the edge's first k - l node chars shifted up l places -- instead of lifted keys
+// level-l source's are the edge's first k - l node chars shifted up l places -- instead of lifted keys.
+// bitmap (RANKS): the levels above kbig (m = k - level <= DUMMY_BITMAP_M) go to the bitmap instead
+// (the count pass counted kbig levels per source); nullptr: every level written (kbig = k)
 template <int L2, int L3, bool RANKS = false>
 __global__ __launch_bounds__(256) void dummy_write_kernel(
     const Key<L2> *__restrict__ keys, const uint8_t *__restrict__ flags,
     const uint8_t *__restrict__ in_flag, uint64_t n, unsigned K,
-    const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out) {
+    const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out, unsigned kbig = 0,
+    uint32_t *__restrict__ bitmap = nullptr) {
     uint64_t *rout = reinterpret_cast<uint64_t *>(out);
     __shared__ uint32_t s_scan[256 / 64 + 1];
     __shared__ uint16_t s_src[4096];  // tile-relative edge index of each source
@@ -855,11 +870,43 @@ __global__ __launch_bounds__(256) void dummy_write_kernel(
     __syncthreads();
     if constexpr (RANKS) {
         uint64_t *o = rout + base + nsink;
-        for (uint32_t it = tid; it < nsrc * k; it += 256) {
-            const uint32_t q = it / k, lev = it - q * k + 1;  // level 1 .. k
+        const unsigned kb = bitmap ? kbig : k;
+        for (uint32_t it = tid; it < nsrc * kb; it += 256) {
+            const uint32_t q = it / kb, lev = it - q * kb + 1;  // level 1 .. kb
             const uint64_t node = keys[t0 + s_src[q]].w[0] >> 2;  // a_1 .. a_k, a_1 lowest
             const uint64_t low = node & ((1ull << (2 * (k - lev))) - 1);  // a_1 .. a_(k - lev)
             o[it] = dummy_rank(low << (2 * lev), k - lev, k, (uint32_t)(node >> (2 * (k - lev))) & 3u);
+        }
+        if (bitmap) {
+            // the levels with <= DUMMY_BITMAP_LDS real chars (a few thousand bits that every tile's sources
+            // hit) gather in an LDS copy first and reach the global bitmap once per word and tile; the
+            // others set their bits directly.  Either way a word already holding the bits (an agent-scope
+            // load, past the non-coherent L1) takes no atomic (0.28 -> 0.49 ms for the write pass when every
+            // (source, level) item took a global atomic on a few hot words)
+            constexpr unsigned ML = DUMMY_BITMAP_LDS;
+            constexpr uint32_t WL = (uint32_t)((dummy_bitmap_base(ML + 1) + 31) / 32);
+            __shared__ uint32_t s_bm[WL];
+            for (uint32_t w = tid; w < WL; w += 256) s_bm[w] = 0;
+            __syncthreads();
+            const unsigned ks = k - kb;  // levels kb + 1 .. k: m = k - level real chars, m <= DUMMY_BITMAP_M
+            for (uint32_t it = tid; it < nsrc * ks; it += 256) {
+                const uint32_t q = it / ks, m = it - q * ks;  // m = 0 .. ks - 1
+                const uint64_t node = keys[t0 + s_src[q]].w[0] >> 2;
+                const uint64_t low = node & ((1ull << (2 * m)) - 1);
+                const uint64_t idx = dummy_bitmap_base(m) + (low << 2 | ((node >> (2 * m)) & 3u));
+                const uint32_t bit = 1u << (idx & 31);
+                if (m <= ML) {
+                    atomicOr(&s_bm[idx >> 5], bit);
+                } else if (!(__hip_atomic_load(&bitmap[idx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) {
+                    atomicOr(&bitmap[idx >> 5], bit);
+                }
+            }
+            __syncthreads();
+            for (uint32_t w = tid; w < WL; w += 256) {
+                const uint32_t v = s_bm[w];
+                if (v && (v & ~__hip_atomic_load(&bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+                    atomicOr(&bitmap[w], v);
+            }
         }
         return;
     }
@@ -1433,6 +1480,28 @@ __global__ void dummy_encode_kernel(const Key<L3> *__restrict__ in, uint64_t n, 
         out[i] = dummy_rank(W, m, k, c - 1);
     }
     if (err) atomicOr(bad, 1u);
+}
+
+// the bitmap's dummies (dummy_write_kernel) appended as ranks at out[*cursor ..): one thread per word,
+// one atomic per word with set bits (the order is free: the ranks are sorted next)
+__global__ void dummy_bitmap_ranks_kernel(const uint32_t *__restrict__ bitmap, uint64_t nwords, unsigned k,
+                                          unsigned ms, uint64_t *__restrict__ out,
+                                          unsigned long long *__restrict__ cursor) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gs) {
+        uint32_t v = bitmap[w];
+        if (!v) continue;
+        uint64_t o = atomicAdd(cursor, (unsigned long long)__popc(v));
+        while (v) {
+            const uint32_t b = __ffs(v) - 1;
+            v &= v - 1;
+            const uint64_t idx = w * 32 + b;
+            unsigned m = 0;
+            while (m + 1 < ms && dummy_bitmap_base(m + 1) <= idx) ++m;
+            const uint64_t r = idx - dummy_bitmap_base(m);  // low << 2 | c
+            out[o++] = dummy_rank((r >> 2) << (2 * (k - m)), m, k, (uint32_t)(r & 3u));
+        }
+    }
 }
 
 template <int L3>

@@ -65,7 +65,7 @@ class Workspace {
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
-        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, NSLOTS
+        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -265,6 +265,9 @@ struct Ctx {
     bool kspec = true;             // MTG_KSPEC=0: the fused K1 passes with K a runtime argument at K = 31 too
     bool dist_pull = true;         // MTG_DIST_SINKS=query: the multi-GPU sink join by routed queries
                                    // (target_split + query_join) instead of the pulled edge slices
+    bool dummy_bitmap = false;     // MTG_DUMMY_BITMAP=1: the source levels with few real chars as bits of a
+                                   // bitmap (dummy_write_kernel) -- the sort gains 0.25 ms, the write pass
+                                   // loses as much, so off by default
     bool dummy_ranks = true;       // MTG_DUMMY_SORT=lifted: sort the dummies as lifted keys, not as
                                    // dense u64 ranks (dummy_encode_kernel)
     // bucket index of the last msd_sort_unique's output over its final bucket bits, when every group
@@ -349,6 +352,7 @@ static void load_knobs(Ctx &c) {
     c.spec_l1 = !is("MTG_SPEC_L1", "0");
     c.dist_pull = !is("MTG_DIST_SINKS", "query");
     c.kspec = !is("MTG_KSPEC", "0");
+    c.dummy_bitmap = is("MTG_DUMMY_BITMAP", "1");
     c.spec_l1_tiny = is("MTG_SPEC_L1_CAPS", "tiny");
     if (const char *e = getenv("MTG_SPEC_L1_STRIPES")) {
         const long v = atol(e);
@@ -2232,12 +2236,16 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
     uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (wtiles + 1) * 4);
     uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (wtiles + 1) * 8);
     uint64_t Draw = 0;
+    // the dense-rank path writes the source levels with <= DUMMY_BITMAP_M real chars as bits of a bitmap
+    // (dummy_write_kernel), so the count pass counts kbig levels per source
+    const bool bitmap_path = L2 == 1 && c.dummy_ranks && c.dummy_bitmap && k >= 1 && k <= 30;
+    const unsigned ks = std::min<unsigned>(k, DUMMY_BITMAP_M + 1), kbig = bitmap_path ? k - ks : k;
     if (R) {
         HIP_CHECK(hipMemsetAsync(in_flag, 0, R, c.stream));
         dummy_sink_kernel<L2><<<dim3((unsigned)ceil_div(R, DummyTraits<L2>::TILE)), dim3(256), 0,
                                 c.stream>>>(ka, R, K, bstart, bshift, flags, in_flag);
         HIP_CHECK(hipGetLastError());
-        dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, k, tcnt);
+        dummy_count_kernel<<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(flags, in_flag, R, kbig, tcnt);
         HIP_CHECK(hipGetLastError());
         uint32_t ep;
         const uint64_t st = ceil_div(wtiles, 4096);
@@ -2250,6 +2258,31 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
         HIP_CHECK(hipStreamSynchronize(c.stream));
     }
     *dk = nullptr;
+    if constexpr (L2 == 1) {
+        if (bitmap_path) {  // written as dense ranks: no lifted keys until the decode
+            const uint64_t nbits = dummy_bitmap_base(ks), nwords = ceil_div(nbits, 32);
+            uint32_t *bm = (uint32_t *)c.ws.get(Workspace::DBITMAP, nwords * 4);
+            HIP_CHECK(hipMemsetAsync(bm, 0, nwords * 4, c.stream));
+            const uint64_t cap = Draw + nbits;  // u64 ranks: the written ones, then at most every bit
+            K3 *da = (K3 *)c.ws.get(Workspace::DA, cap * sizeof(K3));
+            K3 *db = (K3 *)c.ws.get(Workspace::DB, cap * sizeof(K3));
+            if (R) {
+                dummy_write_kernel<L2, L3, true><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(
+                    ka, flags, in_flag, R, K, toff, da, kbig, bm);
+                HIP_CHECK(hipGetLastError());
+            }
+            HIP_CHECK(hipMemcpyAsync(&c.small->total, &Draw, 8, hipMemcpyHostToDevice, c.stream));
+            dummy_bitmap_ranks_kernel<<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(nwords, 256), 4096))),
+                                        dim3(256), 0, c.stream>>>(bm, nwords, k, ks, (uint64_t *)da, &c.small->total);
+            HIP_CHECK(hipGetLastError());
+            const uint64_t Dall = read_u64(c, &c.small->total);  // (also orders the copy of the host local)
+            if (c.debug)
+                fprintf(stderr, "[mtg debug] dummies: %lu written + %lu from the bitmap (%u levels per source)\n",
+                        (unsigned long)Draw, (unsigned long)(Dall - Draw), ks);
+            if (!Dall) return 0;
+            return sort_unique_dummy_ranks<L3>(c, k, da, db, (Key<1> *)da, Dall, dk);
+        }
+    }
     if (!Draw) return 0;
     K3 *da = (K3 *)c.ws.get(Workspace::DA, Draw * sizeof(K3));
     K3 *db = (K3 *)c.ws.get(Workspace::DB, Draw * sizeof(K3));

@@ -104,3 +104,38 @@ def test_ranks_straight_from_the_edge(k):
             src = lifted(top_down, a[k - lev] + 1, k)
             low = node & ((1 << (2 * (k - lev))) - 1)
             assert encode(src, k) == rank_direct(low << (2 * lev), k - lev, k, (node >> (2 * (k - lev))) & 3)
+
+
+def bitmap_base(m):
+    """bits of the source levels with fewer than m real chars (boss_kernels.hpp: dummy_bitmap_base)"""
+    return (4 ** (m + 1) - 4) // 3
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 6])
+def test_source_bitmap_index_is_the_rank(k):
+    # dummy_write_kernel sets bit base(m) + (low << 2 | c) for the level-(k - m) source with first m real
+    # chars `low` (a_1 lowest) and next char c; dummy_bitmap_ranks_kernel turns a set bit back into the
+    # dense rank.  Over every (m, low, c) of the small levels: the bits are distinct, the walk finds m
+    # again, and the rank is the encode of the lifted source (its real chars at node positions
+    # k - m + 1 .. k, a_1 lowest of them, $ below, label c)
+    ms = min(k, 10)
+    seen = set()
+    for m in range(ms):
+        for low in range(4 ** m):
+            for c in range(4):
+                idx = bitmap_base(m) + (low << 2 | c)
+                assert idx not in seen
+                seen.add(idx)
+                mm = 0
+                while mm + 1 < ms and bitmap_base(mm + 1) <= idx:
+                    mm += 1
+                assert mm == m
+                r = idx - bitmap_base(mm)
+                # the lifted source: $ at node positions 1 .. k - m, a_i at position k - m + i
+                x = c + 1
+                for i in range(m):
+                    x |= (((low >> (2 * i)) & 3) + 1) << (3 * (k - m + i + 1))
+                W = (r >> 2) << (2 * (k - m))
+                S = sum((low >> (2 * i)) & 3 for i in range(m))
+                assert 4 * m + (7 * W - 4 * S) // 3 + (r & 3) == encode(x, k)
+    assert len(seen) == bitmap_base(ms)
