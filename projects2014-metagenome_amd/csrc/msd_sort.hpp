@@ -972,6 +972,16 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         return;
     }
     const uint32_t nr = (uint32_t)(g1 - g0), nc = (uint32_t)(c1 - c0);
+    if (nr == 0 && nc == 0) {
+        // an empty bucket range (most of them on a rank of a multi-GPU build, whose keys fill 1/P of the
+        // buckets): its index entries only, no table setup and no barriers
+        if (istart) {
+            const uint64_t base = c0 + (gbase ? gbase[g] : g0);
+            const uint64_t ifirst = gb0 << (ib - b), iend = gb1 << (ib - b);
+            for (uint64_t x = ifirst + tid; x < iend; x += LB) istart[x] = base;
+        }
+        return;
+    }
     for (uint32_t i = tid; i < nr; i += LB) {
         s_r[i] = keys[g0 + i];
         if (COUNTED) s_rv[i] = vals[g0 + i];
