@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void rc_map_gapped_kernel(const Key<L> *__rest
             for (int q = 0; q < 4; ++q) {
                 if (i0 + 64 * q >= m) break;
                 const Key<L> r = revcomp2(x[q], K);
-                rc_out[dst + i0 + 64 * q] = r;
+                if (rc_out) rc_out[dst + i0 + 64 * q] = r;  // (nullptr: the histogram only)
                 if (hist_bits) atomicAdd(&s_hist[bits_at(r, 2 * K - hist_bits, hist_bits)], 1u);
             }
         }
@@ -491,6 +491,178 @@ __global__ __launch_bounds__(256) void rc_map_gapped_kernel(const Key<L> *__rest
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < (1u << hist_bits); i += 256)
             if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
+    }
+}
+
+/*
+ * K4 fused with the rc sort's first MSD level (odd K, the canonical set in its speculative buckets,
+ * Ctx::gap): the rc keys go straight into their level-1 buckets -- one cursor reservation per (tile,
+ * bucket), the tile ranked by bucket in LDS and written as runs, as msd_partition_kernel does -- instead
+ * of being written in canonical order by rc_map_gapped_kernel and partitioned by a second pass (its
+ * histogram pass, rc_map_gapped_kernel with no output, gives the bucket starts).  A tile is TILE
+ * consecutive compact positions p of the canonical set; p lies in canonical bucket g with ustart[g] <= p <
+ * ustart[g + 1] and is read at keys[bstart[g] + p - ustart[g]]: the tile's slice of (ustart, bstart) is
+ * staged in LDS and a position -> bucket map is built there by a max-scan (a binary search per position
+ * measured 1.15 ms per cfg2 rc set vs 0.71 for the separate partition pass; the map, 0.95).  The
+ * histogram pass is the same kernel with HIST (rc_map_gapped_kernel without output, one wave per
+ * canonical bucket: 0.39 ms).
+ */
+template <int L>
+struct RcPartTraits {
+    static constexpr int BLOCK = 512, ITEMS = L == 1 ? 16 : 8, TILE = BLOCK * ITEMS;
+    static constexpr int NBM = 512;  // level-1 buckets at most (9 bits, rc_map_gapped_kernel's histogram)
+    static constexpr int GS = 256;   // canonical buckets of the staged slice
+};
+
+// tile_g[t] = the canonical bucket holding compact position t * TILE (one thread per bucket: the tiles
+// starting inside it) -- a per-tile binary search over ustart, 20 dependent loads, measured 0.64 ms for
+// the histogram pass against 0.39 for the wave-per-bucket one
+__global__ __launch_bounds__(256) void rc_tile_bucket_kernel(const uint64_t *__restrict__ ustart, uint64_t nb,
+                                                             uint32_t tile, uint64_t *__restrict__ tile_g) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= nb) return;
+    const uint64_t a = ustart[g], e = ustart[g + 1];
+    for (uint64_t t = (a + tile - 1) / tile; t * tile < e; ++t) tile_g[t] = g;
+}
+
+// HIST: the histogram pass (hist[b] += the tile's count of rc keys in level-1 bucket b), nothing written
+template <int L, bool HIST = false>
+__global__ __launch_bounds__(512) void rc_partition_gapped_kernel(
+    const Key<L> *__restrict__ keys, const uint64_t *__restrict__ bstart, const uint64_t *__restrict__ ustart,
+    const uint64_t *__restrict__ tile_g, uint64_t nb, uint64_t U, unsigned K, unsigned hb,
+    unsigned long long *__restrict__ cursor, Key<L> *__restrict__ out, uint32_t *__restrict__ hist = nullptr) {
+    using T = RcPartTraits<L>;
+    constexpr int BLOCK = T::BLOCK, ITEMS = T::ITEMS, TILE = T::TILE, GS = T::GS, PER = T::NBM / BLOCK > 0 ? T::NBM / BLOCK : 1;
+    __shared__ Key<L> s_keys[TILE];
+    __shared__ uint32_t s_cnt[T::NBM], s_loff[T::NBM];
+    __shared__ unsigned long long s_gbase[T::NBM];
+    __shared__ uint64_t s_us[GS + 1], s_bs[GS];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t tile = xcd_tile((U + TILE - 1) / TILE);  // grid = xcd_grid(tiles)
+    const uint64_t p0 = tile * TILE;
+    if (p0 >= U) return;
+    const uint64_t p1 = min(U, p0 + TILE);
+    const uint32_t nbk = 1u << hb;
+    for (uint32_t i = tid; i < nbk; i += BLOCK) s_cnt[i] = 0;
+    const uint64_t g0 = tile_g[tile];  // the canonical bucket holding p0: the last g with ustart[g] <= p0
+    for (uint32_t j = tid; j <= (uint32_t)GS; j += BLOCK) {
+        const uint64_t gi = g0 + j;
+        s_us[j] = gi <= nb ? ustart[gi] : ~0ull;
+        if (j < (uint32_t)GS) s_bs[j] = gi < nb ? bstart[gi] : 0;
+    }
+    __syncthreads();
+    const uint64_t send = s_us[GS];  // positions below this are inside the staged slice
+    // the staged bucket of every tile position, as a map in the (not yet used) key tile: each non-empty
+    // bucket starting inside the tile marks its first position, a block max-scan fills the rest
+    uint16_t *s_map = reinterpret_cast<uint16_t *>(s_keys);
+    static_assert(TILE % (8 * BLOCK) == 0 && TILE * 2 <= (int)sizeof(s_keys), "map layout");
+    for (uint32_t i = tid; i < TILE / 8; i += BLOCK) reinterpret_cast<uint4 *>(s_map)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (uint32_t i = tid + 1; i < (uint32_t)GS; i += BLOCK)
+        if (s_us[i] < s_us[i + 1] && s_us[i] < p1) s_map[s_us[i] - p0] = (uint16_t)i;  // s_us[i] > p0 (g0)
+    __syncthreads();
+    {
+        constexpr int PT = TILE / BLOCK;  // positions per thread, contiguous
+        uint16_t v[PT];
+#pragma unroll
+        for (int q = 0; q < PT / 8; ++q) {
+            const uint4 w = reinterpret_cast<const uint4 *>(s_map)[tid * (PT / 8) + q];
+            const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) v[8 * q + 2 * h] = (uint16_t)x[h], v[8 * q + 2 * h + 1] = (uint16_t)(x[h] >> 16);
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int q = 0; q < PT; ++q) m = max(m, (uint32_t)v[q]);
+        const uint32_t lane = tid & 63, wid = tid >> 6;
+        uint32_t inc = m;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(inc, off, 64);
+            if (lane >= (uint32_t)off) inc = max(inc, o);
+        }
+        uint32_t run = __shfl_up(inc, 1, 64);
+        if (lane == 0) run = 0;
+        if (lane == 63) s_scan[wid] = inc;
+        __syncthreads();
+        for (uint32_t w = 0; w < wid; ++w) run = max(run, s_scan[w]);
+#pragma unroll
+        for (int q = 0; q < PT; ++q) run = max(run, (uint32_t)v[q]), v[q] = (uint16_t)run;
+#pragma unroll
+        for (int q = 0; q < PT / 8; ++q) {
+            uint32_t x[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) x[h] = (uint32_t)v[8 * q + 2 * h] | ((uint32_t)v[8 * q + 2 * h + 1] << 16);
+            reinterpret_cast<uint4 *>(s_map)[tid * (PT / 8) + q] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+    }
+    __syncthreads();
+    // sources first, then all ITEMS loads in flight, then the rc keys ranked by bucket
+    uint64_t src[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t p = p0 + (uint64_t)j * BLOCK + tid;
+        src[j] = ~0ull;
+        if (p >= p1) continue;
+        if (p < send) {
+            const uint32_t i = s_map[j * BLOCK + tid];
+            src[j] = s_bs[i] + (p - s_us[i]);
+        } else {  // a tile spanning more than GS canonical buckets (sparse ones): search them all
+            uint64_t glo = g0 + GS - 1, ghi = nb;
+            while (glo < ghi) {
+                const uint64_t mid = (glo + ghi + 1) >> 1;
+                if (ustart[mid] <= p) glo = mid; else ghi = mid - 1;
+            }
+            src[j] = bstart[glo] + (p - ustart[glo]);
+        }
+    }
+    Key<L> k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        if (src[j] != ~0ull) k[j] = keys[src[j]];
+    uint32_t r[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        r[j] = 0xFFFFFFFFu;
+        if (src[j] == ~0ull) continue;
+        k[j] = revcomp2(k[j], K);
+        r[j] = atomicAdd(&s_cnt[bits_at(k[j], 2 * K - hb, hb)], 1u);
+    }
+    __syncthreads();
+    if constexpr (HIST) {
+        for (uint32_t i = tid; i < nbk; i += BLOCK)
+            if (s_cnt[i]) atomicAdd(&hist[i], s_cnt[i]);
+        return;
+    }
+    uint32_t c[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        c[q] = i < nbk ? s_cnt[i] : 0;
+        sum += c[q];
+    }
+    uint32_t total;
+    uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nbk) {
+            s_loff[i] = off;
+            s_gbase[i] = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
+        }
+        off += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        if (r[j] != 0xFFFFFFFFu) s_keys[s_loff[bits_at(k[j], 2 * K - hb, hb)] + r[j]] = k[j];
+    __syncthreads();
+    for (uint32_t q = tid; q < total; q += BLOCK) {
+        const Key<L> key = s_keys[q];
+        const uint32_t b = bits_at(key, 2 * K - hb, hb);
+        out[s_gbase[b] + (q - s_loff[b])] = key;
     }
 }
 

@@ -65,7 +65,7 @@ class Workspace {
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
-        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, NSLOTS
+        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, RC_L1START, RC_L1CUR, RC_TILEG, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -265,6 +265,9 @@ struct Ctx {
     bool kspec = true;             // MTG_KSPEC=0: the fused K1 passes with K a runtime argument at K = 31 too
     bool dist_pull = true;         // MTG_DIST_SINKS=query: the multi-GPU sink join by routed queries
                                    // (target_split + query_join) instead of the pulled edge slices
+    bool rc_fuse = false;          // MTG_RC_FUSE=1: the rc keys of a gapped canonical set written straight into
+                                   // the rc sort's level-1 buckets (rc_partition_gapped_kernel) -- measured
+                                   // even with the map + partition passes, so off
     bool dummy_bitmap = false;     // MTG_DUMMY_BITMAP=1: the source levels with few real chars as bits of a
                                    // bitmap (dummy_write_kernel) -- the sort gains 0.25 ms, the write pass
                                    // loses as much, so off by default
@@ -353,6 +356,7 @@ static void load_knobs(Ctx &c) {
     c.dist_pull = !is("MTG_DIST_SINKS", "query");
     c.kspec = !is("MTG_KSPEC", "0");
     c.dummy_bitmap = is("MTG_DUMMY_BITMAP", "1");
+    c.rc_fuse = is("MTG_RC_FUSE", "1");
     c.spec_l1_tiny = is("MTG_SPEC_L1_CAPS", "tiny");
     if (const char *e = getenv("MTG_SPEC_L1_STRIPES")) {
         const long v = atol(e);
@@ -2081,6 +2085,7 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
     using K2 = Key<L2>;
     uint64_t Urc = U;
     uint32_t *rc_hist = nullptr;
+    bool rc_level1 = false;  // buf already partitioned by the rc sort's level-1 digit
     if (K & 1) {
         unsigned rc_hist_bits = 0;
         if (!c.use_lsd && sort) {
@@ -2095,10 +2100,42 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
         if constexpr (!COUNTED) {
             if (c.gap.valid && c.gap.dst == (const void *)ka && sort) {
                 // the canonical set still in its speculative buckets (Ctx::gap): read it there
-                rc_map_gapped_kernel<L2><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(c.gap.nb, 16), 16384))),
-                                           dim3(256), 0, c.stream>>>((const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart,
-                                                                     c.gap.nb, buf, K, rc_hist, rc_hist_bits);
+                const bool fuse = c.rc_fuse && rc_hist && rc_hist_bits <= 9 && c.gap1_n == 0 && U;
+                const uint64_t tiles = ceil_div(U, RcPartTraits<L2>::TILE);
+                uint64_t *tile_g = nullptr;
+                if (fuse) {
+                    tile_g = (uint64_t *)c.ws.get(Workspace::RC_TILEG, tiles * 8);
+                    rc_tile_bucket_kernel<<<dim3((unsigned)ceil_div(c.gap.nb, 256)), dim3(256), 0, c.stream>>>(
+                        c.gap.ustart, c.gap.nb, RcPartTraits<L2>::TILE, tile_g);
+                    HIP_CHECK(hipGetLastError());
+                    rc_partition_gapped_kernel<L2, true><<<dim3((unsigned)xcd_grid(tiles)), dim3(512), 0, c.stream>>>(
+                        (const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart, tile_g, c.gap.nb, U, K, rc_hist_bits,
+                        nullptr, nullptr, rc_hist);
+                } else {
+                    rc_map_gapped_kernel<L2><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(c.gap.nb, 16), 16384))),
+                                               dim3(256), 0, c.stream>>>((const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart,
+                                                                         c.gap.nb, buf, K, rc_hist, rc_hist_bits);
+                }
                 HIP_CHECK(hipGetLastError());
+                if (fuse) {
+                    // the histogram above gives the level-1 bucket starts; the rc keys are then written
+                    // straight into their level-1 buckets (rc_partition_gapped_kernel)
+                    const uint64_t nbk = 1ull << rc_hist_bits;
+                    uint64_t *st = (uint64_t *)c.ws.get(Workspace::RC_L1START, (nbk + 1) * 8);
+                    auto *cur = (unsigned long long *)c.ws.get(Workspace::RC_L1CUR, nbk * 8);
+                    uint32_t ep;
+                    uint64_t *desc = acquire_desc(c, 1, &ep);
+                    HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+                    scan_counts_kernel<<<dim3(1), dim3(512), 0, c.stream>>>(rc_hist, nbk, st, desc, ep, &c.small->counter,
+                                                                           &c.small->error);
+                    HIP_CHECK(hipGetLastError());
+                    HIP_CHECK(hipMemcpyAsync(cur, st, nbk * 8, hipMemcpyDeviceToDevice, c.stream));
+                    rc_partition_gapped_kernel<L2><<<dim3((unsigned)xcd_grid(tiles)), dim3(512), 0, c.stream>>>(
+                        (const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart, tile_g, c.gap.nb, U, K, rc_hist_bits, cur,
+                        buf);
+                    HIP_CHECK(hipGetLastError());
+                    rc_level1 = true;
+                }
                 done = true;
             }
         }
@@ -2129,7 +2166,7 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
     uint32_t *rca = bufc, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
     if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
     else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true, nullptr,
-                                            false, rm);
+                                            rc_level1, rm);
     *rk = ra;
     *rkc = rca;
     return Urc;

@@ -65,17 +65,18 @@ def test_bench_generator_2m_reads_k31(canonical, bits):
     _assert_same(got, want, "2M reads k=31 canonical=%s bits=%d" % (canonical, bits))
 
 
-@pytest.mark.parametrize("knob", ["MTG_SPEC_RC", "MTG_DEFER_GATHER"])
-def test_bench_generator_speculative_fallbacks(monkeypatch, knob):
+@pytest.mark.parametrize("knob,val", [("MTG_SPEC_RC", "0"), ("MTG_DEFER_GATHER", "0"), ("MTG_RC_FUSE", "1")])
+def test_bench_generator_speculative_fallbacks(monkeypatch, knob, val):
     # the canonical set is left in its speculative buckets for the rc stage (no gather); with the rc
-    # sort's final level exact (MTG_SPEC_RC=0) the compact array is gathered on demand, and
-    # MTG_DEFER_GATHER=0 is the always-gather path
-    monkeypatch.setenv(knob, "0")
+    # sort's final level exact (MTG_SPEC_RC=0) the compact array is gathered on demand,
+    # MTG_DEFER_GATHER=0 is the always-gather path, and MTG_RC_FUSE=1 writes the rc keys straight
+    # into their level-1 buckets from the gapped set (rc_partition_gapped_kernel)
+    monkeypatch.setenv(knob, val)
     asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
     got, _ = _gpu_build(30, asc, True, 0)
     reads = [asc[i].tobytes() for i in range(len(asc))]
     want = O.build_chunk(30, reads, canonical=True, bits_per_count=0)
-    _assert_same(got, want, "2M reads k=31 canonical, %s=0" % knob)
+    _assert_same(got, want, "2M reads k=31 canonical, %s=%s" % (knob, val))
 
 
 @pytest.mark.parametrize("spec3", ["0", "1"])
