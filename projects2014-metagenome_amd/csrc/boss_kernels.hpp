@@ -504,8 +504,8 @@ __global__ __launch_bounds__(256) void rc_map_gapped_kernel(const Key<L> *__rest
  * ustart[g + 1] and is read at keys[bstart[g] + p - ustart[g]]: the tile's slice of (ustart, bstart) is
  * staged in LDS and a position -> bucket map is built there by a max-scan (a binary search per position
  * measured 1.15 ms per cfg2 rc set vs 0.71 for the separate partition pass; the map, 0.95).  The
- * histogram pass is the same kernel with HIST (rc_map_gapped_kernel without output, one wave per
- * canonical bucket: 0.39 ms).
+ * histogram pass is rc_map_gapped_kernel without output (0.39 ms; this kernel's own tiles counting
+ * only: 0.55).
  */
 template <int L>
 struct RcPartTraits {
@@ -515,8 +515,7 @@ struct RcPartTraits {
 };
 
 // tile_g[t] = the canonical bucket holding compact position t * TILE (one thread per bucket: the tiles
-// starting inside it) -- a per-tile binary search over ustart, 20 dependent loads, measured 0.64 ms for
-// the histogram pass against 0.39 for the wave-per-bucket one
+// starting inside it), in place of a per-tile binary search over ustart (~20 dependent loads)
 __global__ __launch_bounds__(256) void rc_tile_bucket_kernel(const uint64_t *__restrict__ ustart, uint64_t nb,
                                                              uint32_t tile, uint64_t *__restrict__ tile_g) {
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -525,12 +524,11 @@ __global__ __launch_bounds__(256) void rc_tile_bucket_kernel(const uint64_t *__r
     for (uint64_t t = (a + tile - 1) / tile; t * tile < e; ++t) tile_g[t] = g;
 }
 
-// HIST: the histogram pass (hist[b] += the tile's count of rc keys in level-1 bucket b), nothing written
-template <int L, bool HIST = false>
+template <int L>
 __global__ __launch_bounds__(512) void rc_partition_gapped_kernel(
     const Key<L> *__restrict__ keys, const uint64_t *__restrict__ bstart, const uint64_t *__restrict__ ustart,
     const uint64_t *__restrict__ tile_g, uint64_t nb, uint64_t U, unsigned K, unsigned hb,
-    unsigned long long *__restrict__ cursor, Key<L> *__restrict__ out, uint32_t *__restrict__ hist = nullptr) {
+    unsigned long long *__restrict__ cursor, Key<L> *__restrict__ out) {
     using T = RcPartTraits<L>;
     constexpr int BLOCK = T::BLOCK, ITEMS = T::ITEMS, TILE = T::TILE, GS = T::GS, PER = T::NBM / BLOCK > 0 ? T::NBM / BLOCK : 1;
     __shared__ Key<L> s_keys[TILE];
@@ -630,11 +628,6 @@ __global__ __launch_bounds__(512) void rc_partition_gapped_kernel(
         r[j] = atomicAdd(&s_cnt[bits_at(k[j], 2 * K - hb, hb)], 1u);
     }
     __syncthreads();
-    if constexpr (HIST) {
-        for (uint32_t i = tid; i < nbk; i += BLOCK)
-            if (s_cnt[i]) atomicAdd(&hist[i], s_cnt[i]);
-        return;
-    }
     uint32_t c[PER];
     uint32_t sum = 0;
 #pragma unroll

@@ -265,9 +265,9 @@ struct Ctx {
     bool kspec = true;             // MTG_KSPEC=0: the fused K1 passes with K a runtime argument at K = 31 too
     bool dist_pull = true;         // MTG_DIST_SINKS=query: the multi-GPU sink join by routed queries
                                    // (target_split + query_join) instead of the pulled edge slices
-    bool rc_fuse = false;          // MTG_RC_FUSE=1: the rc keys of a gapped canonical set written straight into
-                                   // the rc sort's level-1 buckets (rc_partition_gapped_kernel) -- measured
-                                   // even with the map + partition passes, so off
+    bool rc_fuse = true;           // MTG_RC_FUSE=0: the rc keys of a gapped canonical set written in canonical
+                                   // order and partitioned by the rc sort's own level 1, not straight into
+                                   // its level-1 buckets (rc_partition_gapped_kernel)
     bool dummy_bitmap = false;     // MTG_DUMMY_BITMAP=1: the source levels with few real chars as bits of a
                                    // bitmap (dummy_write_kernel) -- the sort gains 0.25 ms, the write pass
                                    // loses as much, so off by default
@@ -356,7 +356,7 @@ static void load_knobs(Ctx &c) {
     c.dist_pull = !is("MTG_DIST_SINKS", "query");
     c.kspec = !is("MTG_KSPEC", "0");
     c.dummy_bitmap = is("MTG_DUMMY_BITMAP", "1");
-    c.rc_fuse = is("MTG_RC_FUSE", "1");
+    c.rc_fuse = !is("MTG_RC_FUSE", "0");
     c.spec_l1_tiny = is("MTG_SPEC_L1_CAPS", "tiny");
     if (const char *e = getenv("MTG_SPEC_L1_STRIPES")) {
         const long v = atol(e);
@@ -2102,22 +2102,16 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
                 // the canonical set still in its speculative buckets (Ctx::gap): read it there
                 const bool fuse = c.rc_fuse && rc_hist && rc_hist_bits <= 9 && c.gap1_n == 0 && U;
                 const uint64_t tiles = ceil_div(U, RcPartTraits<L2>::TILE);
-                uint64_t *tile_g = nullptr;
+                // (fuse: the histogram only)
+                rc_map_gapped_kernel<L2><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(c.gap.nb, 16), 16384))),
+                                           dim3(256), 0, c.stream>>>((const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart,
+                                                                     c.gap.nb, fuse ? nullptr : buf, K, rc_hist, rc_hist_bits);
+                HIP_CHECK(hipGetLastError());
                 if (fuse) {
-                    tile_g = (uint64_t *)c.ws.get(Workspace::RC_TILEG, tiles * 8);
+                    uint64_t *tile_g = (uint64_t *)c.ws.get(Workspace::RC_TILEG, tiles * 8);
                     rc_tile_bucket_kernel<<<dim3((unsigned)ceil_div(c.gap.nb, 256)), dim3(256), 0, c.stream>>>(
                         c.gap.ustart, c.gap.nb, RcPartTraits<L2>::TILE, tile_g);
                     HIP_CHECK(hipGetLastError());
-                    rc_partition_gapped_kernel<L2, true><<<dim3((unsigned)xcd_grid(tiles)), dim3(512), 0, c.stream>>>(
-                        (const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart, tile_g, c.gap.nb, U, K, rc_hist_bits,
-                        nullptr, nullptr, rc_hist);
-                } else {
-                    rc_map_gapped_kernel<L2><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(c.gap.nb, 16), 16384))),
-                                               dim3(256), 0, c.stream>>>((const K2 *)c.gap.keys, c.gap.bstart, c.gap.ustart,
-                                                                         c.gap.nb, buf, K, rc_hist, rc_hist_bits);
-                }
-                HIP_CHECK(hipGetLastError());
-                if (fuse) {
                     // the histogram above gives the level-1 bucket starts; the rc keys are then written
                     // straight into their level-1 buckets (rc_partition_gapped_kernel)
                     const uint64_t nbk = 1ull << rc_hist_bits;

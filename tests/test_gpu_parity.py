@@ -168,7 +168,7 @@ def test_device_build_matches_host_build():
 
 @pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_DUMMY_SORT": "lifted"},
                                  {"MTG_FUSED": "0"}, {"MTG_FUSED_EMIT": "0"}, {"MTG_DUMMY_BITMAP": "1"},
-                                 {"MTG_RC_FUSE": "1"}])
+                                 {"MTG_RC_FUSE": "0"}])
 def test_alternate_device_paths(transcripts_1000, monkeypatch, env):
     # the unfused merge + emit, the compacting emit kernel, the unfused K1 and the LSD sorts
     # stay bit-exact too

@@ -65,12 +65,12 @@ def test_bench_generator_2m_reads_k31(canonical, bits):
     _assert_same(got, want, "2M reads k=31 canonical=%s bits=%d" % (canonical, bits))
 
 
-@pytest.mark.parametrize("knob,val", [("MTG_SPEC_RC", "0"), ("MTG_DEFER_GATHER", "0"), ("MTG_RC_FUSE", "1")])
+@pytest.mark.parametrize("knob,val", [("MTG_SPEC_RC", "0"), ("MTG_DEFER_GATHER", "0"), ("MTG_RC_FUSE", "0")])
 def test_bench_generator_speculative_fallbacks(monkeypatch, knob, val):
     # the canonical set is left in its speculative buckets for the rc stage (no gather); with the rc
     # sort's final level exact (MTG_SPEC_RC=0) the compact array is gathered on demand,
-    # MTG_DEFER_GATHER=0 is the always-gather path, and MTG_RC_FUSE=1 writes the rc keys straight
-    # into their level-1 buckets from the gapped set (rc_partition_gapped_kernel)
+    # MTG_DEFER_GATHER=0 is the always-gather path, and MTG_RC_FUSE=0 writes the rc keys in canonical
+    # order for the rc sort's own level 1 (not straight into its buckets: rc_partition_gapped_kernel)
     monkeypatch.setenv(knob, val)
     asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
     got, _ = _gpu_build(30, asc, True, 0)
