@@ -509,7 +509,10 @@ __global__ __launch_bounds__(256) void rc_map_gapped_kernel(const Key<L> *__rest
  */
 template <int L>
 struct RcPartTraits {
-    static constexpr int BLOCK = 512, ITEMS = L == 1 ? 16 : 8, TILE = BLOCK * ITEMS;
+#ifndef MTG_RCP_ITEMS
+#define MTG_RCP_ITEMS 16
+#endif
+    static constexpr int BLOCK = 512, ITEMS = L == 1 ? MTG_RCP_ITEMS : 8, TILE = BLOCK * ITEMS;
     static constexpr int NBM = 512;  // level-1 buckets at most (9 bits, rc_map_gapped_kernel's histogram)
     static constexpr int GS = 256;   // canonical buckets of the staged slice
 };
