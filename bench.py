@@ -72,6 +72,9 @@ def parse():
                     help="build from a KMC1 database of the reads' canonical k-mer counts (configs[4])")
     ap.add_argument("--parity-full-max", type=int, default=10_000_000,
                     help="largest read count whose whole workload the bench checks against the oracle")
+    ap.add_argument("--launch-timeout", type=float, default=None,
+                    help="seconds the ranks started by --gpus N (no launcher) may run before they are killed "
+                         "(default: 900 s + 10 s per step)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check on the CPU: every rank joins a gloo group and rank 0 prints the "
@@ -249,6 +252,41 @@ def cpu_baseline_kmc(args, kb, boss, kmc_base, n_records):
               "what": "GPU build (host C ABI) of the cpu_baseline record sample vs the oracle: W, last, "
                       "F, weights bit for bit"}
     return base, parity
+
+
+def full_parity_kmc(args, kb, boss, dc, dreads):
+    """configs[4]'s whole workload: the device chunk of the last timed step against the oracle built
+    from every decoded KMC record of this rank's database (each record one k-mer with its count, as
+    the reference's KMC branch feeds them: cli/parse_sequences.hpp:50-101, kmc_parser.cpp:27-62),
+    W, last, F, weights bit for bit.  Single-GPU lines only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle_ctypes
+    L = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    last = np.empty(dc.n, dtype=np.uint8)
+    wt = np.empty(dc.n, dtype=np.uint32)
+    L.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n)
+    L.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n)
+    L.mtg_memcpy_d2h(wt.ctypes.data, dc.weights, dc.n * 4)
+    F = np.array([int(f) for f in dc.F], dtype=np.uint64)
+    n = dreads.n_reads
+    seq = np.empty(dreads.seq_len, dtype=np.uint8)
+    starts = np.empty(n + 1, dtype=np.uint64)
+    counts = np.empty(n, dtype=np.uint32)
+    L.mtg_memcpy_d2h(seq.ctypes.data, dreads.seq, dreads.seq_len)
+    L.mtg_memcpy_d2h(starts.ctypes.data, dreads.read_starts, n * 8)
+    L.mtg_memcpy_d2h(counts.ctypes.data, dreads.counts, n * 4)
+    starts[n] = dreads.seq_len
+    t0 = time.perf_counter()
+    c = oracle_ctypes.build_chunk_packed(kb, seq, starts, canonical=args.mode == "canonical",
+                                         bits_per_count=args.count_width, counts=counts)
+    dt = time.perf_counter() - t0
+    same = (len(W) == len(c.W) and np.array_equal(W, c.W) and np.array_equal(last, c.last)
+            and np.array_equal(F, c.F) and np.array_equal(wt, c.weights))
+    return {"ok": bool(same), "rows": int(len(c.W)), "records": int(n), "oracle_s": dt,
+            "what": "the timed step's device chunk (all %d decoded KMC records of the workload) vs the oracle on "
+                    "the same records and counts: W, last, F, weights bit for bit" % n}
 
 
 def kmc_path(args, kb, boss, kmc_base, steps, n_records):
@@ -449,9 +487,14 @@ def launch_ranks(n, argv=None, timeout=None):
                 for q in pending:
                     q.terminate()
         if timeout is not None and time.time() - t0 > timeout and pending:
+            sys.stderr.write("bench.py: rank(s) %s still running after %.0f s; killing them\n"
+                             % (", ".join(str(procs.index(q)) for q in pending), timeout))
             for q in pending:
                 q.kill()
-            rc = rc or 124
+            for q in pending:
+                q.wait()
+            pending = []
+            rc = 124
         time.sleep(0.05)
     return rc
 
@@ -478,7 +521,8 @@ def dry_run(args, world, rank):
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))
+        limit = args.launch_timeout if args.launch_timeout else 900.0 + 10.0 * (args.steps + args.warmup)
+        sys.exit(launch_ranks(args.gpus, timeout=limit))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -637,7 +681,12 @@ def main():
             result["fasta_path"] = fasta_path(args, kb, boss, args.host_steps, args.fasta_reads)
     if rank == 0 and not args.no_cpu_baseline:
         if args.kmc:
-            result["cpu_baseline"], result["parity"] = cpu_baseline_kmc(args, kb, boss, kmc_base, kmers_per_rank)
+            result["cpu_baseline"], sample_parity = cpu_baseline_kmc(args, kb, boss, kmc_base, kmers_per_rank)
+            if world == 1:
+                result["parity"] = full_parity_kmc(args, kb, boss, dc, dreads)
+                result["parity"]["sample"] = sample_parity
+            else:
+                result["parity"] = sample_parity
         else:
             result["cpu_baseline"], sample_parity = cpu_baseline(args, kb, boss)
             if world == 1 and args.reads <= args.parity_full_max:

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 6
+#define MTG_BOSS_ABI_VERSION 7
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -148,6 +148,9 @@ typedef struct mtg_boss_timings {
     uint64_t sent_bytes;         /* multi-GPU: bytes this rank sent to the other ranks (every exchange) */
     uint64_t spec_l1;            /* 1: the fused extraction scattered into the speculative level-1 layout
                                     (a sampled histogram pass) */
+    uint64_t cached_bytes;       /* device blocks the workspace keeps idle for the next build (counted in
+                                    peak_bytes; freed when a build ends without reusing them, or by
+                                    mtg_boss_ctor_trim) */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);
@@ -156,6 +159,9 @@ const char *mtg_last_error(void);
 mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *params);
 void mtg_boss_ctor_destroy(mtg_boss_ctor *ctor);
 uint64_t mtg_boss_ctor_get_k(const mtg_boss_ctor *ctor);
+/* frees the device blocks the constructor's workspace keeps idle between builds (timings'
+   cached_bytes); a build also frees, when it ends, the kept blocks it did not reuse */
+int mtg_boss_ctor_trim(mtg_boss_ctor *ctor);
 
 /* n sequences, seqs[i] of lens[i] bytes, counts[i] (NULL = all 1).  Copies the input. */
 int mtg_boss_ctor_add_sequences(mtg_boss_ctor *ctor, const char *const *seqs,

@@ -87,7 +87,8 @@ class Timings(ctypes.Structure):
                [("n_batches", ctypes.c_uint64), ("peak_bytes", ctypes.c_uint64),
                 ("input_ms", ctypes.c_double), ("spilled_bytes", ctypes.c_uint64)] + \
                [(name, ctypes.c_uint64) for name in ("spec_levels", "spec_fine_levels", "spec_fallbacks",
-                                                      "collect_mode", "sent_bytes", "spec_l1")]
+                                                      "collect_mode", "sent_bytes", "spec_l1",
+                                                      "cached_bytes")]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -106,7 +107,8 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_boss_write_dbg", "mtg_sdsl_write", "mtg_boss_read_dbg", "mtg_dbg_file_free",
            "mtg_boss_ctor_add_fasta", "mtg_device_copy", "mtg_kmc_load_device",
            "mtg_device_reads_free", "mtg_kmc_write_device", "mtg_host_pool_bytes",
-           "mtg_host_pool_trim", "mtg_comm_create_callbacks", "mtg_comm_local_held_ms")
+           "mtg_host_pool_trim", "mtg_comm_create_callbacks", "mtg_comm_local_held_ms",
+           "mtg_boss_ctor_trim")
 
 COMM_ID_BYTES = 128
 
@@ -186,6 +188,7 @@ def lib():
                                            ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_char_p,
                                            P(ctypes.c_uint64)]
         L.mtg_dbg_file_free.argtypes = [P(_DbgFile)]
+        L.mtg_boss_ctor_trim.argtypes = [ctypes.c_void_p]
         for name in EXPORTS:
             getattr(L, name)
         _lib = L
@@ -437,6 +440,10 @@ class BOSSChunkConstructor:
         t = Timings()
         _check(lib().mtg_boss_last_timings(self._h, ctypes.byref(t)))
         return t
+
+    def trim(self):
+        """Free the device blocks the workspace keeps idle between builds (mtg_boss_ctor_trim)."""
+        _check(lib().mtg_boss_ctor_trim(self._h))
 
 
 class IBOSSChunkConstructor:

@@ -102,10 +102,14 @@ class Workspace {
             }
             b.ptr = p;
             b.cap = cap;
+            ++gen_[s];
         }
         return b.ptr;
     }
-    void swap(Slot a, Slot b) { std::swap(bufs_[a], bufs_[b]); }
+    void swap(Slot a, Slot b) {
+        std::swap(bufs_[a], bufs_[b]);
+        ++gen_[a], ++gen_[b];
+    }
     // the buffers a build's sort, rc, dummy and emit stages hold (not its input, look-back descriptors
     // or pass-A histograms): a build in rounds frees the previous build's before sizing its rounds
     void release_stage_buffers() {
@@ -128,6 +132,7 @@ class Workspace {
         }
         b.ptr = nullptr;
         b.cap = 0;
+        ++gen_[s];
     }
     // every byte the workspace holds, in slots and kept blocks
     uint64_t held() const {
@@ -152,12 +157,34 @@ class Workspace {
         for (auto &b : cache_) (void)hipFree(b.ptr);
         cache_.clear();
     }
+    // end of a build: free the kept blocks no get() took during it (released in an earlier build and
+    // idle since), so a big build's blocks do not pin HBM for the life of the constructor; the blocks
+    // this build gave back stay for the next build of the same shape
+    void end_build() {
+        bool any = false;
+        for (const auto &b : cache_) any |= b.age > 0;
+        if (any) {
+            HIP_CHECK(hipDeviceSynchronize());
+            std::vector<Buf> keep;
+            for (auto &b : cache_) {
+                if (b.age > 0) (void)hipFree(b.ptr);
+                else keep.push_back(b);
+            }
+            cache_.swap(keep);
+        }
+        for (auto &b : cache_) b.age = 1;
+    }
     uint64_t held_slot(Slot s) const { return bufs_[s].cap; }
+    const void *peek(Slot s) const { return bufs_[s].ptr; }
+    // bumped whenever the slot's buffer changes (regrown or released): a block given back may be
+    // handed to another slot, so a pointer comparison alone cannot tell that the data is still there
+    uint64_t generation(Slot s) const { return gen_[s]; }
 
   private:
     struct Buf {
         void *ptr = nullptr;
         size_t cap = 0;
+        uint32_t age = 0;  // kept blocks: builds ended since it was given back (end_build)
     };
     // the smallest kept block of at least `bytes` and at most about twice that (a far bigger block
     // stays for the request it was made for)
@@ -174,6 +201,7 @@ class Workspace {
         return p;
     }
     Buf bufs_[NSLOTS];
+    uint64_t gen_[NSLOTS] = {};
     std::vector<Buf> cache_;
 };
 
@@ -306,6 +334,8 @@ struct Ctx {
                              // sample-sized one (spec_final_level)
     bool spec_tiny = false;  // MTG_SPEC_CAPS=tiny: speculative buckets without slack (tests force the
                              // overflow fallback with it)
+    bool spec_lu_fail = false;  // MTG_SPEC_LU_FAIL=1: the speculative level's local unique pass reports an
+                                // overflow after it ran (tests the exact level after that late fallback)
     // MTG_SPEC_L1=0: the exact fused pass A (a histogram of every window) instead of the sampled one
     // and the speculative level-1 layout (fused_pass_b_spec), used from MTG_SPEC_L1_MIN windows on;
     // MTG_SPEC_L1_SAMPLE: pass A counts every n-th tile
@@ -324,6 +354,7 @@ struct Ctx {
     uint64_t bidx_n = 0;
     const uint64_t *bidx = nullptr;
     unsigned bidx_shift = 0;
+    uint64_t bidx_gen = 0;  // the BUCKETS slot's generation when the index was written
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
@@ -352,6 +383,7 @@ static void load_knobs(Ctx &c) {
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
     c.spec_tiny = is("MTG_SPEC_CAPS", "tiny");
+    c.spec_lu_fail = is("MTG_SPEC_LU_FAIL", "1");
     c.spec_l1 = !is("MTG_SPEC_L1", "0");
     c.dist_pull = !is("MTG_DIST_SINKS", "query");
     c.kspec = !is("MTG_KSPEC", "0");
@@ -745,7 +777,11 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             ++c.timings.spec_fallbacks;
             return ~0ull;
         }
-        if (g1) c.gap1_n = 0, c.gap1_tv = nullptr;  // read: the buckets below are compact per bucket
+        // g1: the padded input stays marked (Ctx::gap1_n) until this level succeeds -- a local pass that
+        // overflows below returns ~0 and the caller's exact level must read the padded array again
+        auto consumed_gap1 = [&]() {
+            if (g1) c.gap1_n = 0, c.gap1_tv = nullptr;  // the buckets below are compact per bucket
+        };
         if (rm) {  // the fused rc merge over the speculative buckets
             uint32_t *cnt = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
             spec_counts_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(bstart, cur, nb, cnt);
@@ -848,6 +884,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         uint32_t novf = 0;
         HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (c.spec_lu_fail) novf = 1;  // MTG_SPEC_LU_FAIL=1 (tests): as if a group had overflowed
         if (novf) {
             if (c.debug) fprintf(stderr, "[mtg debug] speculative level: %u groups overflowed, exact level\n", novf);
             c.radix_ms = 0, c.radix_launches = 0, c.radix_bytes = 0;
@@ -874,6 +911,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             HIP_CHECK(hipMemcpyAsync(gu + nb + 1, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
             const uint64_t u = read_u64(c, (const unsigned long long *)(ustart + nb));
             c.gap = Ctx::GappedSet{true, sb, *keys, u, nb, gb, gu};
+            consumed_gap1();
             ++c.timings.spec_levels;
             if (fine) ++c.timings.spec_fine_levels;
             c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gu};
@@ -901,6 +939,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         }
         HIP_CHECK(hipStreamSynchronize(c.stream));
         if (index && !ibad) c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gi};
+        consumed_gap1();
         ++c.timings.spec_levels;
         if (fine) ++c.timings.spec_fine_levels;
         if (c.debug)
@@ -2244,6 +2283,14 @@ static void note_bucket_index(Ctx &c, const void *keys, uint64_t n, const uint64
     c.bidx_n = n;
     c.bidx = start;
     c.bidx_shift = shift;
+    c.bidx_gen = c.ws.generation(Workspace::BUCKETS);
+}
+
+// the remembered bucket index still describes keys[0..n): the same array and count, and its entries still
+// in the BUCKETS slot it was written to (a released or regrown slot may now hold another stage's data)
+static bool bidx_valid(const Ctx &c, const void *keys, uint64_t n) {
+    return c.bidx && c.bidx_keys == keys && c.bidx_n == n && (const void *)c.bidx == c.ws.peek(Workspace::BUCKETS) &&
+           c.bidx_gen == c.ws.generation(Workspace::BUCKETS);
 }
 
 // K5/K6 on one device: dummy sinks and sources (all levels) of the sorted real edges ka[0..R)
@@ -2255,7 +2302,7 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
     const unsigned bshift = 2 * K - B;
     const uint64_t nb = 1ull << B;
     uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, (nb + 2) * 8);
-    if (!(c.bidx_keys == (const void *)ka && c.bidx_n == R && c.bidx_shift == bshift && c.bidx == bstart)) {
+    if (!(bidx_valid(c, ka, R) && c.bidx_shift == bshift && c.bidx == bstart)) {
         const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(R + 1, 256), 8192));
         bucket_index_kernel<L2><<<dim3((unsigned)g), dim3(256), 0, c.stream>>>(ka, R, bshift, nb, bstart);
         HIP_CHECK(hipGetLastError());
@@ -2360,7 +2407,7 @@ static void stage_merge_emit(Ctx &c, EventTimer &tm, int *ev_merge, unsigned k, 
         uint64_t *jsplit = (uint64_t *)c.ws.get(Workspace::SPLITS, (ntiles + 1) * 8);
         reset_small(c);
         if (D) {
-            const bool idx = c.bidx_keys == (const void *)real && c.bidx_n == R;
+            const bool idx = bidx_valid(c, real, R);
             dummy_rank_kernel<L2, L3><<<dim3((unsigned)ceil_div(D, 256)), dim3(256), 0, c.stream>>>(
                 real, R, dk, D, K, idx ? c.bidx : nullptr, c.bidx_shift, root ? 2 : 1, pos, wl,
                 &c.small->skip, &c.small->root_same);
@@ -3676,7 +3723,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         tr("exchange in-edge bytes", nback);
         // the bucket index of the owned edges, for the split emit's dummy ranks (unless the fused rc
         // merge wrote it)
-        if (!(c.bidx_keys == (const void *)E && c.bidx_n == R)) {
+        if (!bidx_valid(c, E, R)) {
             const unsigned B = bucket_bits<L2>(R, 2 * K);
             const unsigned bshift = 2 * K - B;
             uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << B) + 2) * 8);
@@ -4606,6 +4653,23 @@ void mtg_boss_ctor_destroy(mtg_boss_ctor *c) {
 
 uint64_t mtg_boss_ctor_get_k(const mtg_boss_ctor *c) { return c ? c->params.k : 0; }
 
+int mtg_boss_ctor_trim(mtg_boss_ctor *c) {
+    if (!c) {
+        set_error("bad arguments");
+        return MTG_ERR_ARGUMENT;
+    }
+    std::lock_guard<std::mutex> lock(c->mu);
+    try {
+        HIP_CHECK(hipSetDevice(c->device));
+        c->ctx.ws.drop_cache();
+        c->ctx.timings.cached_bytes = 0;
+        return MTG_OK;
+    } catch (const std::exception &e) {
+        set_error(e.what());
+        return MTG_ERR_DEVICE;
+    }
+}
+
 struct StageTimer {
     std::atomic<uint64_t> &acc;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
@@ -4807,10 +4871,12 @@ static void dispatch_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &
         const mtg::SuffixSpec spec = encode_suffix(c->suffix, &all_sentinel);
         mtg::run_suffix_dispatch(c->ctx, (unsigned)c->params.k, c->params.both_strands != 0,
                                  c->params.bits_per_count, spec, all_sentinel, in, out);
-        return;
+    } else {
+        run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0, c->params.bits_per_count,
+                     in, out);
     }
-    run_dispatch(c->ctx, comm, (unsigned)c->params.k, c->params.both_strands != 0, c->params.bits_per_count,
-                 in, out);
+    c->ctx.ws.end_build();  // idle kept blocks go back to the device
+    c->ctx.timings.cached_bytes = c->ctx.ws.cached();
 }
 
 static int run_build(mtg_boss_ctor *c, mtg::Comm *comm, const BuildInput &in, BuildOutput *out) {

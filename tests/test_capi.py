@@ -46,7 +46,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert boss.lib().mtg_boss_abi_version() == 6
+    assert boss.lib().mtg_boss_abi_version() == 7
 
 
 def test_invalid_arguments_fail_like_reference():

@@ -199,3 +199,11 @@ def test_bench_launcher_propagates_rank_failure():
     # a rank that fails makes the whole launch fail (the launcher exits non-zero)
     rc = bench.launch_ranks(2, ["--gpus", "2", "--dry-run", "--steps", "-x"], timeout=120)
     assert rc != 0
+
+
+def test_bench_launcher_kills_ranks_past_timeout(capfd):
+    # a rank still running at the launch limit (a hung collective looks like this) is killed and the
+    # launch exits 124, naming the ranks; the dry run's torch import outlasts 0.3 s
+    rc = bench.launch_ranks(2, ["--gpus", "2", "--dry-run"], timeout=0.3)
+    assert rc == 124
+    assert "still running" in capfd.readouterr().err

@@ -127,12 +127,16 @@ def test_bench_generator_speculative_overflow(monkeypatch, levels):
 
 
 @pytest.mark.parametrize("canonical,knobs", [(False, {}), (True, {}), (True, {"MTG_SPEC": "0"}),
-                                             (True, {"MTG_SPEC_L1_CAPS": "tiny"})])
+                                             (True, {"MTG_SPEC_L1_CAPS": "tiny"}),
+                                             (False, {"MTG_SPEC_LU_FAIL": "1"}),
+                                             (True, {"MTG_SPEC_LU_FAIL": "1"})])
 def test_bench_generator_speculative_level1(monkeypatch, canonical, knobs):
     # the fused K1's sampled pass A and speculative level-1 layout (fused_pass_b_spec; on by default
     # from 2^28 windows), forced on 2 M reads: the level-2 pass reads the padded segments through
     # tvalid -- speculative (default), exact (MTG_SPEC=0), or never reached because the segments were
-    # sized without slack and overflowed into the exact passes A and B (MTG_SPEC_L1_CAPS=tiny)
+    # sized without slack and overflowed into the exact passes A and B (MTG_SPEC_L1_CAPS=tiny).
+    # MTG_SPEC_LU_FAIL=1: the speculative level 2 partitions, then its local unique pass reports an
+    # overflow; the exact level 2 must still read the padded layout (the late fallback)
     monkeypatch.setenv("MTG_SPEC_L1_MIN", "0")
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
@@ -141,6 +145,8 @@ def test_bench_generator_speculative_level1(monkeypatch, canonical, knobs):
     assert t.n_extracted == 2_000_000 * 120
     if "MTG_SPEC_L1_CAPS" in knobs:
         assert t.spec_l1 == 0 and t.spec_fallbacks >= 1, (t.spec_l1, t.spec_fallbacks)
+    elif "MTG_SPEC_LU_FAIL" in knobs:
+        assert t.spec_l1 == 1 and t.spec_fallbacks >= 1, (t.spec_l1, t.spec_fallbacks)
     else:
         assert t.spec_l1 == 1, t.spec_l1
         if "MTG_SPEC" not in knobs:

@@ -227,7 +227,7 @@ def test_build_from_written_kmc_k31(tmp_path, canonical, bits):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,rounds", [(1, 0), (2, 0), (3, 0), (4, 0), (2, 3), (4, 5)])
+@pytest.mark.parametrize("P,rounds", [(1, 0), (2, 0), (3, 0), (4, 0), (2, 3), (4, 5), (8, 0), (8, 3)])
 def test_dist_build_from_kmc_k31(tmp_path, monkeypatch, P, rounds):
     # configs[4] across ranks: every rank counts its own reads into its own database; the ranks'
     # records meet at their owners, where the counts add with saturation (the count-aggregating
@@ -266,3 +266,55 @@ def test_dist_build_from_kmc_k31(tmp_path, monkeypatch, P, rounds):
             assert np.array_equal(getattr(got, a), getattr(want, a)), (a, canonical, bits)
         if rounds:
             assert all(c.timings().n_batches == rounds for c in ctors)
+
+
+# configs[4] at its full single-GPU size: the KMC1 database of the canonical k = 31 counts of 10 M
+# genome-sampled reads (~1.9e8 records, written by the GPU counter), decoded into HBM, built with
+# --count-kmers --count-width 8 and compared bit for bit (W, last, F, weights) with the oracle's build
+# of every decoded record with its count (kmc_parser.cpp:27-62, sorted_multiset.cpp:54-84)
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+def test_config4_full_kmc_database_vs_oracle(tmp_path):
+    torch = pytest.importorskip("torch")
+    import bench
+    dev = torch.device("cuda", 0)
+    n_reads, L = 10_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    base = str(tmp_path / "cfg5")
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, bits_per_count=8)
+    total = ctor.write_kmc(seq.data_ptr(), seq.numel(), base, 31, canonical=True)
+    del seq
+    torch.cuda.empty_cache()
+    assert total > 100_000_000, total
+    dr = boss.DeviceReads(base)
+    assert dr.n_reads == total
+    dc = ctor.build_device(*dr.build_args())
+    t = ctor.timings()
+    assert t.n_extracted == total
+    Lb = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    last = np.empty(dc.n, dtype=np.uint8)
+    wt = np.empty(dc.n, dtype=np.uint32)
+    assert Lb.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n) == 0
+    assert Lb.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n) == 0
+    assert Lb.mtg_memcpy_d2h(wt.ctypes.data, dc.weights, dc.n * 4) == 0
+    F = np.array([int(f) for f in dc.F], dtype=np.uint64)
+    n_real = dc.n_real
+    n = dr.n_reads
+    hseq = np.empty(dr.seq_len, dtype=np.uint8)
+    starts = np.empty(n + 1, dtype=np.uint64)
+    counts = np.empty(n, dtype=np.uint32)
+    assert Lb.mtg_memcpy_d2h(hseq.ctypes.data, dr.seq, dr.seq_len) == 0
+    assert Lb.mtg_memcpy_d2h(starts.ctypes.data, dr.read_starts, n * 8) == 0
+    assert Lb.mtg_memcpy_d2h(counts.ctypes.data, dr.counts, n * 4) == 0
+    starts[n] = dr.seq_len
+    del dr, ctor
+    # the decoded buffer is the database: record i is 31 chars + '$' at i * 32 with its count
+    assert np.array_equal(starts[:n], np.arange(n, dtype=np.uint64) * 32)
+    assert counts.min() >= 1
+    want = O.build_chunk_packed(30, hseq, starts, canonical=True, bits_per_count=8, counts=counts)
+    assert len(W) == len(want.W)
+    assert np.array_equal(W, want.W) and np.array_equal(last, want.last)
+    assert np.array_equal(F, want.F) and n_real == want.n_real
+    assert np.array_equal(wt, want.weights)
