@@ -965,6 +965,60 @@ __host__ __device__ inline uint64_t dummy_rank_space(unsigned k) {  // T(0)
     return (7ull * (1ull << (2 * k)) - 4) / 3;
 }
 
+// The same ranks in 128 bits for 30 < k <= 62 (7 4^62 < 2^128): BASELINE configs[2]'s k = 63 build
+// (k = 62) sorts 16-byte ranks (16 LSD passes) instead of its 32-byte lifted keys (24 passes).
+// dummy_rank_limbs(k): limbs of the rank word (1: u64, 2: u128, 0: no rank form, sort the lifted keys).
+typedef unsigned __int128 u128;
+__host__ __device__ constexpr int dummy_rank_limbs(unsigned k) { return k <= 30 ? 1 : k <= 62 ? 2 : 0; }
+template <int LR>
+struct RankWordT {
+    typedef uint64_t type;
+};
+template <>
+struct RankWordT<2> {
+    typedef u128 type;
+};
+template <int LR>
+using RankWord = typename RankWordT<LR>::type;
+
+// the inverse of 3 modulo 2^64 / 2^128: (7 W - 4 S) / 3 is exact (4^j = 1 mod 3, so W = S mod 3), and an
+// exact quotient is the product with the inverse (no 128-bit division on the device)
+template <typename R>
+__host__ __device__ constexpr R inv3() {
+    if constexpr (sizeof(R) == 16) return ((u128)0xAAAAAAAAAAAAAAAAull << 64) | 0xAAAAAAAAAAAAAAABull;
+    else return (R)0xAAAAAAAAAAAAAAABull;
+}
+template <typename R>
+__host__ __device__ inline R dummy_rank_space_t(unsigned k) {  // T(0) = (7 4^k - 4) / 3
+    return (((R)7 << (2 * k)) - 4) * inv3<R>();
+}
+// bits of the rank space (host): the LSD passes of the rank sort cover them
+inline unsigned dummy_rank_bits(unsigned k) {
+    const u128 t = dummy_rank_space_t<u128>(k);
+    const uint64_t hi = (uint64_t)(t >> 64), lo = (uint64_t)t;
+    return hi ? 128 - (unsigned)__builtin_clzll(hi) : 64 - (unsigned)__builtin_clzll(lo);
+}
+
+template <int LR>
+__device__ __forceinline__ Key<LR> rank_key(RankWord<LR> v) {
+    Key<LR> r;
+    r.w[0] = (uint64_t)v;
+    if constexpr (LR == 2) r.w[1] = (uint64_t)(v >> 64);
+    return r;
+}
+template <int LR>
+__device__ __forceinline__ RankWord<LR> rank_word(const Key<LR> &k) {
+    if constexpr (LR == 2) return ((u128)k.w[1] << 64) | k.w[0];
+    else return k.w[0];
+}
+// a 2-bit key of at most 2 limbs as one integer (the rank path: 2K <= 128)
+template <int L>
+__device__ __forceinline__ u128 key_u128(const Key<L> &k) {
+    static_assert(L <= 2, "rank path keys are at most 128 bits");
+    if constexpr (L == 2) return ((u128)k.w[1] << 64) | k.w[0];
+    else return k.w[0];
+}
+
 // the lifted key as one 128-bit integer (k <= 30: 3 (k + 1) <= 93 bits)
 template <int L3>
 __device__ __forceinline__ unsigned __int128 lifted128(const Key<L3> &x) {
@@ -976,11 +1030,16 @@ __device__ __forceinline__ unsigned __int128 lifted128(const Key<L3> &x) {
 __device__ __forceinline__ uint64_t char_sum2(uint64_t w) {
     return (uint64_t)__popcll(w & 0x5555555555555555ull) + 2ull * (uint64_t)__popcll(w & 0xAAAAAAAAAAAAAAAAull);
 }
+__device__ __forceinline__ uint64_t char_sum2(u128 w) { return char_sum2((uint64_t)w) + char_sum2((uint64_t)(w >> 64)); }
 
 // rank of the dummy with m real node chars forming the 2-bit word W (r_1 highest, $ run below) and
 // label c (0..3; ignored for a sink, m = k)
 __device__ __forceinline__ uint64_t dummy_rank(uint64_t W, unsigned m, unsigned k, uint32_t c) {
     return 4ull * m + (7 * W - 4 * char_sum2(W)) / 3 + (m < k ? (uint64_t)c : 0ull);
+}
+template <typename R>
+__device__ __forceinline__ R dummy_rank_t(R W, unsigned m, unsigned k, uint32_t c) {
+    return (R)(4u * m) + (7 * W - 4 * (R)char_sum2(W)) * inv3<R>() + (R)(m < k ? c : 0u);
 }
 
 // The source levels with few real chars (m <= DUMMY_BITMAP_M: levels k - m) repeat: a level-(k - m)
@@ -995,18 +1054,21 @@ __host__ __device__ constexpr uint64_t dummy_bitmap_base(unsigned m) {  // bits 
     return ((1ull << (2 * (m + 1))) - 4) / 3;
 }
 
-// RANKS (k <= 30): the dummies as their dense u64 ranks (dummy_rank, below) straight from the 2-bit
-// edge -- a sink's real chars are the edge's target node (x >> 2 with the label moved on top), a
-// level-l source's are the edge's first k - l node chars shifted up l places -- instead of lifted keys.
-// bitmap (RANKS): the levels above kbig (m = k - level <= DUMMY_BITMAP_M) go to the bitmap instead
-// (the count pass counted kbig levels per source); nullptr: every level written (kbig = k)
-template <int L2, int L3, bool RANKS = false>
+// RANKS (k <= 62): the dummies as their dense ranks (dummy_rank, u64 for k <= 30: LR = 1, u128 for
+// k <= 62: LR = 2) straight from the 2-bit edge -- a sink's real chars are the edge's target node
+// (x >> 2 with the label moved on top), a level-l source's are the edge's first k - l node chars shifted
+// up l places -- instead of lifted keys.
+// bitmap (RANKS, LR = 1): the levels above kbig (m = k - level <= DUMMY_BITMAP_M) go to the bitmap
+// instead (the count pass counted kbig levels per source); nullptr: every level written (kbig = k)
+template <int L2, int L3, bool RANKS = false, int LR = 1>
 __global__ __launch_bounds__(256) void dummy_write_kernel(
     const Key<L2> *__restrict__ keys, const uint8_t *__restrict__ flags,
     const uint8_t *__restrict__ in_flag, uint64_t n, unsigned K,
     const uint64_t *__restrict__ toff, Key<L3> *__restrict__ out, unsigned kbig = 0,
     uint32_t *__restrict__ bitmap = nullptr) {
+    static_assert(!RANKS || LR == 1 || L2 <= 2, "u128 ranks: 2-bit keys of at most 128 bits");
     uint64_t *rout = reinterpret_cast<uint64_t *>(out);
+    Key<2> *rout2 = reinterpret_cast<Key<2> *>(out);
     __shared__ uint32_t s_scan[256 / 64 + 1];
     __shared__ uint16_t s_src[4096];  // tile-relative edge index of each source
     const uint32_t tid = threadIdx.x;
@@ -1030,12 +1092,23 @@ __global__ __launch_bounds__(256) void dummy_write_kernel(
             const Key<L2> x = keys[i0 + j];
             const Key<L2> t = (shr(x, 2) | shl(Key<L2>::from(x.w[0] & 3), 2 * (K - 1))) &
                               ~Key<L2>::from(3);
-            if constexpr (RANKS) rout[base + so++] = dummy_rank(t.w[0] >> 2, k, k, 0);
+            if constexpr (RANKS && LR == 2) rout2[base + so++] = rank_key<2>(dummy_rank_t<u128>(key_u128(t) >> 2, k, k, 0));
+            else if constexpr (RANKS) rout[base + so++] = dummy_rank(t.w[0] >> 2, k, k, 0);
             else out[base + so++] = lift_fast<L3>(t, K) & ~Key<L3>::from(7);
         }
         if ((m >> (16 + j)) & 1u) s_src[qo++] = (uint16_t)(tid * 16 + j);
     }
     __syncthreads();
+    if constexpr (RANKS && LR == 2) {
+        Key<2> *o = rout2 + base + nsink;
+        for (uint32_t it = tid; it < nsrc * k; it += 256) {
+            const uint32_t q = it / k, lev = it - q * k + 1;  // level 1 .. k
+            const u128 node = key_u128(keys[t0 + s_src[q]]) >> 2;  // a_1 .. a_k, a_1 lowest
+            const u128 low = node & ((((u128)1) << (2 * (k - lev))) - 1);  // a_1 .. a_(k - lev)
+            o[it] = rank_key<2>(dummy_rank_t<u128>(low << (2 * lev), k - lev, k, (uint32_t)(node >> (2 * (k - lev))) & 3u));
+        }
+        return;
+    }
     if constexpr (RANKS) {
         uint64_t *o = rout + base + nsink;
         const unsigned kb = bitmap ? kbig : k;
@@ -1624,28 +1697,29 @@ __global__ __launch_bounds__(256) void emit_kernel(
 }
 
 
-template <int L3>
+template <int L3, int LR = 1>
 __global__ void dummy_encode_kernel(const Key<L3> *__restrict__ in, uint64_t n, unsigned k,
-                                    uint64_t *__restrict__ out, uint32_t *__restrict__ bad) {
+                                    Key<LR> *__restrict__ out, uint32_t *__restrict__ bad) {
+    using R = RankWord<LR>;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     bool err = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-        const unsigned __int128 v = lifted128(in[i]);
-        uint64_t W = 0;
+        const Key<L3> v = in[i];
+        R W = 0;
         unsigned m = 0, top_dollar = 0;  // highest node position holding $
         for (unsigned j = 1; j <= k; ++j) {
-            const uint32_t ch = (uint32_t)(v >> (3 * j)) & 7u;
+            const uint32_t ch = char_at(v, j, 3);
             if (ch) {
-                W |= (uint64_t)(ch - 1) << (2 * (j - 1));
+                W |= (R)(ch - 1) << (2 * (j - 1));
                 ++m;
             } else {
                 top_dollar = j;
             }
         }
-        const uint32_t c = (uint32_t)v & 7u;
+        const uint32_t c = (uint32_t)v.w[0] & 7u;
         // the $ run must be exactly node positions 1 .. k - m, the label real iff m < k
-        err |= top_dollar != k - m || (m < k) != (c != 0) || c > 4 || (v >> (3 * (k + 1))) != 0;
-        out[i] = dummy_rank(W, m, k, c - 1);
+        err |= top_dollar != k - m || (m < k) != (c != 0) || c > 4 || shr(v, 3 * (k + 1)) != Key<L3>::zero();
+        out[i] = rank_key<LR>(dummy_rank_t<R>(W, m, k, c - 1));
     }
     if (err) atomicOr(bad, 1u);
 }
@@ -1672,36 +1746,31 @@ __global__ void dummy_bitmap_ranks_kernel(const uint32_t *__restrict__ bitmap, u
     }
 }
 
-template <int L3>
-__global__ void dummy_decode_kernel(const uint64_t *__restrict__ in, uint64_t n, unsigned k, Key<L3> *__restrict__ out) {
+template <int L3, int LR = 1>
+__global__ void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n, unsigned k, Key<L3> *__restrict__ out) {
+    using R = RankWord<LR>;
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t T0 = dummy_rank_space(k);
+    const R T0 = dummy_rank_space_t<R>(k);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-        uint64_t r = in[i], T = T0;
+        R r = rank_word<LR>(in[i]), T = T0;
         // the real chars r_1, r_2, ... enter at the bottom of x one by one (r_p ends up at node
         // position k - p + 1); then one shift leaves the $ run and the label below them
-        unsigned __int128 x = 0;
+        Key<L3> x = Key<L3>::zero();
         unsigned m = 0;
         uint64_t label = 0;  // $ for a sink
         for (unsigned p = 1; p <= k; ++p) {
             if (r < 4) {  // a source of level k - (p - 1): its label
-                label = r + 1;
+                label = (uint64_t)r + 1;
                 break;
             }
             r -= 4;
             T = (T - 4) >> 2;  // T(p): strings below one real char at depth p
-            const uint64_t rp = (uint64_t)(r >= T) + (r >= 2 * T) + (r >= 3 * T);
+            const R rp = (R)(r >= T) + (R)(r >= 2 * T) + (R)(r >= 3 * T);
             r -= rp * T;
-            x = (x << 3) | (rp + 1);
+            x = shl(x, 3) | Key<L3>::from((uint64_t)rp + 1);
             ++m;
         }
-        x = (x << (3 * (k - m) + 3)) | label;
-        Key<L3> o;  // all k node chars real and no label: a sink ($)
-        o.w[0] = (uint64_t)x;
-        if constexpr (L3 > 1) o.w[1] = (uint64_t)(x >> 64);
-#pragma unroll
-        for (int q = 2; q < L3; ++q) o.w[q] = 0;
-        out[i] = o;
+        out[i] = shl(x, 3 * (k - m) + 3) | Key<L3>::from(label);
     }
 }
 

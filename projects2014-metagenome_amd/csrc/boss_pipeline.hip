@@ -80,10 +80,25 @@ class Workspace {
             void *p = take_cached(bytes, &cap);
             if (!p) {
                 cap = bytes + bytes / 8;
+                const auto t0 = std::chrono::steady_clock::now();
+                bool dropped = false;
                 if (hipMalloc(&p, cap) != hipSuccess) {
                     (void)hipGetLastError();
-                    drop_cache();
-                    if (hipMalloc(&p, cap) != hipSuccess) {
+                    // no room for a new block: a kept block that holds the request, however big (freeing
+                    // kept blocks is what costs: ~12 ms per GB while the driver clears them, 2.3 s a build
+                    // at configs[2] when every failed allocation dropped the whole cache), and only then
+                    // kept blocks freed one at a time, largest first
+                    p = take_cached(bytes, &cap, true);
+                    while (!p && !cache_.empty()) {
+                        dropped = true;
+                        drop_largest();
+                        cap = bytes + bytes / 8;
+                        if (hipMalloc(&p, cap) != hipSuccess) {
+                            (void)hipGetLastError();
+                            p = nullptr;
+                        }
+                    }
+                    if (!p && hipMalloc(&p, cap) != hipSuccess) {
                         (void)hipGetLastError();
                         size_t fr = 0, tot = 0;
                         (void)hipMemGetInfo(&fr, &tot);
@@ -94,6 +109,11 @@ class Workspace {
                                                  " MiB)");
                     }
                 }
+                if (trace && cap >= (1ull << 28))
+                    fprintf(stderr, "[mtg trace] workspace slot %d: new %lu MiB%s, %.1f ms (held %lu MiB, kept %lu MiB)\n",
+                            (int)s, (unsigned long)(cap >> 20), dropped ? " after dropping the kept blocks" : "",
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                            (unsigned long)(held() >> 20), (unsigned long)(cached() >> 20));
             }
             if (keep && b.ptr) HIP_CHECK(hipMemcpyAsync(p, b.ptr, keep, hipMemcpyDeviceToDevice, stream));
             if (b.ptr) {
@@ -151,6 +171,15 @@ class Workspace {
         HIP_CHECK(hipMemGetInfo(&fr, &tot));
         return (uint64_t)fr + cached();
     }
+    void drop_largest() {
+        if (cache_.empty()) return;
+        HIP_CHECK(hipDeviceSynchronize());
+        size_t big = 0;
+        for (size_t i = 1; i < cache_.size(); ++i)
+            if (cache_[i].cap > cache_[big].cap) big = i;
+        (void)hipFree(cache_[big].ptr);
+        cache_.erase(cache_.begin() + (long)big);
+    }
     void drop_cache() {
         if (cache_.empty()) return;
         HIP_CHECK(hipDeviceSynchronize());
@@ -187,11 +216,11 @@ class Workspace {
         uint32_t age = 0;  // kept blocks: builds ended since it was given back (end_build)
     };
     // the smallest kept block of at least `bytes` and at most about twice that (a far bigger block
-    // stays for the request it was made for)
-    void *take_cached(size_t bytes, size_t *cap) {
+    // stays for the request it was made for); any: no upper bound (the device has no room left)
+    void *take_cached(size_t bytes, size_t *cap, bool any = false) {
         size_t best = cache_.size();
         for (size_t i = 0; i < cache_.size(); ++i)
-            if (cache_[i].cap >= bytes && cache_[i].cap <= 2 * bytes + (64u << 20) &&
+            if (cache_[i].cap >= bytes && (any || cache_[i].cap <= 2 * bytes + (64u << 20)) &&
                 (best == cache_.size() || cache_[i].cap < cache_[best].cap))
                 best = i;
         if (best == cache_.size()) return nullptr;
@@ -202,6 +231,11 @@ class Workspace {
     }
     Buf bufs_[NSLOTS];
     uint64_t gen_[NSLOTS] = {};
+
+  public:
+    bool trace = false;  // MTG_TRACE: report every fresh allocation of 256 MiB or more
+
+  private:
     std::vector<Buf> cache_;
 };
 
@@ -285,6 +319,7 @@ struct Ctx {
     unsigned fused_b1 = 0;         // MTG_FUSED_B1=n: the fused K1's level-1 digit forced to n bits (A/B runs)
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
     bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
+    bool lu_lean = false;          // MTG_LU_LEAN=1: the speculative level's local pass as local_unique_lean_kernel
     uint32_t merge_it = 1;         // MTG_MERGE_IT: local_merge_kernel's least outputs per thread (A/B)
     bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
     bool kmc_mirror = true;  // add_kmc copies the first database to the device while reading it
@@ -376,6 +411,7 @@ static void load_knobs(Ctx &c) {
     c.wide_b1 = !is("MTG_WIDE_B1", "0");
     c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
     c.lu_fast = !is("MTG_LU_FAST", "0");
+    c.lu_lean = is("MTG_LU_LEAN", "1");
     if (const char *e = getenv("MTG_MERGE_IT")) c.merge_it = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
     c.spec_final = !is("MTG_SPEC", "0");
@@ -403,6 +439,7 @@ static void load_knobs(Ctx &c) {
     c.force_spill = is("MTG_SPILL", "1");
     c.debug = getenv("MTG_DEBUG") != nullptr;
     c.trace = getenv("MTG_TRACE") != nullptr;
+    c.ws.trace = c.trace;
     if (const char *e = getenv("MTG_FUSED_MIN")) c.fused_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("MTG_RANGES")) c.force_ranges = (uint32_t)std::max(0L, std::min(4096L, atol(e)));
     if (const char *e = getenv("MTG_HIST_ROWS")) c.hist_rows = (uint32_t)std::max(1L, std::min(2048L, atol(e)));
@@ -419,6 +456,21 @@ static uint64_t read_u64(Ctx &c, const unsigned long long *p) {
     HIP_CHECK(hipStreamSynchronize(c.stream));
     return v;
 }
+
+// MTG_TRACE: host wall time since the previous trace point (stream drained first)
+struct Tracer {
+    Ctx &c;
+    int rank;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void operator()(const char *what, uint64_t a = 0, uint64_t b = 0) {
+        if (!c.trace) return;
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[mtg trace r%d] %-22s %9.3f ms  %lu %lu\n", rank, what,
+                std::chrono::duration<double, std::milli>(now - t).count(), (unsigned long)a, (unsigned long)b);
+        t = now;
+    }
+};
 
 static void check_error_word(Ctx &c) {
     uint32_t e = 0;
@@ -867,7 +919,10 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // fraction of them); the others count 0 keys
         HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
         bucket_pieces(blo, bhi, [&](uint64_t g0, unsigned cnt) {
-            if (keycas && c.lu_fast)
+            if (!COUNTED && keycas && c.lu_lean)
+                local_unique_lean_kernel<LocalTraits<1>::SLOTS / 2><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                    (const uint64_t *)sa, bstart, cur, (uint64_t *)sb, ucount, ovf, &c.small->counter, g0);
+            else if (keycas && c.lu_fast)
                 local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE, true>
                     <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
                                                             &c.small->counter, cmax, cur, g0);
@@ -1219,6 +1274,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             return nov;
         };
         uint32_t novf = launch_local(nullptr, ngroups, 0);
+        if (c.trace)
+            fprintf(stderr, "[mtg trace] msd n=%lu levels=%u b=%u groups=%lu overflow=%u\n", (unsigned long)n, levels, b,
+                    (unsigned long)ngroups, novf);
         if (c.debug)
             fprintf(stderr, "[mtg debug] msd n=%lu nbits=%u levels=%u b=%u buckets=%lu groups=%lu overflow=%u\n",
                     (unsigned long)n, nbits, levels, b, (unsigned long)nbuckets, (unsigned long)ngroups, novf);
@@ -1500,8 +1558,8 @@ struct FusedA {
     std::vector<uint32_t> h;   // their sum over the 2^FUSED_HB top-bit bins (host)
 };
 
-static bool fused_applies(const Ctx &c, unsigned K, uint64_t npos) {
-    return c.fused && !c.use_lsd && npos >= c.fused_min && npos >= 4096 && K - 1 >= FUSED_HB / 2 && K <= 32;
+static bool fused_applies(const Ctx &c, unsigned K, uint64_t npos, unsigned kmax = 32) {
+    return c.fused && !c.use_lsd && npos >= c.fused_min && npos >= 4096 && K - 1 >= FUSED_HB / 2 && K <= kmax;
 }
 
 // pass A over every window, and the duplication estimate from a sample of windows (on a side stream
@@ -1521,13 +1579,22 @@ static void launch_part_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, A... a) {
 // sample > 1 (fused_pass_b_spec): every row counts every sample-th of its tiles, and the 2048 rows form
 // c.spec_l1_stripes stripes (A->h, A->N are then estimates)
 constexpr uint32_t kSpecRows = 2048;
-static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &in, FusedA *A, uint32_t sample = 1) {
+static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &in, FusedA *A, uint32_t sample = 1,
+                         int fbk = 512) {
+    // fbk: pass B's workgroup size (fused_block<L>: 512 for u64 keys, 256 for u128); K > 32: the wide
+    // histogram kernel (u128 windows)
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
     constexpr uint32_t M = 1u << 19, SLOTS = 1u << 21;
     unsigned long long *table = (unsigned long long *)c.ws.get(Workspace::DUP_TABLE, (SLOTS + 2) * 8ull);
     HIP_CHECK(hipMemsetAsync(table, 0, (SLOTS + 2) * 8ull, c.stream));
-    dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
-                                                                          M, table, SLOTS - 1, table + SLOTS);
+    // (K > 32: the sampled k-mers need u128 words -- truncated to 64 bits, distinct k-mers collided and
+    // the duplication estimate planned too few MSD bits for the u128 rounds)
+    if (K > 32)
+        dup_sample_reads_kernel<2><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                              M, table, SLOTS - 1, table + SLOTS);
+    else
+        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                              M, table, SLOTS - 1, table + SLOTS);
     HIP_CHECK(hipGetLastError());
     constexpr int TILE = ExtractTraits<1>::TILE;
     const uint64_t tiles = ceil_div(npos, TILE);
@@ -1536,9 +1603,9 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
     // workgroups per CU).  With XCD-contiguous tiles and stripes the short runs of neighbouring tiles
     // meet in one L2: extract stage 6.97 -> 5.61 ms vs 1024-thread tiles (16 K windows), which won
     // before the XCD mapping (their longer runs: PMC writes 1.16 vs 1.30 x N w)
-    const int fbk = 512;
     const uint32_t rps = (uint32_t)(16 * fbk / TILE);
-    uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
+    // (stripe_cursor_kernel takes at most 1024 stripes: 2048 rows at rps = 2, 1024 at rps = 1)
+    uint32_t nrows = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(tiles, c.hist_rows), 1024ull * rps);
     if (nrows >= rps) nrows -= nrows % rps;
     const unsigned hb = FUSED_HB;
     const uint32_t nbh = 1u << hb;
@@ -1566,8 +1633,17 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
         stripes = (uint32_t)ceil_div(tiles_b, per_stripe);
         rps_out = srps;
     }
-    launch_hist_fast<false>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, canonical ? 1 : 0, tiles, per_row, rows,
-                            (uint32_t *)nullptr, sample);
+    if (K > 32) {
+        if (K == 63 && c.kspec)
+            extract_hist_wide_kernel<63><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                              tiles, per_row, rows, sample);
+        else
+            extract_hist_wide_kernel<0><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+                                                                             tiles, per_row, rows, sample);
+    } else {
+        launch_hist_fast<false>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, canonical ? 1 : 0, tiles, per_row,
+                                rows, (uint32_t *)nullptr, sample);
+    }
     HIP_CHECK(hipGetLastError());
     hist_rows_reduce_kernel<<<dim3(std::min<uint32_t>(nrows, 256), (unsigned)ceil_div(nbh, 256)), dim3(256), 0,
                               c.stream>>>(rows, nrows, nbh, h12);
@@ -1606,9 +1682,9 @@ struct BucketSel {
 // pass B: the k-mers whose level-1 bucket (top b1 bits) is in `sel` (nullptr: every bucket)
 // scattered into ka by that bucket; returns their number and their level-1 counts in *dh1 (device;
 // zero outside `sel`)
-template <bool COUNTED>
+template <int L, bool COUNTED>
 static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
-                             const FusedA &A, unsigned b1, const BucketSel *sel, Key<1> *ka, uint32_t *ca,
+                             const FusedA &A, unsigned b1, const BucketSel *sel, Key<L> *ka, uint32_t *ca,
                              const uint32_t **dh1_out) {
     const uint32_t nb1 = 1u << b1;
     const unsigned hb = FUSED_HB;
@@ -1638,6 +1714,7 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
     // per-stripe cursors (stripe_cursor_kernel): pass-B tile t writes through stripe t / per_stripe
     static_assert(FusedTraits<COUNTED, 512>::TILE == 2 * ExtractTraits<1>::TILE, "a pass-B tile = 2 pass-A tiles");
+    static_assert(FusedTraits<COUNTED, fused_block<2>()>::TILE == ExtractTraits<1>::TILE, "u128: a pass-B tile = 1 pass-A tile");
     auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)A.stripes * nb1 * 16);
     unsigned long long *send = scur + (size_t)A.stripes * nb1;
     stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(A.rows, A.nrows, hb, b1, A.stripes, A.rps, dcur, scur,
@@ -1645,8 +1722,21 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     HIP_CHECK(hipGetLastError());
     EventTimer tm(c.stream);
     tm.mark();
-    const bool fast_b = !COUNTED && K <= 32;
-    if (fast_b) {
+    const bool fast_b = L == 1 && !COUNTED && K <= 32;
+    if constexpr (L == 2) {
+        // u128 windows (K <= 64): the generic pass B on 256-thread tiles (A was made for them)
+        constexpr int B = fused_block<2>();
+        if (b1 > 9) throw std::runtime_error("the u128 pass B takes at most 9 bits");
+        const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, B>::TILE);
+        if (K == 63 && c.kspec)
+            extract_partition_kernel<2, COUNTED, B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
+                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
+                A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
+        else
+            extract_partition_kernel<2, COUNTED, B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
+                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
+                A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
+    } else if (fast_b) {
         constexpr int B = 512;
         const dim3 g((unsigned)xcd_grid(ceil_div(A.npos, 16 * B)));
         if (b1 > 9)
@@ -1658,9 +1748,9 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     } else {
         if (b1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, 512>::TILE);
-        extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+        extract_partition_kernel<1, COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
             in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
-            A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
+            A.per_stripe, scur, send, (Key<1> *)ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
     }
     HIP_CHECK(hipGetLastError());
     cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)A.stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
@@ -1805,7 +1895,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(N, 1) * 8);
         *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(N, 1) * 4) : nullptr;
         *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(N, 1) * 4) : nullptr;
-        fused_pass_b<COUNTED>(c, K, canonical, cmax, in, A, b1, nullptr, *ka, COUNTED ? *ca : nullptr, hist1_out);
+        fused_pass_b<1, COUNTED>(c, K, canonical, cmax, in, A, b1, nullptr, *ka, COUNTED ? *ca : nullptr, hist1_out);
         c.timings.n_positions = npos;
         c.timings.n_extracted = N;
         *N_out = N;
@@ -1996,19 +2086,33 @@ static uint64_t collect_ranges(Ctx &c, unsigned K, bool canonical, uint32_t cmax
 // one-pass build (the role of SortedSetDisk's merged chunks, boss_chunk_construct.cpp:664-933).
 // R is the fewest rounds whose sort buffers fit next to what the later stages hold
 // (memory_preallocated, else the free HBM).  False (nothing kept) where the fused K1 does not apply.
-template <bool COUNTED>
+template <int L, bool COUNTED>
 static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
-                                 Key<1> **out, uint32_t **outc, uint64_t *U_out) {
-    using K2 = Key<1>;
+                                 Key<L> **out, uint32_t **outc, uint64_t *U_out) {
+    // L = 2: u128 windows (32 < K <= 64, BASELINE configs[2]'s k = 63) -- the wide pass A and the generic
+    // pass B on 256-thread tiles; the later levels are the MSD sort's exact ones
+    using K2 = Key<L>;
     const uint64_t npos = in.seq_len >= K ? in.seq_len - K + 1 : 0;
-    if (c.range_scan || c.disk || !fused_applies(c, K, npos)) return false;
+    if (c.range_scan || c.disk || !fused_applies(c, K, npos, L == 1 ? 32 : 64)) return false;
     // a previous build's stage buffers would crowd out this build's rounds: they go now (and are
     // allocated again at the sizes this build needs)
+    Tracer tr{c, 0};
     c.ws.release_stage_buffers();
+    tr("rounds: release");
     FusedA A;
-    fused_pass_a(c, K, canonical, in, &A);
+    fused_pass_a(c, K, canonical, in, &A, 1, fused_block<L>());
+    tr("rounds: pass A", A.N, (uint64_t)(A.dup * 1000));
     const uint64_t N = A.N;
-    const MsdPlan plan = fused_plan(c, N, 2 * K, A.dup, !COUNTED && K <= 32);
+    MsdPlan plan = L == 1 ? fused_plan(c, N, 2 * K, A.dup, !COUNTED && K <= 32) : msd_plan<L>(c, N, 2 * K, A.dup);
+    if (L == 2 && plan.levels && plan.digit_end[1] > 9) {
+        // the u128 pass B takes at most 9 bits: level 1 of 9, the rest split over the later levels
+        const unsigned T = plan.digit_end[plan.levels];
+        MsdPlan q{};
+        q.levels = 1 + (T - 9 + MSD_DBITS - 1) / MSD_DBITS;
+        q.digit_end[1] = 9;
+        for (unsigned l = 2; l <= q.levels; ++l) q.digit_end[l] = 9 + (T - 9) * (l - 1) / (q.levels - 1);
+        plan = q;
+    }
     if (!plan.levels) return false;
     const unsigned b1 = plan.digit_end[1];
     const uint32_t nb1 = 1u << b1;
@@ -2025,8 +2129,13 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
             budget = 0.9 * ((double)fr + (double)c.ws.held());
         }
         const double u_est = std::min((double)N, (double)N / A.dup * 1.25);
-        const double per_u = 8.0 * 5 + 4.0 + (COUNTED ? 4.0 * 5 + 8.0 : 0.0);
-        const double per_key = COUNTED ? 24.0 : 16.0;
+        const double kb = (double)sizeof(K2);
+        // (u128: the rounds hold only the growing canonical set beside their buffers, which are released
+        // before the rc stage; reserving the later stages' 5 keys per distinct k-mer as well would plan
+        // ~10 rounds at configs[2] instead of 2)
+        const double per_u = L == 2 ? kb * 2 + 4.0 + (COUNTED ? 8.0 : 0.0)
+                                    : kb * 5 + 4.0 + (COUNTED ? 4.0 * 5 + 8.0 : 0.0);
+        const double per_key = 2 * kb + (COUNTED ? 8.0 : 0.0);
         const double avail = budget - per_u * u_est;
         R = avail > 0 ? (uint32_t)std::min<double>(std::ceil((double)N * per_key / avail), nb1) : nb1;
         R = std::max<uint32_t>(R, 2);
@@ -2039,10 +2148,11 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         for (uint64_t b = bb[r]; b < bb[r + 1]; ++b) nr[r] += h1[b];
         nmax = std::max(nmax, nr[r]);
     }
-    K2 *ka = (K2 *)c.ws.get(Workspace::KA, nmax * 8);
-    K2 *kb = (K2 *)c.ws.get(Workspace::KB, nmax * 8);
+    K2 *ka = (K2 *)c.ws.get(Workspace::KA, nmax * sizeof(K2));
+    K2 *kb = (K2 *)c.ws.get(Workspace::KB, nmax * sizeof(K2));
     uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nmax * 4) : nullptr;
     uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nmax * 4) : nullptr;
+    tr("rounds: buffers", R, nmax);
     if (c.debug)
         fprintf(stderr, "[mtg debug] canonical rounds: N=%lu dup=%.2f levels=%u digit1=%u rounds=%u largest=%lu\n",
                 (unsigned long)N, A.dup, plan.levels, b1, R, (unsigned long)nmax);
@@ -2059,15 +2169,17 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         const uint32_t *dh1 = nullptr;
         BucketSel sel;
         sel.add(bb[r], bb[r + 1]);
-        const uint64_t n = fused_pass_b<COUNTED>(c, K, canonical, cmax, in, A, b1, &sel, ka, ca, &dh1);
+        const uint64_t n = fused_pass_b<L, COUNTED>(c, K, canonical, cmax, in, A, b1, &sel, ka, ca, &dh1);
         if (n != nr[r]) throw std::runtime_error("a collect round's k-mers differ from its histogram");
+        tr("rounds: pass B", r, n);
         K2 *xa = ka, *xb = kb;
         uint32_t *xac = ca, *xbc = cb;
         c.track_partition = first;  // the roofline's partition pass: the first round's level 2
-        const uint64_t U = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n, 2 * K, cmax, A.dup, dh1, false,
+        const uint64_t U = msd_sort_unique<L, COUNTED>(c, &xa, &xb, &xac, &xbc, n, 2 * K, cmax, A.dup, dh1, false,
                                                        nullptr, true, nullptr, &plan);
         c.track_partition = false;
         first = false;
+        tr("rounds: sort", r, U);
         if (off + U > cap) {
             // first round: size the canonical set from its distinct ratio (+25 %); later growth keeps
             // what is already appended
@@ -2097,12 +2209,12 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     // bits (a one-pass build gets it from its own sort's groups)
     c.gidx = Ctx::GroupIndex{};
     if (canonical && off && !COUNTED) {
-        const MsdPlan rp = msd_plan<1>(c, off, 2 * K, 1.0);
+        const MsdPlan rp = msd_plan<L>(c, off, 2 * K, 1.0);
         const unsigned fb = rp.levels ? rp.digit_end[rp.levels] : 0;
         if (fb && fb <= 26) {
             const uint64_t nb = 1ull << fb;
             uint64_t *gi = (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8);
-            bucket_index<1>(c, *out, off, 2 * K - fb, nb, gi);
+            bucket_index<L>(c, *out, off, 2 * K - fb, nb, gi);
             HIP_CHECK(hipMemcpyAsync(gi + nb + 1, gi + nb, 8, hipMemcpyDeviceToDevice, c.stream));
             c.gidx = Ctx::GroupIndex{*out, off, fb, 2 * K, gi};
         }
@@ -2213,25 +2325,26 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
 // the dense-rank dummy sort (boss_kernels.hpp: dummy_rank): `ranks` (u64 view of one of the two
 // Draw-key buffers xa / xb) sorted + deduplicated, the distinct ranks decoded to lifted keys in
 // whichever buffer does not hold them (both hold Draw lifted keys); returns D, *dk = the keys
-template <int L3>
-static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3> *xb, Key<1> *ranks, uint64_t Draw,
+template <int L3, int LR = 1>
+static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3> *xb, Key<LR> *ranks, uint64_t Draw,
                                         Key<L3> **dk) {
-    Key<1> *ra = ranks, *rb = (void *)ranks == (void *)xa ? (Key<1> *)xb : (Key<1> *)xa;
+    static_assert(sizeof(Key<LR>) <= sizeof(Key<L3>), "the rank buffers are the lifted key buffers");
+    Key<LR> *ra = ranks, *rb = (void *)ranks == (void *)xa ? (Key<LR> *)xb : (Key<LR> *)xa;
     uint32_t *nv = nullptr;
-    const unsigned nbits = 64 - (unsigned)__builtin_clzll(dummy_rank_space(kb));
+    const unsigned nbits = dummy_rank_bits(kb);
     // (the real k-mers' MSD partition + LDS-hash unique on these ranks: dummy stage 4.4 -> 6.8 ms)
-    radix_sort<1, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
+    radix_sort<LR, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
     reset_small(c);
     const uint64_t ut = ceil_div(Draw, 2048);
     uint32_t udesc_ep;
     uint64_t *udesc = acquire_desc(c, ut, &udesc_ep);
-    unique_kernel<1, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
+    unique_kernel<LR, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
         ra, nullptr, Draw, rb, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total, &c.small->error);
     HIP_CHECK(hipGetLastError());
     const uint64_t D = read_u64(c, &c.small->total);
     Key<L3> *outk = (void *)rb == (void *)xa ? xb : xa;
-    dummy_decode_kernel<L3><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
-                              dim3(256), 0, c.stream>>>((const uint64_t *)rb, D, kb, outk);
+    dummy_decode_kernel<L3, LR><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
+                                  dim3(256), 0, c.stream>>>(rb, D, kb, outk);
     HIP_CHECK(hipGetLastError());
     *dk = outk;
     return D;
@@ -2250,15 +2363,22 @@ static uint64_t sort_unique_dummies(Ctx &c, unsigned K, Key<L3> *da, Key<L3> *db
     uint64_t D = 0;
     uint32_t *nv = nullptr;
     const unsigned kb = K - 1;
-    if (c.dummy_ranks && kb >= 1 && kb <= 30 && Draw) {
+    const int LR = dummy_rank_limbs(kb);
+    if (c.dummy_ranks && kb >= 1 && LR && (LR == 1 || L3 >= 2) && Draw) {
         HIP_CHECK(hipMemsetAsync(&c.small->bad_dummy, 0, 4, c.stream));
         const unsigned g = (unsigned)std::min<uint64_t>(ceil_div(Draw, 256), 16384);
-        dummy_encode_kernel<L3><<<dim3(g), dim3(256), 0, c.stream>>>(da, Draw, kb, (uint64_t *)db, &c.small->bad_dummy);
+        if (LR == 1)
+            dummy_encode_kernel<L3, 1><<<dim3(g), dim3(256), 0, c.stream>>>(da, Draw, kb, (Key<1> *)db, &c.small->bad_dummy);
+        else
+            dummy_encode_kernel<L3, 2><<<dim3(g), dim3(256), 0, c.stream>>>(da, Draw, kb, (Key<2> *)db, &c.small->bad_dummy);
         HIP_CHECK(hipGetLastError());
         uint32_t bad = 0;
         HIP_CHECK(hipMemcpyAsync(&bad, &c.small->bad_dummy, 4, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
-        if (!bad) return sort_unique_dummy_ranks<L3>(c, kb, da, db, (Key<1> *)db, Draw, dk);
+        if (!bad) {
+            if (LR == 1) return sort_unique_dummy_ranks<L3, 1>(c, kb, da, db, (Key<1> *)db, Draw, dk);
+            if constexpr (L3 >= 2) return sort_unique_dummy_ranks<L3, 2>(c, kb, da, db, (Key<2> *)db, Draw, dk);
+        }
         if (c.debug) fprintf(stderr, "[mtg debug] dummy keys outside the rank shape: lifted sort\n");
     }
     {
@@ -2370,6 +2490,14 @@ static uint64_t stage_dummies_local(Ctx &c, unsigned K, const Key<L2> *ka, uint6
                                                                                                   R, K, toff, da);
             HIP_CHECK(hipGetLastError());
             return sort_unique_dummy_ranks<L3>(c, k, da, db, (Key<1> *)da, Draw, dk);
+        }
+    }
+    if constexpr (L2 <= 2 && L3 >= 2) {
+        if (c.dummy_ranks && dummy_rank_limbs(k) == 2) {  // 30 < k <= 62: dense u128 ranks (configs[2]: k = 62)
+            dummy_write_kernel<L2, L3, true, 2><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(ka, flags, in_flag,
+                                                                                                     R, K, toff, da);
+            HIP_CHECK(hipGetLastError());
+            return sort_unique_dummy_ranks<L3, 2>(c, k, da, db, (Key<2> *)da, Draw, dk);
         }
     }
     dummy_write_kernel<L2, L3><<<dim3((unsigned)wtiles), dim3(256), 0, c.stream>>>(ka, flags, in_flag, R, K,
@@ -2525,6 +2653,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     HIP_CHECK(hipMemsetAsync(c.small, 0, sizeof(Small), c.stream));
     EventTimer tm(c.stream);
     const int ev_start = tm.mark();
+    Tracer tr{c, 0};
 
     // ---- K1 extract (fused with K2's first partition level when it applies)
     K2 *ka, *kb;
@@ -2546,8 +2675,8 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     bool rounds = false;  // the canonical set collected in rounds of the fused K1 (collect_rounds_fused)
     if (P > 1) {
         ev_extract = tm.mark();
-        if constexpr (L2 == 1) {
-            rounds = collect_rounds_fused<COUNTED>(c, K, canonical, cmax, in, &ka, &ca, &U);
+        if constexpr (L2 <= 2) {
+            rounds = collect_rounds_fused<L2, COUNTED>(c, K, canonical, cmax, in, &ka, &ca, &U);
             if (rounds) {
                 R = U;
                 kb = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(U, 1) * sizeof(K2));
@@ -2605,9 +2734,19 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         }
         ka = real;
         ca = realc;
+        if (rounds) {
+            // the canonical set and the rc sort's buffers are merged into REAL: give them back before the
+            // dummy stage (configs[2]: 41 + 2 x 32 GB of u128 keys; with them held, the emit's last array
+            // did not fit the 288 GB), and the dummy buffers take them from the workspace's kept blocks
+            for (auto sl : {Workspace::CANON, Workspace::CANONC, Workspace::KB, Workspace::CB, Workspace::RC_ALT,
+                            Workspace::RC_ALTC, Workspace::SPEC_A, Workspace::SPEC_B, Workspace::SPEC_AC,
+                            Workspace::SPEC_BC})
+                c.ws.release(sl);
+        }
     }
     ensure_compact(c);  // (a no-op unless the canonical set is still in buckets)
     T.n_real = R;
+    tr("collect + rc", U, R);
     debug_check_sorted(c, "real k-mers", ka, R);
     const int ev_rc = tm.mark();
 
@@ -2615,6 +2754,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     Key<L3> *dk = nullptr;
     const uint64_t D = stage_dummies_local<L2, L3>(c, K, ka, R, &dk);
     T.n_dummy = D + 1;
+    tr("dummies", D);
     debug_check_sorted(c, "dummy k-mers", dk, D);
     const int ev_dummy = tm.mark();
 
@@ -2622,6 +2762,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
     int ev_merge;
     stage_merge_emit<L2, L3, COUNTED>(c, tm, &ev_merge, k, bits, ka, ca, R, dk, D, true, out);
     const int ev_emit = tm.mark();
+    tr("emit", out->n);
     check_error_word(c);
     HIP_CHECK(hipStreamSynchronize(c.stream));
 
@@ -2687,21 +2828,6 @@ __global__ void gather_strided_kernel(const uint64_t *__restrict__ src, uint64_t
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j < cnt) dst[j] = src[(uint64_t)j * stride];
 }
-
-// MTG_TRACE: host wall time since the previous trace point (stream drained first)
-struct Tracer {
-    Ctx &c;
-    int rank;
-    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    void operator()(const char *what, uint64_t a = 0, uint64_t b = 0) {
-        if (!c.trace) return;
-        HIP_CHECK(hipStreamSynchronize(c.stream));
-        const auto now = std::chrono::steady_clock::now();
-        fprintf(stderr, "[mtg trace r%d] %-22s %9.3f ms  %lu %lu\n", rank, what,
-                std::chrono::duration<double, std::milli>(now - t).count(), (unsigned long)a, (unsigned long)b);
-        t = now;
-    }
-};
 
 struct Dist {
     Comm &comm;
@@ -3084,7 +3210,8 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     const uint64_t tiles = ceil_div(npos, TILE);
     const int fbk = 512;
     const uint32_t rps = (uint32_t)(16 * fbk / TILE);
-    uint32_t nrows = (uint32_t)std::min<uint64_t>(tiles, c.hist_rows);
+    // (stripe_cursor_kernel takes at most 1024 stripes: 2048 rows at rps = 2, 1024 at rps = 1)
+    uint32_t nrows = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(tiles, c.hist_rows), 1024ull * rps);
     if (nrows >= rps) nrows -= nrows % rps;
     constexpr uint32_t NBH = 1u << FUSED_HB;
     // pass A: per-row histograms of the canonical keys' top 12 bits (and of the other strand's)
@@ -3251,7 +3378,7 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
             } else {
                 if (B1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
                 const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
-                extract_partition_kernel<COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+                extract_partition_kernel<1, COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
                     in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
                     B1, per_stripe, scur, send, ka, ca, &c.small->error, dsel);
             }

@@ -146,6 +146,13 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// popcount of the bits of m below this lane: v_mbcnt_lo + v_mbcnt_hi, two VALU (popcll(m & lanemask_lt())
+// built the mask with a runtime 64-bit shift and selects every time: ~8 VALU per call, per key in the
+// local passes' list positions)
+__device__ __forceinline__ uint32_t popc_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // inclusive wave scan (sum) of 32-bit values
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
     const uint32_t lane = __lane_id();

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(RT_BLOCK) void route_write_kernel(
             uint32_t b = 0;
             if (__lane_id() == leader) b = atomicAdd(&s_c[lo], (uint32_t)__popcll(same));
             b = __shfl(b, leader, 64);
-            if (valid && o == lo) pos = b + (uint32_t)__popcll(same & lanemask_lt());
+            if (valid && o == lo) pos = b + popc_below(same);
             active &= ~same;
         }
         if (valid) {
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(RT_BLOCK) void sink_write_kernel(const Key<L2> *__r
             b = atomicAdd(&s_c, (uint32_t)__popcll(m));
         b = __shfl(b, (uint32_t)(__ffsll((unsigned long long)(m ? m : 1)) - 1), 64);
         if (miss) {
-            const uint32_t pos = b + (uint32_t)__popcll(m & lanemask_lt());
+            const uint32_t pos = b + popc_below(m);
             out[base + pos] = lift_fast<L3>(q[i], K) & ~Key<L3>::from(7);
         }
     }

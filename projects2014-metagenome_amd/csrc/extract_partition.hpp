@@ -182,28 +182,98 @@ __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *_
     }
 }
 
+// A for windows of up to 64 chars (u128 keys; BASELINE configs[2]: K = 63): the same histogram of the
+// canonical keys' top 12 bits as extract_hist_fast_kernel, from five packed words per thread (a thread's
+// 16 windows span 15 + K <= 79 chars); the forward top of window j is chars j + K - 7 .. j + K - 2, a
+// 12-bit field of a funnel-shifted pair of words, validity the K-bit field of the 80-bit invalid mask.
+// KC: K as a compile-time constant (0: the runtime K_).
+template <int KC = 0>
+__global__ __launch_bounds__(256) void extract_hist_wide_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
+                                                                unsigned K_, int canonical, uint64_t ntiles,
+                                                                uint64_t per_row, uint32_t *__restrict__ rows,
+                                                                uint32_t tstride = 1) {
+    const unsigned K = KC ? (unsigned)KC : K_;
+    constexpr int BLOCK = 256, PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 5;
+    constexpr uint32_t NB = 1u << FUSED_HB;
+    __shared__ uint32_t s_pack[NW];
+    __shared__ uint32_t s_inv[NW];
+    __shared__ uint32_t s_h[NB];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < NB; i += BLOCK) s_h[i] = 0;
+    const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
+    const uint64_t maskK = K >= 64 ? ~0ull : (1ull << K) - 1;
+    const unsigned fs = 2 * (K - 7);  // bit offset of window 0's forward top in the thread's span
+    const unsigned qs = fs >> 5, bs = fs & 31;
+    const uint64_t t0 = (uint64_t)blockIdx.x * per_row, t1 = min(ntiles, t0 + per_row);
+    for (uint64_t tile = t0; tile < t1; tile += tstride) {
+        const uint64_t base = tile * TILE;
+        __syncthreads();  // the previous tile's words are read
+        for (uint32_t w = tid; w < (uint32_t)NW; w += BLOCK) {
+            uint32_t a, b;
+            pack_word(seq, seq_len, base + 16ull * w, a, b);
+            s_pack[w] = a;
+            s_inv[w] = b;
+        }
+        __syncthreads();
+        const uint64_t p0 = base + 16ull * tid;
+        if (p0 >= npos) continue;
+        const uint32_t nwin = (uint32_t)min<uint64_t>(PPT, npos - p0);
+        uint32_t w[6];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) w[q] = s_pack[tid + q];
+        w[5] = 0;
+        const u128 inv = (u128)s_inv[tid] | ((u128)s_inv[tid + 1] << 16) | ((u128)s_inv[tid + 2] << 32) |
+                         ((u128)s_inv[tid + 3] << 48) | ((u128)s_inv[tid + 4] << 64);
+        // the words at qs, qs + 1, qs + 2 (a select chain: no dynamic register indexing)
+        uint32_t x0 = w[0], x1 = w[1], x2 = w[2];
+#pragma unroll
+        for (unsigned q = 1; q < 4; ++q)
+            if (qs == q) x0 = w[q], x1 = w[q + 1], x2 = w[q + 2];
+        const uint32_t flo = bs ? __builtin_amdgcn_alignbit(x1, x0, bs) : x0;
+        const uint32_t fhi = bs ? __builtin_amdgcn_alignbit(x2, x1, bs) : x1;
+        const uint32_t q1 = rc_word(w[1]), q2 = rc_word(w[0]);
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const uint32_t f = (j ? __builtin_amdgcn_alignbit(fhi, flo, 2 * j) : flo) & (NB - 1);
+            const int sr = 2 * (41 - j);  // 52 .. 82
+            const uint32_t r = (sr >= 64 ? (q2 >> (sr - 64)) : __builtin_amdgcn_alignbit(q2, q1, sr - 32)) & (NB - 1);
+            const bool ok = (uint32_t)j < nwin && ((uint64_t)(inv >> j) & maskK) == 0;
+            if (ok) atomicAdd(&s_h[take_rc_top(canonical, f, r) ? r : f], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < NB; i += BLOCK) rows[(uint64_t)blockIdx.x * NB + i] = s_h[i];
+}
+
 template <bool COUNTED, int BLOCK_ = COUNTED ? 512 : 1024>
 struct FusedTraits {
     static constexpr int BLOCK = BLOCK_;  // the LDS tile: BLOCK * PPT keys (16 K at 1024 threads)
     static constexpr int PPT = ExtractTraits<1>::PPT;
     static constexpr int TILE = BLOCK * PPT;
 };
+// pass B's workgroup for L-limb keys: 512 threads (8 K windows) for u64, 256 (4 K windows, 64 KB of
+// u128 keys in LDS) for u128
+template <int L>
+constexpr int fused_block() { return L == 1 ? 512 : 256; }
 
 // B: extract one tile, order its k-mers by the top b bits in LDS, write one run per bucket at
-// cursor[bucket] (the bucket starts of pass A's histogram)
-template <bool COUNTED, int BLOCK_>
+// cursor[bucket] (the bucket starts of pass A's histogram).  L-limb keys (u128: BASELINE configs[2]'s
+// k = 63 rounds); KC: the window length as a compile-time constant (0: the runtime K)
+template <int L, bool COUNTED, int BLOCK_, int KC = 0>
 __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
-    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K, int canonical,
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical,
     const uint64_t *__restrict__ read_starts, const uint32_t *__restrict__ read_counts, uint64_t n_reads,
     const uint64_t *__restrict__ rid_at, uint32_t cmax, unsigned b, uint64_t per_stripe, unsigned long long *__restrict__ cursor,
-    const unsigned long long *__restrict__ bend, Key<1> *__restrict__ kout, uint32_t *__restrict__ vout,
+    const unsigned long long *__restrict__ bend, Key<L> *__restrict__ kout, uint32_t *__restrict__ vout,
     uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
+    const unsigned K = KC ? (unsigned)KC : K_;
     using F = FusedTraits<COUNTED, BLOCK_>;
     constexpr int BLOCK = F::BLOCK, PPT = F::PPT, TILE = F::TILE;
     constexpr int NBMAX = 512;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
-    __shared__ __align__(16) uint8_t s_code[TILE + ExtractTraits<1>::MAXK];
-    __shared__ Key<1> s_keys[TILE];
+    static_assert(ExtractTraits<L>::PPT == PPT, "16 windows per thread");
+    __shared__ __align__(16) uint8_t s_code[TILE + ExtractTraits<L>::MAXK];
+    __shared__ Key<L> s_keys[TILE];
     __shared__ uint32_t s_vals[COUNTED ? TILE : 1];
     __shared__ uint32_t s_cnt[NBMAX];  // bucket counts, then the buckets' offsets in the tile
     __shared__ unsigned long long s_gbase[NBMAX];
@@ -222,9 +292,9 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     const uint64_t span_end = min(seq_len, base + TILE + K - 1);
     stage_codes<BLOCK>(seq, base, span_end, s_code, tid);
     __syncthreads();
-    Key<1> kk[PPT];
+    Key<L> kk[PPT];
     uint32_t cc[PPT];
-    uint32_t m = slide_windows<1, COUNTED, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos, K,
+    uint32_t m = slide_windows<L, COUNTED, PPT, true>(s_code, tid * PPT, base + (uint64_t)tid * PPT, npos, K,
                                                       canonical, read_starts, read_counts, n_reads, rid_at, cmax, kk, cc);
     if (sel) {  // one round of a batched collect: only the level-1 buckets of its mask
 #pragma unroll
@@ -275,7 +345,7 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     }
     __syncthreads();
     for (uint32_t p = tid; p < total; p += BLOCK) {
-        const Key<1> key = s_keys[p];
+        const Key<L> key = s_keys[p];
         const uint32_t lb = key_prefix(key, 2 * K, b);
         if (s_gbase[lb] == ~0ull) continue;
         const uint64_t o = s_gbase[lb] + (p - s_cnt[lb]);

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(512) void onesweep_kernel(
         }
     }
 
-    const uint64_t lt = lanemask_lt();
+
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const bool valid = wbase + (uint64_t)j * 64 + lane < n;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(512) void onesweep_kernel(
             s_whist[wid * 256 + d] = old + (uint32_t)__popcll(peers);
         }
         old = __shfl(old, (int)leader, 64);
-        rank[j] = old + (uint32_t)__popcll(peers & lt);
+        rank[j] = old + popc_below(peers);
     }
     __syncthreads();
 

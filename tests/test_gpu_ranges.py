@@ -100,11 +100,14 @@ def test_ranges_empty_and_tiny(monkeypatch):
         _check(k, ["N" * 100, "$" * 50, "."], False, 8)
 
 
-def test_config2_default_planner_many_ranges():
+def test_config2_default_planner_many_ranges(monkeypatch):
     # configs[2]'s shape (k = 63, u128 keys, genome-sampled 150 bp reads) at 2 M reads, with a
-    # memory budget that makes the DEFAULT planner (no MTG_RANGES) cut the collection into >= 8 key
-    # ranges, the way the 100 M-read configs[2] build runs within HBM; bit for bit vs the oracle
+    # memory budget that makes the DEFAULT range planner (no MTG_RANGES) cut the collection into >= 8
+    # key ranges; bit for bit vs the oracle.  (The default collect of such a build is the canonical
+    # rounds of the fused extraction since round 5 -- test_gpu_rounds.py; MTG_COLLECT=ranges keeps
+    # this path, which the disk container and the multi-GPU u128 build still take.)
     import bench
+    monkeypatch.setenv("MTG_COLLECT", "ranges")
     asc = bench.make_reads_host_codes(2_000_000, 150, 4321, "genome", 10.0)
     data = asc.reshape(-1)
     off = np.arange(len(asc) + 1, dtype=np.uint64) * asc.shape[1]

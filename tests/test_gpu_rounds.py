@@ -158,3 +158,61 @@ def test_rounds_20m_reads_memory_planned_vs_oracle():
     assert len(W) == len(want.W)
     assert np.array_equal(W, want.W) and np.array_equal(last, want.last)
     assert np.array_equal(F, want.F) and n_real == want.n_real
+
+
+# u128 windows (BOSS k 32..63, K = 33..64: BASELINE configs[2]'s k = 63 is BOSS k = 62): the wide pass A
+# (extract_hist_wide_kernel), the generic pass B on u128 keys and the exact later MSD levels in every
+# round, then the one-pass rc / dummy (dense u128 ranks) / emit stages; k = 62 takes the kernels with
+# K = 63 compiled in, the others the runtime K
+@pytest.mark.parametrize("rounds", [2, 5])
+@pytest.mark.parametrize("k", [32, 33, 47, 62, 63])
+def test_rounds_u128_random_reads(small_fused, rounds, k):
+    small_fused.setenv("MTG_RANGES", str(rounds))
+    reads = _random_reads(3000 + k, 300, 150, 6000, n_rate=0.005, lower=True)
+    for canonical in (False, True):
+        for bits in (0, 16):
+            _, t = _check(k, reads, canonical, bits)
+            assert t.collect_mode == ROUNDS and t.n_batches == rounds, (t.collect_mode, t.n_batches)
+
+
+def test_rounds_u128_counts_saturate(small_fused):
+    small_fused.setenv("MTG_RANGES", "3")
+    rng = np.random.default_rng(41)
+    seqs = _random_reads(43, 300, 100, 3000)
+    counts = rng.integers(1, 400, size=len(seqs)).tolist()
+    for bits in (4, 8, 32):
+        for canonical in (False, True):
+            _, t = _check(40, seqs, canonical, bits, counts)
+            assert t.collect_mode == ROUNDS
+
+
+# configs[2]'s shape (k = 63, u128) at a size the oracle finishes: 10 M genome-sampled reads under a
+# memory_preallocated budget that the DEFAULT planner answers with u128 rounds (no MTG_RANGES), bit for
+# bit against the oracle
+@pytest.mark.timeout(1200)
+def test_rounds_u128_10m_reads_memory_planned_vs_oracle():
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    n_reads, L = 10_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    ctor = boss.IBOSSChunkConstructor.initialize(62, both_strands=True, memory_preallocated=3.0e10)
+    dc = ctor.build_device(seq.data_ptr(), seq.numel())
+    t = ctor.timings()
+    assert t.collect_mode == ROUNDS and t.n_batches >= 2, (t.collect_mode, t.n_batches)
+    assert t.n_extracted == n_reads * (L - 63 + 1)
+    L_ = boss.lib()
+    W = np.empty(dc.n, dtype=np.uint8)
+    last = np.empty(dc.n, dtype=np.uint8)
+    assert L_.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n) == 0
+    assert L_.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n) == 0
+    F = np.array([int(f) for f in dc.F], dtype=np.uint64)
+    n_real = dc.n_real
+    del ctor
+    host = seq.cpu().numpy()
+    del seq
+    want = O.build_chunk_packed(62, host, np.arange(n_reads + 1, dtype=np.uint64) * (L + 1), canonical=True)
+    assert len(W) == len(want.W)
+    assert np.array_equal(W, want.W) and np.array_equal(last, want.last)
+    assert np.array_equal(F, want.F) and n_real == want.n_real

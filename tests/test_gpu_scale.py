@@ -271,10 +271,15 @@ def test_full_bench_size_vs_oracle(canonical, bits):
         assert np.array_equal(wt, want.weights)
 
 
-# configs[2]'s bounded-memory planner without overrides: a budget for which plan_ranges itself
-# picks 8 key ranges (k = 63, u128 keys, 4 M reads), bit for bit against the oracle
+# configs[2]'s bounded-memory planner without overrides (k = 63, u128 keys, 4 M reads, a 12 GB budget):
+# the default collect is the canonical rounds of the fused extraction (collect_mode 2); with
+# MTG_COLLECT=ranges the key-range collect, for which plan_ranges itself picks >= 8 ranges.  Both bit
+# for bit against the oracle
 @pytest.mark.timeout(900)
-def test_cfg3_planner_default_ranges_vs_oracle():
+@pytest.mark.parametrize("collect", ["rounds", "ranges"])
+def test_cfg3_planner_default_ranges_vs_oracle(monkeypatch, collect):
+    if collect == "ranges":
+        monkeypatch.setenv("MTG_COLLECT", "ranges")
     asc = bench.make_reads_host_codes(4_000_000, 150, 777, "genome", 10.0)
     ctor = boss.IBOSSChunkConstructor.initialize(62, both_strands=True, bits_per_count=0,
                                                  num_threads=8, memory_preallocated=1.2e10)
@@ -282,9 +287,12 @@ def test_cfg3_planner_default_ranges_vs_oracle():
     ctor.add_packed(data, off)
     got = ctor.build_chunk()
     t = ctor.timings()
-    assert t.n_batches >= 8, t.n_batches
+    if collect == "ranges":
+        assert t.collect_mode == 1 and t.n_batches >= 8, (t.collect_mode, t.n_batches)
+    else:
+        assert t.collect_mode == 2 and t.n_batches >= 2, (t.collect_mode, t.n_batches)
     want = O.build_chunk_packed(62, data, off, canonical=True)
-    _assert_same(got, want, "cfg3 planner, %d ranges" % t.n_batches)
+    _assert_same(got, want, "cfg3 planner, %s, %d batches" % (collect, t.n_batches))
 
 
 # configs[3]: one full 125 M-read share (1.5e10 windows) through the multi-GPU build on a
