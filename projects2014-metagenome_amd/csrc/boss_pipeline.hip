@@ -320,6 +320,7 @@ struct Ctx {
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
     bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
     bool lu_lean = false;          // MTG_LU_LEAN=1: the speculative level's local pass as local_unique_lean_kernel
+    bool fast2 = true;             // MTG_FAST2=0: the u128 rounds' pass B as the generic extract_partition_kernel
     uint32_t merge_it = 1;         // MTG_MERGE_IT: local_merge_kernel's least outputs per thread (A/B)
     bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
     bool kmc_mirror = true;  // add_kmc copies the first database to the device while reading it
@@ -412,6 +413,7 @@ static void load_knobs(Ctx &c) {
     c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
     c.lu_fast = !is("MTG_LU_FAST", "0");
     c.lu_lean = is("MTG_LU_LEAN", "1");
+    c.fast2 = !is("MTG_FAST2", "0");
     if (const char *e = getenv("MTG_MERGE_IT")) c.merge_it = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
     c.spec_final = !is("MTG_SPEC", "0");
@@ -1724,11 +1726,21 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     tm.mark();
     const bool fast_b = L == 1 && !COUNTED && K <= 32;
     if constexpr (L == 2) {
-        // u128 windows (K <= 64): the generic pass B on 256-thread tiles (A was made for them)
+        // u128 windows (K <= 64): pass B on 256-thread tiles (A was made for them); uncounted canonical /
+        // basic builds take the packed-word kernel (MTG_FAST2=0: the generic one)
         constexpr int B = fused_block<2>();
         if (b1 > 9) throw std::runtime_error("the u128 pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, B>::TILE);
-        if (K == 63 && c.kspec)
+        if (!COUNTED && c.fast2 && K > 32 && K <= 64) {
+            if (K == 63 && c.kspec)
+                extract_partition_fast2_kernel<B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
+                    in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
+                    (const uint32_t *)dsel);
+            else
+                extract_partition_fast2_kernel<B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
+                    in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
+                    (const uint32_t *)dsel);
+        } else if (K == 63 && c.kspec)
             extract_partition_kernel<2, COUNTED, B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
                 in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
                 A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);

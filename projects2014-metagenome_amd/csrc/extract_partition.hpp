@@ -508,6 +508,153 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     }
 }
 
+// Pass B for u128 windows (33 <= K <= 64, BASELINE configs[2]'s k = 63), VALU-lean like the u64 kernel
+// above: the tile is packed once (16 chars a word + an invalid mask), a thread's 16 windows span five
+// words, and window j's forward plain word is four funnel shifts of them (v_alignbit by 2j); the rc word
+// slides one char a window (two 64-bit halves); the BOSS rotation drops the top char with a shift and
+// puts it in the label; validity is the K-bit field of the 80-bit invalid mask.  Same k-mers as
+// slide_windows<2> (forward and rc plain words, plain_to_boss, rc < fwd picks rc), so the same output as
+// extract_partition_kernel<2>.  canonical: 0 / 1 only (the routed u128 collect is not fused).
+template <int BLOCK, int KC = 0>
+__global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical, unsigned b,
+    uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
+    Key<2> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
+    const unsigned K = KC ? (unsigned)KC : K_;
+    constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 5;  // +5 words: a thread's windows reach 15 + 63 chars on
+    constexpr int NBMAX = 512;
+    constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
+    static_assert(TILE <= 65536, "u16 in-tile offsets");
+    __shared__ uint32_t s_pack[NW];
+    __shared__ uint32_t s_inv[NW];
+    __shared__ ulonglong2 s_keys[TILE];
+    __shared__ unsigned long long s_gbase[NBMAX];  // the run bases; first the u32 bucket counts (s_cnt)
+    __shared__ uint16_t s_off[NBMAX];
+    __shared__ uint32_t s_scan[BLOCK / 64 + 1];
+    __shared__ uint32_t s_sel[FUSED_SEL_WORDS];
+    uint32_t *s_cnt = reinterpret_cast<uint32_t *>(s_gbase);
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nb = 1u << b;
+    const uint64_t npos = seq_len >= K ? seq_len - K + 1 : 0;
+    const uint64_t tile = xcd_tile((npos + TILE - 1) / TILE);
+    if (tile * TILE >= npos) return;
+    for (uint32_t i = tid; i < nb; i += BLOCK) s_cnt[i] = 0;
+    if (sel && tid < FUSED_SEL_WORDS) s_sel[tid] = sel[tid];
+    const uint64_t base = tile * TILE;
+    for (uint32_t w = tid; w < (uint32_t)NW; w += BLOCK) {
+        uint32_t pk, iv;
+        pack_word(seq, seq_len, base + 16ull * w, pk, iv);
+        s_pack[w] = pk;
+        s_inv[w] = iv;
+    }
+    __syncthreads();
+
+    uint32_t w[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) w[q] = s_pack[tid + q];
+    const uint64_t invlo = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) | ((uint64_t)s_inv[tid + 2] << 32) |
+                           ((uint64_t)s_inv[tid + 3] << 48);
+    const uint64_t invhi = s_inv[tid + 4];
+    const uint64_t p0 = base + 16ull * tid;
+    const uint32_t nwin = p0 < npos ? (uint32_t)min<uint64_t>(PPT, npos - p0) : 0u;
+    const uint64_t maskK = K >= 64 ? ~0ull : (1ull << K) - 1;
+    const unsigned hb = 2 * K - 64;                                   // bits of the high half (2 .. 64)
+    const uint64_t mhi = hb >= 64 ? ~0ull : (1ull << hb) - 1;
+    // E: the chars entering windows 1..16 (char K + j - 1 for window j), 2 bits each
+    uint32_t E;
+    {
+        const unsigned qe = K >> 4, se = 2 * (K & 15);
+        uint32_t a = w[2], c2 = w[3];
+        if (qe == 3) a = w[3], c2 = w[4];
+        if (qe == 4) a = w[4], c2 = 0;
+        E = se ? __builtin_amdgcn_alignbit(c2, a, se) : a;
+    }
+    // R: the rc plain word of window 0 = the reversed, complemented chars of P0, shifted down to 2K bits
+    uint64_t rlo, rhi;
+    {
+        const uint64_t plo = (uint64_t)w[0] | ((uint64_t)w[1] << 32), phi = ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) & mhi;
+        const uint64_t xl = reverse_pairs64(~phi), xh = reverse_pairs64(~plo);  // (~P) reversed, 128 bits
+        const unsigned sh = 128 - 2 * K;                                         // 0 .. 62
+        rlo = sh ? (xl >> sh) | (xh << (64 - sh)) : xl;
+        rhi = (sh ? xh >> sh : xh) & mhi;
+    }
+    const unsigned tsh = 2 * K - 66;  // the top char's bit in the high half
+    const unsigned bs = 2 * K - b;    // the level-1 digit: key bits [bs, 2K)
+    ulonglong2 kk[PPT];
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+        const uint32_t d0 = j ? __builtin_amdgcn_alignbit(w[1], w[0], 2 * j) : w[0];
+        const uint32_t d1 = j ? __builtin_amdgcn_alignbit(w[2], w[1], 2 * j) : w[1];
+        const uint32_t d2 = j ? __builtin_amdgcn_alignbit(w[3], w[2], 2 * j) : w[2];
+        const uint32_t d3 = j ? __builtin_amdgcn_alignbit(w[4], w[3], 2 * j) : w[3];
+        const uint64_t plo = (uint64_t)d0 | ((uint64_t)d1 << 32), phi = ((uint64_t)d2 | ((uint64_t)d3 << 32)) & mhi;
+        if (j) {
+            rhi = ((rhi << 2) | (rlo >> 62)) & mhi;
+            rlo = (rlo << 2) | (3u - ((E >> (2 * (j - 1))) & 3u));
+        }
+        // plain -> BOSS: the 2K-bit word shifted up one char (its top char falls off) with that char as the label
+        const uint64_t flo = (plo << 2) | ((phi >> tsh) & 3u), fhi = ((phi << 2) | (plo >> 62)) & mhi;
+        const uint64_t qlo = (rlo << 2) | ((rhi >> tsh) & 3u), qhi = ((rhi << 2) | (rlo >> 62)) & mhi;
+        const bool rc = canonical && (qhi < fhi || (qhi == fhi && qlo < flo));
+        kk[j] = rc ? make_ulonglong2(qlo, qhi) : make_ulonglong2(flo, fhi);
+        const uint64_t iw = j ? (invlo >> j) | (invhi << (64 - j)) : invlo;
+        m |= (uint32_t)((uint32_t)j < nwin && (iw & maskK) == 0) << j;
+    }
+    auto digit = [&](const ulonglong2 &x) -> uint32_t {
+        return (uint32_t)(bs >= 64 ? x.y >> (bs - 64) : (x.x >> bs) | (x.y << (64 - bs)));
+    };
+    if (sel) {  // one round of a batched collect: only the level-1 buckets of its mask
+#pragma unroll
+        for (int j = 0; j < PPT; ++j) {
+            const uint32_t pb = digit(kk[j]);
+            if (!((s_sel[pb >> 5] >> (pb & 31)) & 1u)) m &= ~(1u << j);
+        }
+    }
+    uint32_t r[PPT];
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) r[j] = (m & (1u << j)) ? atomicAdd(&s_cnt[digit(kk[j])], 1u) : 0u;
+    __syncthreads();
+    uint32_t c[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        c[q] = i < nb ? s_cnt[i] : 0;
+        sum += c[q];
+    }
+    uint32_t total;
+    uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+    __syncthreads();  // every count is read before the run bases overwrite them
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nb) {
+            s_off[i] = (uint16_t)off;
+            const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
+            unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
+            if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
+                atomicOr(error, 2u);            // write past its range
+                g = ~0ull;
+            }
+            s_gbase[i] = g;
+        }
+        off += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+        if (m & (1u << j)) s_keys[s_off[digit(kk[j])] + r[j]] = kk[j];
+    __syncthreads();
+    for (uint32_t p = tid; p < total; p += BLOCK) {
+        const ulonglong2 key = s_keys[p];
+        const uint32_t lb = digit(key);
+        if (s_gbase[lb] == ~0ull) continue;
+        *reinterpret_cast<ulonglong2 *>(&kout[s_gbase[lb] + (p - s_off[lb])]) = key;
+    }
+}
+
 // Pass B's write cursors, one set per stripe.  All tiles scatter into the same 2^b level-1
 // buckets, so one cursor per bucket would take every tile's atomic (146 k tiles x 512 buckets at
 // the bench size, all on 512 words).  A pass-B tile is rps pass-A tiles; stripe s is the pass-B

@@ -175,6 +175,18 @@ def test_rounds_u128_random_reads(small_fused, rounds, k):
             assert t.collect_mode == ROUNDS and t.n_batches == rounds, (t.collect_mode, t.n_batches)
 
 
+@pytest.mark.parametrize("k", [32, 47, 62, 63])
+def test_rounds_u128_generic_pass_b(small_fused, k):
+    # MTG_FAST2=0: the uncounted u128 rounds' pass B as the generic extract_partition_kernel<2> (slide_windows)
+    # instead of the packed-word extract_partition_fast2_kernel; the same chunk
+    small_fused.setenv("MTG_RANGES", "3")
+    small_fused.setenv("MTG_FAST2", "0")
+    reads = _random_reads(5000 + k, 300, 150, 6000, n_rate=0.005, lower=True)
+    for canonical in (False, True):
+        _, t = _check(k, reads, canonical, 0)
+        assert t.collect_mode == ROUNDS and t.n_batches == 3
+
+
 def test_rounds_u128_counts_saturate(small_fused):
     small_fused.setenv("MTG_RANGES", "3")
     rng = np.random.default_rng(41)
