@@ -680,6 +680,15 @@ def main():
             result["kmc_path"] = kmc_path(args, kb, boss, kmc_base, args.host_steps, kmers_per_rank)
         else:
             result["host_path"] = host_path(args, kb, boss, seq, args.host_steps)
+            hp = result["host_path"]
+            # SURVEY.md section 8(d)(i) as its own field: extract-start -> BOSS::Chunk arrays on the host,
+            # through the reference's interface (add_packed + build_chunk); `value` stays the device-resident rate
+            result["hot_path_host_arrays"] = {
+                "value": hp["value"], "unit": "k-mers/s", "ms_per_step": hp["ms_per_step"],
+                "device_path_ms": hp["stages_ms"]["device_path"],
+                "host_legs_ms": hp["ms_per_step"] - hp["stages_ms"]["device_path"],
+                "what": "SURVEY.md 8(d)(i): extract-start -> Chunk arrays (W, last, F, weights) on the host, the "
+                        "same reads through add_packed + build_chunk (host_path)"}
         if args.fasta_reads > 0:
             result["fasta_path"] = fasta_path(args, kb, boss, args.host_steps, args.fasta_reads)
     if rank == 0 and not args.no_cpu_baseline:

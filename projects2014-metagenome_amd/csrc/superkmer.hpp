@@ -22,6 +22,7 @@
 
 #include "boss_kernels.hpp"
 #include "device_common.hpp"
+#include "extract_partition.hpp"
 
 namespace mtg {
 
@@ -158,8 +159,11 @@ __global__ __launch_bounds__(SK_BLOCK) void sk_owner_kernel(const uint8_t *__res
  * the scanned offsets (toff: runs, toffw: words, both owner-major) plus an LDS cursor (order inside a
  * tile's share is free: the owner sorts).
  * A run starts where the owner changes and at every multiple of SK_RUN_MAX windows, so no run
- * leaves its tile (SK_TILE is a multiple): the tile's owners and chars are staged in LDS (padded
- * like sk_owner_kernel's) and every scan and pack reads them there.
+ * leaves its tile (SK_TILE is a multiple).  Round 5: the tile's run boundaries are a bitmap in LDS
+ * (one 16-bit field per thread), so a run's end is the next set bit (at most 16 fields on); and its
+ * chars are a 2-bit image of the tile in LDS (16 chars a word), so each output word is three LDS reads
+ * and two funnel shifts instead of 28 byte reads and shifts (the char-by-char pack was 5.9 ms of an
+ * 8-rank build's 2.5 M-read rank, twice the routed collect's compute).
  */
 static_assert(SK_TILE % SK_RUN_MAX == 0, "runs must not cross tiles");
 constexpr uint32_t SK_WCH = 28;  // chars per packed word
@@ -176,8 +180,10 @@ __global__ __launch_bounds__(SK_BLOCK) void sk_runs_kernel(const uint8_t *__rest
                                                           uint64_t *__restrict__ words, uint32_t *__restrict__ nwords,
                                                           uint32_t *__restrict__ cnt) {
     constexpr int NC = SK_TILE + SK_KMAX;
-    __shared__ uint8_t s_own[SK_TILE + SK_TILE / 4 + 16];
-    __shared__ uint8_t s_chr[COUNT_ONLY ? 1 : NC + NC / 4 + 16];
+    constexpr int NWC = NC / 16 + 3;  // 2-bit image words (+ the overhang of a word's 3-word read)
+    __shared__ uint8_t s_own[SK_TILE + 1];
+    __shared__ uint16_t s_bnd[SK_BLOCK + 1];       // run boundaries: bit j of field t = window 16 t + j
+    __shared__ uint32_t s_pk[COUNT_ONLY ? 1 : NWC];
     // one 64-bit cursor per owner: runs << 40 | words, so a run's slot and word offset come from
     // one atomic (the receiver finds the runs' first words from the word counts in slot order)
     __shared__ unsigned long long s_cur[SK_MAX_OWNERS];
@@ -193,20 +199,51 @@ __global__ __launch_bounds__(SK_BLOCK) void sk_runs_kernel(const uint8_t *__rest
             s_wbase[o] = toffw[(uint64_t)o * ntiles + blockIdx.x];
         }
     }
-    for (uint32_t i = tid; i < tn; i += SK_BLOCK) s_own[sk_cpad(i)] = own[base + i];
+    const uint32_t r0 = tid * SK_PER;
+    // this thread's 16 owner bytes (+ the one before them)
+    uint8_t ob[SK_PER];
+#pragma unroll
+    for (int q = 0; q < SK_PER; ++q) ob[q] = r0 + q < tn ? own[base + r0 + q] : SK_NONE;
+#pragma unroll
+    for (int q = 0; q < SK_PER; ++q) s_own[r0 + q] = ob[q];
     if (!COUNT_ONLY) {
         const uint32_t nch = tn + K - 1;
-        for (uint32_t i = tid; i < nch; i += SK_BLOCK) s_chr[sk_cpad(i)] = (uint8_t)(encode_dna(seq[base + i]) & 3u);
+        for (uint32_t wi = tid; wi < (uint32_t)NWC; wi += SK_BLOCK) {
+            uint32_t pk = 0, iv;
+            if (16 * wi < nch) pack_word(seq, base + nch, base + 16ull * wi, pk, iv);
+            s_pk[wi] = pk;
+        }
     }
     __syncthreads();
-    const uint32_t r0 = tid * SK_PER;
+    // boundaries: window 0, every SK_RUN_MAX-th window, every owner change; the end of the tile
+    const uint8_t prev0 = r0 ? s_own[r0 - 1] : SK_NONE;
+    uint32_t bnd = 0;
+#pragma unroll
     for (int q = 0; q < SK_PER; ++q) {
         const uint32_t r = r0 + q;
-        if (r >= tn) break;
-        const uint8_t o = s_own[sk_cpad(r)];
-        if (o == SK_NONE || (r % SK_RUN_MAX != 0 && s_own[sk_cpad(r - 1)] == o)) continue;
-        uint32_t e = r + 1;
-        while (e < tn && e % SK_RUN_MAX != 0 && s_own[sk_cpad(e)] == o) ++e;
+        const uint8_t pv = q ? ob[q - 1] : prev0;
+        if (r < tn && (r % SK_RUN_MAX == 0 || ob[q] != pv)) bnd |= 1u << q;
+        if (r >= tn) bnd |= 1u << q;  // past the tile: every position ends a run
+    }
+    s_bnd[tid] = (uint16_t)bnd;
+    if (tid == 0) s_bnd[SK_BLOCK] = 0xFFFFu;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < SK_PER; ++q) {
+        const uint32_t r = r0 + q;
+        const uint8_t o = ob[q];
+        if (r >= tn || o == SK_NONE || !((bnd >> q) & 1u)) continue;
+        // the run's end: the next boundary after r (this thread's field first, then the next fields)
+        uint32_t e;
+        const uint32_t rest = bnd >> (q + 1);
+        if (rest) {
+            e = r + 1 + (uint32_t)__ffs(rest) - 1;
+        } else {
+            uint32_t t = tid + 1;
+            while (!s_bnd[t]) ++t;
+            e = 16 * t + (uint32_t)__ffs((uint32_t)s_bnd[t]) - 1;
+        }
+        e = min(e, tn);
         const uint32_t len = (e - r) + K - 1;
         const uint32_t nw = len / SK_WCH + 1;  // = ceil((len + 1) / 28)
         const unsigned long long old = atomicAdd(&s_cur[o], (1ull << 40) | (unsigned long long)nw);
@@ -218,11 +255,15 @@ __global__ __launch_bounds__(SK_BLOCK) void sk_runs_kernel(const uint8_t *__rest
             cnt[slot] = read_counts[read_of(read_starts, n_reads, rid_at, base + r)];
         }
         for (uint32_t wi = 0; wi < nw; ++wi) {
-            const uint32_t c0 = wi * SK_WCH;
-            const uint32_t m = min(SK_WCH, len - c0);
-            uint64_t v = (uint64_t)m << 56;
-            for (uint32_t j = 0; j < m; ++j) v |= (uint64_t)s_chr[sk_cpad(r + c0 + j)] << (2 * j);
-            words[wo + wi] = v;
+            const uint32_t c0 = r + wi * SK_WCH;  // first char of the word in the tile
+            const uint32_t m = min(SK_WCH, len - wi * SK_WCH);
+            const uint32_t q0 = c0 >> 4, sh = 2 * (c0 & 15);
+            const uint32_t a = s_pk[q0], b = s_pk[q0 + 1], d = s_pk[q0 + 2];
+            const uint32_t lo = sh ? __builtin_amdgcn_alignbit(b, a, sh) : a;
+            const uint32_t hi = sh ? __builtin_amdgcn_alignbit(d, b, sh) : b;
+            uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+            v &= (1ull << (2 * m)) - 1;  // m <= 28: 56 bits at most
+            words[wo + wi] = v | ((uint64_t)m << 56);
         }
     }
     if (COUNT_ONLY) {
