@@ -321,6 +321,8 @@ struct Ctx {
     bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
     bool lu_lean = false;          // MTG_LU_LEAN=1: the speculative level's local pass as local_unique_lean_kernel
     bool fast2 = true;             // MTG_FAST2=0: the u128 rounds' pass B as the generic extract_partition_kernel
+    int canon_mode = 1;            // the single-build extraction's canonical representative (cmode); the
+                                   // super-k-mer owners of a multi-GPU build extract with 2
     uint32_t merge_it = 1;         // MTG_MERGE_IT: local_merge_kernel's least outputs per thread (A/B)
     bool range_scan = false;       // MTG_COLLECT=ranges: a build too big for one pass collects in key ranges
     bool kmc_mirror = true;  // add_kmc copies the first database to the device while reading it
@@ -394,6 +396,11 @@ struct Ctx {
 };
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// the extraction kernels' canonical argument: 0 basic, 1 min(fwd, rc), 2 the strand whose top 12 bits hash
+// smaller (boss_kernels.hpp: take_rc) -- any one representative per {x, rc x} gives the same real edges and
+// weights; 2 spreads the representatives over the key space (the multi-GPU collects, Ctx::canon_mode)
+static inline int cmode(const Ctx &c, bool canonical) { return canonical ? c.canon_mode : 0; }
 
 // The few environment switches, read once per constructor.  All but MTG_DEBUG / MTG_TRACE select
 // alternate device paths that exist for correctness (fallbacks the parity tests force on small
@@ -1464,7 +1471,7 @@ static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax,
         uint32_t *tcnt = (uint32_t *)c.ws.get(Workspace::DTCNT, (tiles + 1) * 4);
         uint64_t *toff = (uint64_t *)c.ws.get(Workspace::DTOFF, (tiles + 1) * 8);
         extract_kernel<L2, COUNTED, true><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
+            in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
             nullptr, nullptr, tcnt, nullptr, nullptr, 0);
         HIP_CHECK(hipGetLastError());
         uint32_t ep;
@@ -1476,7 +1483,7 @@ static uint64_t stage_extract(Ctx &c, unsigned K, bool canonical, uint32_t cmax,
         HIP_CHECK(hipGetLastError());
         N = read_u64(c, (const unsigned long long *)(toff + tiles));
         extract_kernel<L2, COUNTED, false><<<dim3((unsigned)tiles), dim3(256), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
+            in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
             *ka, *ca, nullptr, toff, nullptr, 0);
         HIP_CHECK(hipGetLastError());
     }
@@ -1511,7 +1518,7 @@ static bool stage_extract_windows(Ctx &c, unsigned K, bool canonical, uint32_t c
     HIP_CHECK(hipMemsetAsync(&c.small->wbad, 0, 4, c.stream));
     HIP_CHECK(hipMemsetAsync(&c.small->wcursor, 0, 8, c.stream));
     window_reads_kernel<L2, COUNTED><<<dim3((unsigned)ceil_div(n, 256 * 8)), dim3(256), 0, c.stream>>>(
-        in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, n, cmax, *ka,
+        in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, n, cmax, *ka,
         COUNTED ? *ca : nullptr, &c.small->wcursor, &c.small->wbad);
     HIP_CHECK(hipGetLastError());
     uint32_t bad = 0;
@@ -1592,10 +1599,10 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
     // (K > 32: the sampled k-mers need u128 words -- truncated to 64 bits, distinct k-mers collided and
     // the duplication estimate planned too few MSD bits for the u128 rounds)
     if (K > 32)
-        dup_sample_reads_kernel<2><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+        dup_sample_reads_kernel<2><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, cmode(c, canonical),
                                                                               M, table, SLOTS - 1, table + SLOTS);
     else
-        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+        dup_sample_reads_kernel<1><<<dim3(M / 256), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, cmode(c, canonical),
                                                                               M, table, SLOTS - 1, table + SLOTS);
     HIP_CHECK(hipGetLastError());
     constexpr int TILE = ExtractTraits<1>::TILE;
@@ -1637,13 +1644,13 @@ static void fused_pass_a(Ctx &c, unsigned K, bool canonical, const BuildInput &i
     }
     if (K > 32) {
         if (K == 63 && c.kspec)
-            extract_hist_wide_kernel<63><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+            extract_hist_wide_kernel<63><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, cmode(c, canonical),
                                                                               tiles, per_row, rows, sample);
         else
-            extract_hist_wide_kernel<0><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, canonical ? 1 : 0,
+            extract_hist_wide_kernel<0><<<dim3(nrows), dim3(256), 0, c.stream>>>(in.seq, in.seq_len, K, cmode(c, canonical),
                                                                              tiles, per_row, rows, sample);
     } else {
-        launch_hist_fast<false>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, canonical ? 1 : 0, tiles, per_row,
+        launch_hist_fast<false>(c, K, dim3(nrows), dim3(256), in.seq, in.seq_len, K, cmode(c, canonical), tiles, per_row,
                                 rows, (uint32_t *)nullptr, sample);
     }
     HIP_CHECK(hipGetLastError());
@@ -1731,37 +1738,37 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
         constexpr int B = fused_block<2>();
         if (b1 > 9) throw std::runtime_error("the u128 pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, B>::TILE);
-        if (!COUNTED && c.fast2 && K > 32 && K <= 64) {
+        if (!COUNTED && c.fast2 && K > 32 && K <= 64 && cmode(c, canonical) <= 1) {
             if (K == 63 && c.kspec)
                 extract_partition_fast2_kernel<B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
-                    in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
+                    in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
                     (const uint32_t *)dsel);
             else
                 extract_partition_fast2_kernel<B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
-                    in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
+                    in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
                     (const uint32_t *)dsel);
         } else if (K == 63 && c.kspec)
             extract_partition_kernel<2, COUNTED, B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
+                in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
                 A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
         else
             extract_partition_kernel<2, COUNTED, B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
-                in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
+                in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
                 A.per_stripe, scur, send, ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
     } else if (fast_b) {
         constexpr int B = 512;
         const dim3 g((unsigned)xcd_grid(ceil_div(A.npos, 16 * B)));
         if (b1 > 9)
-            launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur,
+            launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur,
                                       send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr);
         else
-            launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur,
+            launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur,
                                      send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr);
     } else {
         if (b1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, 512>::TILE);
         extract_partition_kernel<1, COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
-            in.seq, in.seq_len, K, canonical ? 1 : 0, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
+            in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
             A.per_stripe, scur, send, (Key<1> *)ka, COUNTED ? ca : nullptr, &c.small->error, dsel);
     }
     HIP_CHECK(hipGetLastError());
@@ -1822,10 +1829,10 @@ static uint64_t fused_pass_b_spec(Ctx &c, unsigned K, bool canonical, const Buil
     constexpr int B = 512;
     const dim3 g((unsigned)xcd_grid(ceil_div(A.npos, 16 * B)));
     if (b1 > 9)
-        launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send,
+        launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send,
                                   *ka, &c.small->error, (const uint32_t *)nullptr, &c.small->spec_ovf);
     else
-        launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, canonical ? 1 : 0, b1, A.per_stripe, scur, send,
+        launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send,
                                  *ka, &c.small->error, (const uint32_t *)nullptr, &c.small->spec_ovf);
     HIP_CHECK(hipGetLastError());
     tm.mark();
@@ -3680,11 +3687,21 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
         double dup = 0;
         const uint32_t *hist1 = nullptr;
         MsdPlan fplan{};
+        // a super-k-mer owner keeps the representative whose top bits hash smaller (cmode 2): its keys
+        // spread evenly over the key space instead of piling up at small prefixes (min(fwd, rc)), so the
+        // local sort's buckets do not overflow, and the range owners' shares stay even
+        struct ModeScope {
+            Ctx &c;
+            int old;
+            ~ModeScope() { c.canon_mode = old; }
+        } mode_scope{c, c.canon_mode};
+        if (sk && d.P > 1) c.canon_mode = 2;
         if (stage_extract_windows<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N))
             dup = 1.0;
         else if (!stage_extract_fused<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb, &N, &dup, &hist1,
                                                     &fplan))
             N = stage_extract<L2, COUNTED>(c, K, canonical, cmax, cin, &ka, &kb, &ca, &cb);
+        c.canon_mode = mode_scope.old;
         if (sk) {  // the windows of this rank's reads, not of the received runs
             T.n_positions = in.seq_len >= K ? in.seq_len - K + 1 : 0;
         }

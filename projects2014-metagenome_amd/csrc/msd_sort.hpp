@@ -1140,6 +1140,12 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     __shared__ uint32_t s_rv[COUNTED ? CAP : 1], s_sv[COUNTED ? CAP : 1], s_cv[COUNTED ? CAP : 1];
     __shared__ uint32_t s_hist[256], s_fill[256];
     __shared__ int s_hb;
+    // index gaps longer than IGAP entries between two consecutive outputs, filled by the whole workgroup
+    // after the merge (a thread filling them alone serialized groups that span many sparse buckets: an
+    // 8-rank super-k-mer build's rc merge took 0.1-0.8 s per launch)
+    constexpr uint32_t IGAP = 64, NGAP = 64;
+    __shared__ uint32_t s_glo[NGAP], s_ghi[NGAP], s_go[NGAP];
+    __shared__ uint32_t s_gn;
     const uint32_t tid = threadIdx.x;
     const uint64_t g = glist ? glist[blockIdx.x] : g_base + blockIdx.x;
     const uint64_t g0 = gstart[g], g1 = gend ? (uint64_t)gend[g] : gstart[g + 1];
@@ -1176,7 +1182,10 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         s_hist[tid] = 0;
         s_fill[tid] = 0;
     }
-    if (tid == 0) s_hb = -1;
+    if (tid == 0) {
+        s_hb = -1;
+        s_gn = 0;
+    }
     __syncthreads();
     if (nr) {
         const Key<L> ref = s_r[0];
@@ -1250,9 +1259,23 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         if (take_r) ++i; else ++j;
         if (istart) {
             const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
-            for (uint64_t x = prevb + 1; x <= kb; ++x) istart[x] = base + o;
+            uint32_t q = NGAP;
+            if (kb > prevb + IGAP && kb - ifirst < 0xFFFFFFFFull) q = atomicAdd(&s_gn, 1u);
+            if (q < NGAP) {
+                s_glo[q] = (uint32_t)(prevb + 1 - ifirst);
+                s_ghi[q] = (uint32_t)(kb - ifirst);
+                s_go[q] = o;
+            } else {
+                for (uint64_t x = prevb + 1; x <= kb; ++x) istart[x] = base + o;
+            }
             prevb = kb;
         }
+    }
+    if (istart) {  // the long gaps, by the whole workgroup
+        __syncthreads();
+        const uint32_t ng = min(s_gn, NGAP);
+        for (uint32_t q = 0; q < ng; ++q)
+            for (uint64_t x = ifirst + s_glo[q] + tid; x <= ifirst + s_ghi[q]; x += LB) istart[x] = base + s_go[q];
     }
     if (istart) {  // after the group's last key, up to the end of its range
         uint64_t lastb = ifirst - 1;
