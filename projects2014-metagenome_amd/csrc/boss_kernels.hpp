@@ -786,17 +786,22 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     const Key<L> *__restrict__ keys, uint64_t n, unsigned K, const uint64_t *__restrict__ start,
     unsigned bshift, uint8_t *__restrict__ flags, uint8_t *__restrict__ in_flag,
     const Key<L> *__restrict__ q = nullptr, uint64_t nq = 0) {
+    // (round 5) the tile's edges come in as 16-byte loads, a thread's PER flag bytes go out as one
+    // store, and the in-edge marks of staged edges are set in LDS first and written over the staged
+    // ranges in order (consecutive lanes, consecutive bytes) instead of one scattered byte per probe
     using T = DummyTraits<L>;
     const Key<L> *__restrict__ look = q ? q : keys;
     const uint64_t nl = q ? nq : n;
     constexpr int PER = T::PER;
     __shared__ Key<L> s_r[T::CAP];
+    __shared__ uint32_t s_hit[(T::CAP + 3) / 4];  // in-edge marks of the staged edges (bytes)
     __shared__ uint64_t s_lo[4];
     __shared__ uint32_t s_cnt[4], s_off[4];
     const uint32_t tid = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * T::TILE;
     const uint32_t tn = (uint32_t)min((uint64_t)T::TILE, n - base);
     const Key<L> m3 = Key<L>::from(3);
+    uint8_t *s_hitb = reinterpret_cast<uint8_t *>(s_hit);
 
     if (tid < 4) {
         // key range of the sink probes of label c = tid, read off the bucket index
@@ -808,18 +813,30 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         s_lo[tid] = a;
         s_cnt[tid] = (uint32_t)min(b - a, (uint64_t)0xFFFFFFFFu);
     }
+    for (uint32_t i = tid; i < (uint32_t)(T::CAP + 3) / 4; i += 256) s_hit[i] = 0;
     const uint32_t j0 = tid * PER;
     Key<L> x[PER];
     uint32_t first = 0;
     {
         Key<L> prev = base + j0 > 0 && j0 < tn ? keys[base + j0 - 1] : Key<L>::zero();
+        const Key<L> *src = keys + base + j0;
+        if constexpr (L == 1 && PER == 4) {
+            if (j0 + PER <= tn && (((uintptr_t)src) & 15) == 0) {
+                const ulonglong2 a = *(const ulonglong2 *)src, b = *(const ulonglong2 *)(src + 2);
+                x[0] = Key<L>::from(a.x), x[1] = Key<L>::from(a.y), x[2] = Key<L>::from(b.x), x[3] = Key<L>::from(b.y);
+            } else {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            x[q] = Key<L>::zero();
-            if (j0 + q < tn) {
-                x[q] = keys[base + j0 + q];
-                if (base + j0 + q == 0 || shr(prev, 2) != shr(x[q], 2)) first |= 1u << q;
-                prev = x[q];
+                for (int q2 = 0; q2 < PER; ++q2) x[q2] = j0 + q2 < tn ? src[q2] : Key<L>::zero();
+            }
+        } else {
+#pragma unroll
+            for (int q2 = 0; q2 < PER; ++q2) x[q2] = j0 + q2 < tn ? src[q2] : Key<L>::zero();
+        }
+#pragma unroll
+        for (int q2 = 0; q2 < PER; ++q2) {
+            if (j0 + q2 < tn) {
+                if (base + j0 + q2 == 0 || shr(prev, 2) != shr(x[q2], 2)) first |= 1u << q2;
+                prev = x[q2];
             }
         }
     }
@@ -844,17 +861,18 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = look[a + j];
     }
     __syncthreads();
+    uint32_t fw = 0;  // this thread's flag bytes, byte q = edge j0 + q
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        if (j0 + q >= tn) continue;
+    for (int q2 = 0; q2 < PER; ++q2) {
+        if (j0 + q2 >= tn) continue;
         if (ABL & 12) {
-            if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)(1u | (((first >> q) & 1u) << 1)) ^ (uint8_t)s_r[q & 7].w[0];
+            fw |= (uint32_t)((uint8_t)(1u | (((first >> q2) & 1u) << 1)) ^ (uint8_t)s_r[q2 & 7].w[0]) << (8 * q2);
             continue;
         }
-        const uint32_t c = (uint32_t)(x[q].w[0] & 3);
+        const uint32_t c = (uint32_t)(x[q2].w[0] & 3);
         // to_next(x, K, 0): node a_2..a_K, label 0 (kmer_boss.hpp:147-169)
-        const Key<L> p = (shr(x[q], 2) | shl(Key<L>::from(c), 2 * (K - 1))) & ~m3;
-        uint64_t hit = ~0ull;
+        const Key<L> p = (shr(x[q2], 2) | shl(Key<L>::from(c), 2 * (K - 1))) & ~m3;
+        bool hit = false;
         const uint32_t off = s_off[c];
         if (off != ~0u) {
             const uint32_t cnt = s_cnt[c];
@@ -863,14 +881,43 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
                 const uint32_t mid = (lo + hi) >> 1;
                 if (s_r[off + mid] < p) lo = mid + 1; else hi = mid;
             }
-            if (lo < cnt && shr(s_r[off + lo], 2) == shr(p, 2)) hit = s_lo[c] + lo;
+            if (lo < cnt && shr(s_r[off + lo], 2) == shr(p, 2)) {
+                hit = true;
+                if (!(ABL & 1)) s_hitb[off + lo] = 1;
+            }
         } else {
             const uint64_t i = lower_bound_bucketed(look, start, bshift, p);
-            if (i < nl && shr(look[i], 2) == shr(p, 2)) hit = i;
+            if (i < nl && shr(look[i], 2) == shr(p, 2)) {
+                hit = true;
+                if (!(ABL & 1)) in_flag[i] = 1;
+            }
         }
-        if (!(ABL & 1) && hit != ~0ull) in_flag[hit] = 1;
-        if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)((hit == ~0ull ? 1u : 0u) | (((first >> q) & 1u) << 1));
-        else if (hit == 12345) flags[0] = 1;  // keep the search
+        fw |= ((hit ? 0u : 1u) | (((first >> q2) & 1u) << 1)) << (8 * q2);
+    }
+    if (!(ABL & 2)) {
+        uint8_t *fo = flags + base + j0;
+        if (j0 + PER <= tn && (((uintptr_t)fo) & (PER - 1)) == 0) {
+            if constexpr (PER == 4) *(uint32_t *)fo = fw;
+            else *(uint16_t *)fo = (uint16_t)fw;
+        } else {
+#pragma unroll
+            for (int q2 = 0; q2 < PER; ++q2)
+                if (j0 + q2 < tn) fo[q2] = (uint8_t)(fw >> (8 * q2));
+        }
+    } else if (fw == 12345u) {
+        flags[0] = 1;  // keep the search
+    }
+    if (ABL & 13) return;
+    __syncthreads();
+    // the marks of the staged edges, in order over each staged range (only 1s: the ranges of
+    // neighbouring tiles overlap at their ends)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t off = s_off[c];
+        if (off == ~0u) continue;
+        uint8_t *dst = in_flag + s_lo[c];
+        for (uint32_t j = tid; j < s_cnt[c]; j += 256)
+            if (s_hitb[off + j]) dst[j] = 1;
     }
 }
 

@@ -14,6 +14,103 @@
 
 using namespace mtg;
 
+namespace mtg {
+// the round-4 kernel (per-probe byte stores), for the A/B below
+template <int L, int ABL = 0>
+__global__ __launch_bounds__(256) void dummy_sink_kernel_r4(
+    const Key<L> *__restrict__ keys, uint64_t n, unsigned K, const uint64_t *__restrict__ start,
+    unsigned bshift, uint8_t *__restrict__ flags, uint8_t *__restrict__ in_flag,
+    const Key<L> *__restrict__ q = nullptr, uint64_t nq = 0) {
+    using T = DummyTraits<L>;
+    const Key<L> *__restrict__ look = q ? q : keys;
+    const uint64_t nl = q ? nq : n;
+    constexpr int PER = T::PER;
+    __shared__ Key<L> s_r[T::CAP];
+    __shared__ uint64_t s_lo[4];
+    __shared__ uint32_t s_cnt[4], s_off[4];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * T::TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)T::TILE, n - base);
+    const Key<L> m3 = Key<L>::from(3);
+
+    if (tid < 4) {
+        // key range of the sink probes of label c = tid, read off the bucket index
+        const Key<L> c = shl(Key<L>::from(tid), 2 * (K - 1));
+        const Key<L> lo = (shr(keys[base], 2) | c) & ~m3;
+        const Key<L> hi = shr(keys[base + tn - 1], 2) | c | m3;
+        const uint64_t blo = bits_at(shr(lo, bshift), 0, 32), bhi = bits_at(shr(hi, bshift), 0, 32);
+        const uint64_t a = start[blo], b = start[bhi + 1];
+        s_lo[tid] = a;
+        s_cnt[tid] = (uint32_t)min(b - a, (uint64_t)0xFFFFFFFFu);
+    }
+    const uint32_t j0 = tid * PER;
+    Key<L> x[PER];
+    uint32_t first = 0;
+    {
+        Key<L> prev = base + j0 > 0 && j0 < tn ? keys[base + j0 - 1] : Key<L>::zero();
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            x[q] = Key<L>::zero();
+            if (j0 + q < tn) {
+                x[q] = keys[base + j0 + q];
+                if (base + j0 + q == 0 || shr(prev, 2) != shr(x[q], 2)) first |= 1u << q;
+                prev = x[q];
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t cum = 0;
+        for (int c = 0; c < 4; ++c) {
+            s_off[c] = ~0u;  // ~0 = global fallback
+            if ((uint64_t)cum + s_cnt[c] <= (uint64_t)T::CAP) {
+                s_off[c] = cum;
+                cum += s_cnt[c];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (ABL & 4) break;
+        if (s_off[c] == ~0u) continue;
+        const uint64_t a = s_lo[c];
+        const uint32_t off = s_off[c];
+        for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = look[a + j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (j0 + q >= tn) continue;
+        if (ABL & 12) {
+            if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)(1u | (((first >> q) & 1u) << 1)) ^ (uint8_t)s_r[q & 7].w[0];
+            continue;
+        }
+        const uint32_t c = (uint32_t)(x[q].w[0] & 3);
+        // to_next(x, K, 0): node a_2..a_K, label 0 (kmer_boss.hpp:147-169)
+        const Key<L> p = (shr(x[q], 2) | shl(Key<L>::from(c), 2 * (K - 1))) & ~m3;
+        uint64_t hit = ~0ull;
+        const uint32_t off = s_off[c];
+        if (off != ~0u) {
+            const uint32_t cnt = s_cnt[c];
+            uint32_t lo = 0, hi = cnt;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_r[off + mid] < p) lo = mid + 1; else hi = mid;
+            }
+            if (lo < cnt && shr(s_r[off + lo], 2) == shr(p, 2)) hit = s_lo[c] + lo;
+        } else {
+            const uint64_t i = lower_bound_bucketed(look, start, bshift, p);
+            if (i < nl && shr(look[i], 2) == shr(p, 2)) hit = i;
+        }
+        if (!(ABL & 1) && hit != ~0ull) in_flag[hit] = 1;
+        if (!(ABL & 2)) flags[base + j0 + q] = (uint8_t)((hit == ~0ull ? 1u : 0u) | (((first >> q) & 1u) << 1));
+        else if (hit == 12345) flags[0] = 1;  // keep the search
+    }
+}
+
+}  // namespace mtg
+
 __device__ __forceinline__ uint64_t gmix64(uint64_t x) {
     x += 0x9e3779b97f4a7c15ull;
     x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -102,14 +199,32 @@ int main(int argc, char **argv) {
         printf("edges %lu (of %lu windows), bucket bits %u: sinks %lu, nodes %lu, marked in %lu\n", (unsigned long)R,
                (unsigned long)ne, B, (unsigned long)sinks, (unsigned long)firsts, (unsigned long)marked);
     }
+    {
+        // the round-5 kernel against the round-4 one: byte-identical flags and in-edge marks
+        uint8_t *f2, *in2;
+        HIP_CHECK(hipMalloc(&f2, R + 64));
+        HIP_CHECK(hipMalloc(&in2, R + 64));
+        HIP_CHECK(hipMemsetAsync(in2, 0, R, s));
+        dummy_sink_kernel_r4<1><<<dim3((unsigned)stiles), dim3(256), 0, s>>>(keys, R, K, bstart, bshift, f2, in2);
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<uint8_t> a(R), b(R), c(R), d(R);
+        HIP_CHECK(hipMemcpy(a.data(), flags, R, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(b.data(), f2, R, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(c.data(), in_flag, R, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(d.data(), in2, R, hipMemcpyDeviceToHost));
+        printf("round-5 vs round-4 kernel: flags %s, in-edge marks %s\n", a == b ? "equal" : "DIFFER",
+               c == d ? "equal" : "DIFFER");
+        if (a != b || c != d) return 1;
+    }
     auto run = [&](const char *what, auto kern) {
         const float t = time_ms(s, 5, [&] {
-            kern<<<dim3((unsigned)stiles), dim3(256), 0, s>>>(keys, R, K, bstart, bshift, flags, in_flag);
+            kern<<<dim3((unsigned)stiles), dim3(256), 0, s>>>(keys, R, K, bstart, bshift, flags, in_flag, nullptr, 0);
         });
         printf("%-44s %.3f ms  (%.1f GB/s of 19 B/edge)\n", what, t, R * 19.0 / 1e9 / (t * 1e-3));
     };
     const float tm = time_ms(s, 5, [&] { HIP_CHECK(hipMemsetAsync(in_flag, 0, R, s)); });
     printf("%-44s %.3f ms\n", "memset in_flag", tm);
+    run("dummy_sink round 4 (per-probe stores)", dummy_sink_kernel_r4<1, 0>);
     run("dummy_sink (product)", dummy_sink_kernel<1, 0>);
     run("no in_flag stores", dummy_sink_kernel<1, 1>);
     run("no flags stores", dummy_sink_kernel<1, 2>);
