@@ -857,8 +857,24 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         if (ABL & 4) break;
         if (s_off[c] == ~0u) continue;
         const uint64_t a = s_lo[c];
-        const uint32_t off = s_off[c];
-        for (uint32_t j = tid; j < s_cnt[c]; j += 256) s_r[off + j] = look[a + j];
+        const uint32_t off = s_off[c], cnt = s_cnt[c];
+        if constexpr (L == 1) {
+            if ((((uintptr_t)look) & 15) == 0) {
+                // 16-byte loads from the even index at or below a (half the load instructions)
+                const uint64_t a0 = a & ~1ull, e = a + cnt;
+                for (uint64_t i = a0 + 2ull * tid; i < e; i += 512) {
+                    if (i + 1 < nl) {  // (never past the array's last key)
+                        const ulonglong2 v = *(const ulonglong2 *)(look + i);
+                        if (i >= a) s_r[off + (uint32_t)(i - a)] = Key<L>::from(v.x);
+                        if (i + 1 < e) s_r[off + (uint32_t)(i + 1 - a)] = Key<L>::from(v.y);
+                    } else if (i >= a) {
+                        s_r[off + (uint32_t)(i - a)] = look[i];
+                    }
+                }
+                continue;
+            }
+        }
+        for (uint32_t j = tid; j < cnt; j += 256) s_r[off + j] = look[a + j];
     }
     __syncthreads();
     uint32_t fw = 0;  // this thread's flag bytes, byte q = edge j0 + q

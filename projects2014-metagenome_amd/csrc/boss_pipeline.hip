@@ -65,7 +65,8 @@ class Workspace {
         LAST_BITS, DPOS, DWL, RANGE_BINS, MSD_GBUCKET, RC_CSTART, RC_COMB, RC_SENDC, PACKED, W4, FA_RAW, FA_TLAST, FA_PREV, FA_TA, FA_TB, FA_OA, FA_OB, FA_KOFF, RID_AT, BRUNS,
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
-        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, RC_L1START, RC_L1CUR, RC_TILEG, NSLOTS
+        FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, RC_L1START, RC_L1CUR, RC_TILEG,
+        KA2, ROUND_DELTA, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -136,7 +137,7 @@ class Workspace {
         for (Slot sl : {KA, KB, CA, CB, SUMS, BUCKETS, FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, FB_K, FB_V,
                         RC_ALT, RC_ALTC, REAL, REALC, INFLAG, XA, XAC, XB, XBC, QSEND, QRECV, QFLAG, DSRC, DSEND,
                         DRECV, RC_SENDC, LAST_BITS, W4, WN, DPOS, DWL, CANON, CANONC, CANON_IDX, SPEC_A, SPEC_B,
-                        SPEC_AC, SPEC_BC})
+                        SPEC_AC, SPEC_BC, KA2})
             release(sl);
     }
     // a slot gives its buffer back (batched builds drop their round buffers before the later stages
@@ -368,6 +369,7 @@ struct Ctx {
     // step overflowed into the exact level, sort 30.3 -> 38.9 ms; level 3 now samples every tile's
     // first eighth.)
     bool spec3 = true;
+    bool rounds_one_b = false;  // MTG_ROUNDS_ONE_B=1: two collect rounds share one pass B (collect_rounds_fused)
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
     bool spec_tiny = false;  // MTG_SPEC_CAPS=tiny: speculative buckets without slack (tests force the
@@ -427,6 +429,7 @@ static void load_knobs(Ctx &c) {
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
+    c.rounds_one_b = is("MTG_ROUNDS_ONE_B", "1");
     c.spec_tiny = is("MTG_SPEC_CAPS", "tiny");
     c.spec_lu_fail = is("MTG_SPEC_LU_FAIL", "1");
     c.spec_l1 = !is("MTG_SPEC_L1", "0");
@@ -1394,8 +1397,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
 
 template <int L>
 static unsigned bucket_bits(uint64_t n, unsigned keybits) {
+    // ~4 keys a bucket; at most 2^26 buckets up to 2^30 keys (configs[1]: 5.5 a bucket), 2^29 above: at
+    // configs[3]'s share (4.7e9 real edges) 2^26 buckets held 69 edges each, and the dummy sink join's
+    // staged class ranges (whole buckets at both ends) outgrew its LDS and fell back to global searches
+    const unsigned cap = n > (1ull << 30) ? 29 : 26;
     unsigned b = 1;
-    while (b < 26 && (1ull << (b + 2)) < n) ++b;
+    while (b < cap && (1ull << (b + 2)) < n) ++b;
     return std::min(b, keybits);
 }
 
@@ -1694,7 +1701,9 @@ struct BucketSel {
 template <int L, bool COUNTED>
 static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                              const FusedA &A, unsigned b1, const BucketSel *sel, Key<L> *ka, uint32_t *ca,
-                             const uint32_t **dh1_out) {
+                             const uint32_t **dh1_out, const long long *bdelta = nullptr) {
+    // bdelta (the u64 pass B only): per level-1 bucket, where its keys go relative to ka (elements) --
+    // the collect rounds' one pass B writes each round's buckets into that round's own buffer
     const uint32_t nb1 = 1u << b1;
     const unsigned hb = FUSED_HB;
     if (sel && nb1 > 32 * FUSED_SEL_WORDS) throw std::runtime_error("collect round mask: level-1 digit too wide");
@@ -1732,6 +1741,7 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     EventTimer tm(c.stream);
     tm.mark();
     const bool fast_b = L == 1 && !COUNTED && K <= 32;
+    if (bdelta && !fast_b) throw std::runtime_error("per-bucket destinations need the u64 pass B");
     if constexpr (L == 2) {
         // u128 windows (K <= 64): pass B on 256-thread tiles (A was made for them); uncounted canonical /
         // basic builds take the packed-word kernel (MTG_FAST2=0: the generic one)
@@ -1760,10 +1770,10 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
         const dim3 g((unsigned)xcd_grid(ceil_div(A.npos, 16 * B)));
         if (b1 > 9)
             launch_part_fast<B, 1024>(c, K, g, dim3(B), in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur,
-                                      send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr);
+                                      send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr, bdelta);
         else
             launch_part_fast<B, 512>(c, K, g, dim3(B), in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur,
-                                     send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr);
+                                     send, ka, &c.small->error, (const uint32_t *)dsel, (uint32_t *)nullptr, bdelta);
     } else {
         if (b1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, 512>::TILE);
@@ -2140,14 +2150,14 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     // rounds: the later stages hold ~5 keys of 8 B per distinct canonical k-mer (the canonical set, the
     // real edges, the rc sort's two buffers) plus the rows; a round holds its keys twice (+ counts)
     uint32_t R = c.force_ranges;
+    double budget = c.mem_budget;
+    if (budget <= 0) {
+        size_t fr = 0, tot = 0;
+        HIP_CHECK(hipMemGetInfo(&fr, &tot));
+        budget = 0.9 * ((double)fr + (double)c.ws.held());
+    }
+    const double u_est = std::min((double)N, (double)N / A.dup * 1.25);
     if (!R) {
-        double budget = c.mem_budget;
-        if (budget <= 0) {
-            size_t fr = 0, tot = 0;
-            HIP_CHECK(hipMemGetInfo(&fr, &tot));
-            budget = 0.9 * ((double)fr + (double)c.ws.held());
-        }
-        const double u_est = std::min((double)N, (double)N / A.dup * 1.25);
         const double kb = (double)sizeof(K2);
         // (u128: the rounds hold only the growing canonical set beside their buffers, which are released
         // before the rc stage; reserving the later stages' 5 keys per distinct k-mer as well would plan
@@ -2167,11 +2177,41 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         for (uint64_t b = bb[r]; b < bb[r + 1]; ++b) nr[r] += h1[b];
         nmax = std::max(nmax, nr[r]);
     }
-    K2 *ka = (K2 *)c.ws.get(Workspace::KA, nmax * sizeof(K2));
+    // one pass B for every round (MTG_ROUNDS_ONE_B=0: a pass B per round) when the whole level-1 layout
+    // (N keys) fits in KA beside one round's partition buffer and the canonical set: the rounds then
+    // sort their slices of it, and the reads are scanned once instead of R times (configs[3]'s share:
+    // two 40 ms pass-B scans)
+    // MTG_ROUNDS_ONE_B=1: two rounds of the u64 pass B (configs[3]'s share) become one when both rounds'
+    // keys fit beside the partition buffer and the canonical set: the pass writes round 0's buckets into
+    // KA and round 1's into KA2 (per-bucket destinations, bdelta), so the reads are scanned once (pass B
+    // 2 x 40 -> 48.7 ms).  Off by default: the third ~64 GB block fragments the workspace for the later
+    // stages (their 4-20 GB requests were handed the idle 64 GB blocks once HBM ran out, and the emit
+    // ran out of memory at configs[3]'s share; gpurun_out/r5p), and freeing it costs ~12 ms per GB
+    bool one_b = false;
+    if (R == 2 && c.rounds_one_b && L == 1 && !COUNTED && K <= 32) {
+        const double kb = (double)sizeof(K2);
+        const double need = ((double)N + (double)nmax) * kb + u_est * 1.25 * kb + (double)(1ull << 30);
+        one_b = need <= budget;
+    }
+    K2 *ka = (K2 *)c.ws.get(Workspace::KA, (one_b ? nr[0] : nmax) * sizeof(K2));
+    K2 *ka2 = one_b ? (K2 *)c.ws.get(Workspace::KA2, std::max<uint64_t>(nr[1], 1) * sizeof(K2)) : nullptr;
     K2 *kb = (K2 *)c.ws.get(Workspace::KB, nmax * sizeof(K2));
     uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nmax * 4) : nullptr;
     uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nmax * 4) : nullptr;
     tr("rounds: buffers", R, nmax);
+    if (one_b) {
+        // round 1's buckets start at nr[0] in the pass's layout and at ka2 in memory
+        std::vector<long long> delta(nb1, 0);
+        const long long d1 = (long long)(ka2 - ka) - (long long)nr[0];
+        for (uint32_t b = (uint32_t)bb[1]; b < nb1; ++b) delta[b] = d1;
+        long long *dd = (long long *)c.ws.get(Workspace::ROUND_DELTA, nb1 * 8);
+        HIP_CHECK(hipMemcpyAsync(dd, delta.data(), nb1 * 8, hipMemcpyHostToDevice, c.stream));
+        const uint32_t *dh1_all = nullptr;
+        const uint64_t n = fused_pass_b<L, COUNTED>(c, K, canonical, cmax, in, A, b1, nullptr, ka, ca, &dh1_all, dd);
+        if (n != N) throw std::runtime_error("the collect rounds' pass B differs from its histogram");
+        tr("rounds: pass B (both rounds)", R, n);
+    }
+    std::vector<uint32_t> h1r(nb1);  // one_b: a round's level-1 counts (zero outside its buckets)
     if (c.debug)
         fprintf(stderr, "[mtg debug] canonical rounds: N=%lu dup=%.2f levels=%u digit1=%u rounds=%u largest=%lu\n",
                 (unsigned long)N, A.dup, plan.levels, b1, R, (unsigned long)nmax);
@@ -2186,13 +2226,25 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     for (uint32_t r = 0; r < R; ++r) {
         if (!nr[r]) continue;
         const uint32_t *dh1 = nullptr;
-        BucketSel sel;
-        sel.add(bb[r], bb[r + 1]);
-        const uint64_t n = fused_pass_b<L, COUNTED>(c, K, canonical, cmax, in, A, b1, &sel, ka, ca, &dh1);
-        if (n != nr[r]) throw std::runtime_error("a collect round's k-mers differ from its histogram");
-        tr("rounds: pass B", r, n);
+        uint64_t n = 0;
         K2 *xa = ka, *xb = kb;
         uint32_t *xac = ca, *xbc = cb;
+        if (one_b) {
+            // this round's slice of the whole layout, and its level-1 counts
+            for (uint32_t b = 0; b < nb1; ++b) h1r[b] = b >= bb[r] && b < bb[r + 1] ? (uint32_t)h1[b] : 0u;
+            uint32_t *d = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
+            HIP_CHECK(hipMemcpyAsync(d, h1r.data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
+            HIP_CHECK(hipStreamSynchronize(c.stream));  // h1r is rewritten next round
+            dh1 = d;
+            n = nr[r];
+            xa = r == 0 ? ka : ka2;
+        } else {
+            BucketSel sel;
+            sel.add(bb[r], bb[r + 1]);
+            n = fused_pass_b<L, COUNTED>(c, K, canonical, cmax, in, A, b1, &sel, ka, ca, &dh1);
+            if (n != nr[r]) throw std::runtime_error("a collect round's k-mers differ from its histogram");
+            tr("rounds: pass B", r, n);
+        }
         c.track_partition = first;  // the roofline's partition pass: the first round's level 2
         const uint64_t U = msd_sort_unique<L, COUNTED>(c, &xa, &xb, &xac, &xbc, n, 2 * K, cmax, A.dup, dh1, false,
                                                        nullptr, true, nullptr, &plan);
@@ -2222,7 +2274,8 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     debug_check_sorted(c, "canonical rounds", *out, off);
     // the round buffers (sized for the largest round) go; the rc stage takes KB and SPEC_A again at
     // its own size
-    for (auto sl : {Workspace::KA, Workspace::CA, Workspace::KB, Workspace::CB, Workspace::SPEC_A, Workspace::SPEC_B})
+    for (auto sl : {Workspace::KA, Workspace::KA2, Workspace::CA, Workspace::KB, Workspace::CB, Workspace::SPEC_A,
+                    Workspace::SPEC_B})
         c.ws.release(sl);
     // the fused rc merge reads the canonical keys through their bucket index over the rc sort's final
     // bits (a one-pass build gets it from its own sort's groups)

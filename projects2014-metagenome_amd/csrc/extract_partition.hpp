@@ -368,9 +368,11 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
     Key<1> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr,
-    uint32_t *__restrict__ povf = nullptr) {
+    uint32_t *__restrict__ povf = nullptr, const long long *__restrict__ bdelta = nullptr) {
     // povf (the speculative level-1 layout): a reservation past its segment's end writes nothing and
     // raises *povf instead of the error word -- the caller then runs the exact passes A and B
+    // bdelta (the collect rounds' one pass B): bucket i's keys go bdelta[i] elements away from their
+    // layout position (each round's buckets into that round's buffer)
     const unsigned K = KC ? (unsigned)KC : K_;
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
     constexpr int NBMAX = NB;
@@ -490,6 +492,8 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
             if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
                 atomicOr(povf ? povf : error, povf ? 1u : 2u);  // write past its range
                 g = ~0ull;
+            } else if (bdelta) {
+                g += (unsigned long long)bdelta[i];
             }
             s_gbase[i] = g;
         }

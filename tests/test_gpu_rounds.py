@@ -56,6 +56,20 @@ def test_rounds_random_reads(small_fused, rounds, k):
             assert t.collect_mode == ROUNDS and t.n_batches == rounds, (t.collect_mode, t.n_batches)
 
 
+@pytest.mark.parametrize("k", [20, 31])
+def test_rounds_pass_b_per_round_knob(small_fused, k):
+    # two rounds of the u64 pass B run as one pass writing each round's buckets into its own buffer;
+    # (MTG_ROUNDS_ONE_B=1, opt-in); 0: a pass B per round (the masked scan)
+    small_fused.setenv("MTG_RANGES", "2")
+    reads = _random_reads(3000 + k, 400, 150, 5000, n_rate=0.005, lower=True)
+    for one_b in ("1", "0"):
+        small_fused.setenv("MTG_ROUNDS_ONE_B", one_b)
+        for canonical in (False, True):
+            for bits in (0, 8):
+                _, t = _check(k, reads, canonical, bits)
+                assert t.collect_mode == ROUNDS and t.n_batches == 2, (t.collect_mode, t.n_batches)
+
+
 def test_rounds_counts_saturate(small_fused):
     small_fused.setenv("MTG_RANGES", "4")
     rng = np.random.default_rng(18)
