@@ -935,7 +935,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
                 local_unique_lean_kernel<LocalTraits<1>::SLOTS / 2><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                     (const uint64_t *)sa, bstart, cur, (uint64_t *)sb, ucount, ovf, &c.small->counter, g0);
             else if (keycas && c.lu_fast)
-                local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE, true>
+                local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE, true, false>
                     <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
                                                             &c.small->counter, cmax, cur, g0);
             else if (keycas)
@@ -1259,6 +1259,13 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 constexpr int WPE = (L == 1 && KC && !ND && !COUNTED) ? MTG_LU_WPE : 1;
                 bucket_pieces(0, count, [&](uint64_t g0, unsigned cnt) {
                     if constexpr (KC && !ND) {
+                        if (c.lu_fast && sbits == 0) {  // the first launch: no key-range slices
+                            local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE, true, false><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                                *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits,
+                                *alt, COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax, nullptr,
+                                glist ? 0 : g0);
+                            return;
+                        }
                         if (c.lu_fast) {
                             local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE, true><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                                 *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits,
@@ -1581,15 +1588,26 @@ static bool fused_applies(const Ctx &c, unsigned K, uint64_t npos, unsigned kmax
 // pass A over every window, and the duplication estimate from a sample of windows (on a side stream
 // it overlapped pass A but measured no faster: 26.3 vs 26.2 ms per step)
 // the fused passes with K = 31 compiled in (KC, extract_partition.hpp) unless MTG_KSPEC=0
+// (K = 31 also takes the canonical mode cm as a template constant: extract_partition.hpp, CM)
 template <bool OTHER, typename... A>
-static void launch_hist_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, A... a) {
-    if (K == 31 && c.kspec) extract_hist_fast_kernel<OTHER, 31><<<g, b, 0, c.stream>>>(a...);
-    else extract_hist_fast_kernel<OTHER, 0><<<g, b, 0, c.stream>>>(a...);
+static void launch_hist_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, const uint8_t *seq, uint64_t seq_len,
+                             unsigned K_, int cm, A... a) {
+    if (K == 31 && c.kspec && cm == 0) extract_hist_fast_kernel<OTHER, 31, 0><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
+    else if (K == 31 && c.kspec && cm == 1) extract_hist_fast_kernel<OTHER, 31, 1><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
+    else if (K == 31 && c.kspec && cm == 2) extract_hist_fast_kernel<OTHER, 31, 2><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
+    else extract_hist_fast_kernel<OTHER, 0><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
 }
 template <int BLOCK, int NB, typename... A>
-static void launch_part_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, A... a) {
-    if (K == 31 && c.kspec) extract_partition_fast_kernel<BLOCK, NB, 31><<<g, b, 0, c.stream>>>(a...);
-    else extract_partition_fast_kernel<BLOCK, NB, 0><<<g, b, 0, c.stream>>>(a...);
+static void launch_part_fast(const Ctx &c, unsigned K, dim3 g, dim3 b, const uint8_t *seq, uint64_t seq_len,
+                             unsigned K_, int cm, A... a) {
+    if (K == 31 && c.kspec && cm == 0)
+        extract_partition_fast_kernel<BLOCK, NB, 31, 0><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
+    else if (K == 31 && c.kspec && cm == 1)
+        extract_partition_fast_kernel<BLOCK, NB, 31, 1><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
+    else if (K == 31 && c.kspec && cm == 2)
+        extract_partition_fast_kernel<BLOCK, NB, 31, 2><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
+    else
+        extract_partition_fast_kernel<BLOCK, NB, 0><<<g, b, 0, c.stream>>>(seq, seq_len, K_, cm, a...);
 }
 
 // sample > 1 (fused_pass_b_spec): every row counts every sample-th of its tiles, and the 2048 rows form

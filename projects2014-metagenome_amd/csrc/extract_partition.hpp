@@ -94,15 +94,19 @@ __device__ __forceinline__ uint32_t rc_word(uint32_t w) {
 // KC (both fused passes): the window length K as a compile-time constant (0 = the runtime argument);
 // the host instantiates KC = 31, the k = 30 BOSS build of BASELINE configs[1] / [3], so the 64-bit masks
 // and shifts of the window loop fold into immediates
-template <bool OTHER = false, int KC = 0>
+// CM (both fused passes): the canonical mode as a compile-time constant (-1 = the runtime argument):
+// a runtime mode split every window's code into branches around the hash-canonical test, and the 16
+// windows of a thread could not be scheduled together
+template <bool OTHER = false, int KC = 0, int CM = -1>
 __global__ __launch_bounds__(256) void extract_hist_fast_kernel(const uint8_t *__restrict__ seq, uint64_t seq_len,
-                                                                unsigned K_, int canonical, uint64_t ntiles,
+                                                                unsigned K_, int canonical_, uint64_t ntiles,
                                                                 uint64_t per_row, uint32_t *__restrict__ rows,
                                                                 uint32_t *__restrict__ rows_other = nullptr,
                                                                 uint32_t tstride = 1) {
     // tstride > 1: a sample -- row r counts every tstride-th of its tiles (the speculative level-1
     // layout of fused_pass_b_spec sizes its segments from it)
     const unsigned K = KC ? (unsigned)KC : K_;
+    const int canonical = CM >= 0 ? CM : canonical_;
     constexpr int BLOCK = 256, PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;
     constexpr uint32_t NB = 1u << FUSED_HB;
     static_assert(FUSED_HB == 12, "6-char tops");
@@ -363,9 +367,9 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
 // NB: the widest digit's bucket count (1024: a 10-bit level 1, so that inputs of ~2e9 k-mers keep a
 // 2-level plan).  The bucket counts live in the run-base array until the scan has read them, and the
 // in-tile offsets are u16, so NB = 1024 still fits two workgroups per CU (78 KB of LDS).
-template <int BLOCK, int NB = 512, int KC = 0>
+template <int BLOCK, int NB = 512, int KC = 0, int CM = -1>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
-    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical, unsigned b,
+    const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical_, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
     Key<1> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr,
     uint32_t *__restrict__ povf = nullptr, const long long *__restrict__ bdelta = nullptr) {
@@ -374,6 +378,7 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     // bdelta (the collect rounds' one pass B): bucket i's keys go bdelta[i] elements away from their
     // layout position (each round's buckets into that round's buffer)
     const unsigned K = KC ? (unsigned)KC : K_;
+    const int canonical = CM >= 0 ? CM : canonical_;
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 2;  // +2 words: the last thread's overhang
     constexpr int NBMAX = NB;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;

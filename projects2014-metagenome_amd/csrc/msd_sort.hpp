@@ -502,12 +502,15 @@ __device__ __forceinline__ int key_msb(const Key<L> &k) {
 #ifndef MTG_LU_WPE
 #define MTG_LU_WPE 8
 #endif
+// SLICED: the launch may pass sbits > 0 (the sliced reruns); false compiles the key-range slice test
+// out of the per-key loop (the first launch and the speculative level's)
 template <int L, bool COUNTED, bool KEYCAS, int LB = 512, int SL = LocalTraits<L>::SLOTS,
-          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? MTG_LU_WPE : 1, bool FAST = false>
+          bool NODUP = false, int WPE = (L == 1 && KEYCAS && !NODUP && !COUNTED) ? MTG_LU_WPE : 1, bool FAST = false,
+          bool SLICED = true>
 __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void local_unique_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals,
     const uint64_t *__restrict__ gstart, const uint32_t *__restrict__ glist, unsigned nbits,
-    unsigned b, unsigned sbits, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
+    unsigned b, unsigned sbits_, Key<L> *__restrict__ tmp, uint32_t *__restrict__ tcnt,
     uint32_t *__restrict__ ucount, uint32_t *__restrict__ overflow, uint32_t *__restrict__ novf,
     uint32_t cmax, const unsigned long long *__restrict__ gend = nullptr, uint64_t g_base = 0) {
     // gend (speculative buckets): group g is [gstart[g], gend[g]), with gaps between groups; g_base: the
@@ -543,6 +546,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     // slices: keys split by the sbits bits right below the b-bit bucket prefix; only valid for
     // a group made of one bucket (several buckets would interleave)
+    const unsigned sbits = SLICED ? sbits_ : 0u;
     const unsigned sshift = nbits - b - sbits;
     if (sbits && key_prefix(keys[g0], nbits, b) != key_prefix(keys[g1 - 1], nbits, b)) {
         if (tid == 0) {
@@ -641,7 +645,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 const uint32_t lane = __lane_id();
 #pragma unroll
                 for (int q = 0; q < BATCH * PAIR; ++q) {
-                    const bool act = hv[q] && (!sbits || bits_at(kb[q], sshift, sbits) == slice);
+                    const bool act = hv[q] && (!SLICED || !sbits || bits_at(kb[q], sshift, sbits) == slice);
                     const uint64_t m = __ballot(act);
                     if (!m) continue;
                     const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                 // loop, one LDS atomic per wave (an atomicAdd on s_distinct from the inserting lanes
                 // is the atomic optimizer's lane-by-lane loop: ~5 SALU per new key)
                 int32_t ins = -1;
-                if (hv[q] && !ovf && (!sbits || bits_at(kb[q], sshift, sbits) == slice)) {
+                if (hv[q] && !ovf && (!SLICED || !sbits || bits_at(kb[q], sshift, sbits) == slice)) {
                 const Key<L> key = kb[q];
                 uint32_t h = slot_of<SLOTS>(key_hash(key));
                 for (uint32_t probes = 0;;) {
@@ -1251,12 +1255,20 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         const bool pr = pi > 0 && (pj == 0 || s_c[pj - 1] < s_r[pi - 1]);
         prevb = bits_at(shr(pr ? s_r[pi - 1] : s_c[pj - 1], ishift), 0, 32);
     }
+    // (round 5) the two run heads stay in registers: one LDS read a step (the consumed side's next key,
+    // from a selected address) and no branches around the comparison -- the step read both heads and
+    // then the taken one again, under two nested exec masks
+    Key<L> ha = s_r[min(i, (uint32_t)CAP - 1)], hc = s_c[min(j, (uint32_t)CAP - 1)];
     for (uint32_t o = o0; o < o1; ++o) {
-        const bool take_r = i < nr && (j >= nc || s_r[i] < s_c[j]);
-        const Key<L> key = take_r ? s_r[i] : s_c[j];
+        const bool take_r = (i < nr) & ((j >= nc) | (ha < hc));  // (no short-circuit: no exec mask)
+        const Key<L> key = take_r ? ha : hc;
         out[base + o] = key;
-        if (COUNTED) outc[base + o] = take_r ? s_rv[i] : s_cv[j];
-        if (take_r) ++i; else ++j;
+        if (COUNTED) outc[base + o] = *(take_r ? s_rv + i : s_cv + j);
+        i += take_r ? 1u : 0u;
+        j += take_r ? 0u : 1u;
+        const Key<L> nx = *(take_r ? s_r + min(i, (uint32_t)CAP - 1) : s_c + min(j, (uint32_t)CAP - 1));
+        ha = take_r ? nx : ha;
+        hc = take_r ? hc : nx;
         if (istart) {
             const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
             uint32_t q = NGAP;
