@@ -2927,7 +2927,43 @@ struct Dist {
     uint64_t nb;      // 4^m prefixes
     EventTimer *tm;
     std::vector<std::pair<int, int>> xev;  // event pairs around exchanges
+    uint32_t coresident = 1;  // ranks on this rank's GPU (dist_coresident), the HBM they share
 };
+
+// the ranks that share this rank's GPU (threads of one process on its device, or several processes
+// on one card): an all-gather of a hash of the device's PCI bus id.  The rounds planners give each
+// of them an equal share of the free HBM -- each planning for the whole free memory over-committed
+// it (8 co-resident ranks of the round-4 simulation ran out of memory)
+static uint32_t dist_coresident(Ctx &c, Dist &d) {
+    if (d.P <= 1) return 1;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        snprintf(bus, sizeof(bus), "device %d", dev);
+    }
+    uint64_t h = 1469598103934665603ull;  // FNV-1a
+    for (const char *q = bus; *q; ++q) h = (h ^ (uint8_t)*q) * 1099511628211ull;
+    uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, (1 + (uint64_t)d.P) * 8);
+    HIP_CHECK(hipMemcpyAsync(dv, &h, 8, hipMemcpyHostToDevice, c.stream));
+    d.comm.allgather_u64(dv, dv + 1, 1, c.stream);
+    std::vector<uint64_t> all(d.P);
+    HIP_CHECK(hipMemcpyAsync(all.data(), dv + 1, (uint64_t)d.P * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // `h` is a host local
+    uint32_t n = 0;
+    for (uint64_t v : all) n += v == h;
+    return std::max<uint32_t>(n, 1);
+}
+
+// a rank's HBM budget for planning its rounds: memory_preallocated, else its share of the free HBM
+// (the ranks on its GPU split it) plus what its workspace holds
+static double dist_budget(const Ctx &c, const Dist &d) {
+    if (c.mem_budget > 0) return c.mem_budget;
+    size_t fr = 0, tot = 0;
+    HIP_CHECK(hipMemGetInfo(&fr, &tot));
+    return 0.9 * ((double)fr / (double)std::max<uint32_t>(d.coresident, 1) + (double)c.ws.held());
+}
 
 // prefix index of a sorted 2-bit array: start[p] = first key with prefix >= p, p in [0, nb]
 template <int L2>
@@ -3086,12 +3122,7 @@ static uint32_t plan_rounds_dist(Ctx &c, Dist &d, unsigned K, bool canonical, co
         want = c.force_ranges;
     } else if (can) {
         const double per_key = (double)sizeof(Key<L2>) + (COUNTED ? 4.0 : 0.0);
-        double budget = c.mem_budget;
-        if (budget <= 0) {
-            size_t fr = 0, tot = 0;
-            HIP_CHECK(hipMemGetInfo(&fr, &tot));
-            budget = 0.9 * ((double)fr + (double)c.ws.held());
-        }
+        const double budget = dist_budget(c, d);
         // single pass: KA + KB over every window, the exchange buffers and the owned real edges
         if ((double)npos * per_key * 3.0 > budget || c.disk) {
             const double keys = (double)npos * (canonical ? 2.0 : 1.0);
@@ -3377,12 +3408,7 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     {
         uint64_t want = c.force_ranges;
         if (!want) {
-            double budget = c.mem_budget;
-            if (budget <= 0) {
-                size_t fr = 0, tot = 0;
-                HIP_CHECK(hipMemGetInfo(&fr, &tot));
-                budget = 0.9 * ((double)fr + (double)c.ws.held());
-            }
+            const double budget = dist_budget(c, d);
             const double per_key = 8.0 + (COUNTED ? 4.0 : 0.0);
             // one pass: the rank's keys, the received runs and their ping-pong buffer, plus ~3 N of later
             // stages (the owned canonical set, its rc keys, the real edges) at low duplication
@@ -3705,6 +3731,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     Dist d{comm, comm.size(), comm.rank(), 0, 0, 1, &tm, {}};
     const uint64_t sent0 = comm.sent_bytes;
     if (d.P > MAX_RANKS) throw std::runtime_error("more ranks than the routing kernels support");
+    d.coresident = dist_coresident(c, d);
     T.world = (uint64_t)d.P;
     T.n_batches = 1;
     // ranges on the top m node chars, m <= k - 1 keeps every emission group inside one rank
