@@ -1809,6 +1809,74 @@ __global__ void dummy_bitmap_ranks_kernel(const uint32_t *__restrict__ bitmap, u
     }
 }
 
+// the inverse of an odd a modulo 2^64 / 2^128 (Newton: every step doubles the correct low bits)
+template <typename R>
+__host__ __device__ constexpr R inv_odd(R a) {
+    R x = a;  // a * a = 1 mod 8 for odd a
+    for (int i = 0; i < 7; ++i) x *= (R)2 - a * x;
+    return x;
+}
+
+// 21 2-bit digits (bits 2d, 2d + 1) spread to 3-bit slots (bits 3d, 3d + 1): five mask-and-shift steps,
+// the units whose index has bit s set moving up 2^s places, highest s first (so no unit passes another)
+struct SpreadMasks {
+    uint64_t m[5];
+};
+__host__ __device__ constexpr SpreadMasks make_spread_masks() {
+    SpreadMasks r{};
+    int pos[21] = {};
+    for (int d = 0; d < 21; ++d) pos[d] = 2 * d;
+    for (int s = 4, i = 0; s >= 0; --s, ++i) {
+        uint64_t mk = 0;
+        for (int d = 0; d < 21; ++d)
+            if ((d >> s) & 1) {
+                mk |= 3ull << pos[d];
+                pos[d] += 1 << s;
+            }
+        r.m[i] = mk;
+    }
+    return r;
+}
+__device__ __forceinline__ uint64_t spread21(uint64_t x) {
+    constexpr SpreadMasks M = make_spread_masks();
+#pragma unroll
+    for (int i = 0; i < 5; ++i) x = (x & ~M.m[i]) | ((x & M.m[i]) << (16 >> i));
+    return x;
+}
+
+// The rank of a source dummy with m <= k - 5 real chars inverted in closed form: 3 r = 12 m + 7 W - 4 S + 3 c
+// with 7 W a multiple of 4^(k - m) >= 2^10 and 0 <= 12 m - 4 S + 3 c < 2^10, so the low 10 bits of 3 r are
+// eps = 12 m - 4 S + 3 c, W = (3 r - eps) / 7 (exact: times the inverse of 7), S = the digit sum of W, and
+// eps + 4 S = 12 m + 3 c gives m and c.  A candidate whose digits lie in [k - m, k) has rank r, so it is
+// the dummy (the rank is a bijection); anything else (sinks, the last 4 source levels) returns false and
+// takes the char-by-char walk.  Writes the lifted key: real char p (digit k - p of W) + 1 at char slot
+// k - p + 1, the label c + 1 at slot 0.
+template <int L3, typename R>
+__device__ __forceinline__ bool dummy_decode_fast(R r, unsigned k, Key<L3> &out) {
+    constexpr R INV7 = inv_odd<R>((R)7);
+    const R V = r * (R)3;
+    const uint32_t eps = (uint32_t)V & 1023u;
+    const R W = (V - (R)eps) * INV7;
+    const uint32_t t = eps + 4u * (uint32_t)char_sum2(W);
+    const uint32_t m = t / 12u, c = (t % 12u) / 3u;
+    if (t % 3u || m + 5 > k || (W >> (2 * k)) != 0) return false;
+    const unsigned lo = k - m;  // the lowest real digit
+    if ((W & (((R)1 << (2 * lo)) - 1)) != 0) return false;
+    constexpr uint64_t ONES = 0x1249249249249249ull & ((1ull << 63) - 1);  // 001 in every 3-bit slot
+    Key<L3> x = Key<L3>::from((uint64_t)(c + 1));
+#pragma unroll
+    for (int pi = 0; pi < 3; ++pi) {
+        const unsigned d0 = 21u * pi;  // digits d0 .. d0 + 20
+        if (d0 >= k || 63 * pi + 3 >= 64 * L3) break;
+        const uint64_t chunk = (uint64_t)(W >> (2 * d0)) & ((1ull << 42) - 1);
+        const unsigned a = lo > d0 ? lo - d0 : 0u, b = k - d0 < 21u ? k - d0 : 21u;  // valid digits [a, b)
+        const uint64_t ones = a < b ? (ONES & ((b == 21u ? ~0ull : (1ull << (3 * b)) - 1)) & ~((1ull << (3 * a)) - 1)) : 0ull;
+        x = x | shl(Key<L3>::from(spread21(chunk) + ones), 63 * pi + 3);
+    }
+    out = x;
+    return true;
+}
+
 template <int L3, int LR = 1>
 __global__ void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n, unsigned k, Key<L3> *__restrict__ out) {
     using R = RankWord<LR>;
@@ -1816,6 +1884,13 @@ __global__ void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n, 
     const R T0 = dummy_rank_space_t<R>(k);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
         R r = rank_word<LR>(in[i]), T = T0;
+        {
+            Key<L3> f;
+            if (dummy_decode_fast<L3, R>(r, k, f)) {  // (round 5: 61 -> ? ms at configs[2])
+                out[i] = f;
+                continue;
+            }
+        }
         // the real chars r_1, r_2, ... enter at the bottom of x one by one (r_p ends up at node
         // position k - p + 1); then one shift leaves the $ run and the label below them
         Key<L3> x = Key<L3>::zero();

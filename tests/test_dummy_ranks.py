@@ -139,3 +139,69 @@ def test_source_bitmap_index_is_the_rank(k):
                 S = sum((low >> (2 * i)) & 3 for i in range(m))
                 assert 4 * m + (7 * W - 4 * S) // 3 + (r & 3) == encode(x, k)
     assert len(seen) == bitmap_base(ms)
+
+
+def _spread21(x):
+    # dummy_decode_fast's spread21: 21 2-bit digits to 3-bit slots by five mask-and-shift steps
+    pos = [2 * d for d in range(21)]
+    for s in range(4, -1, -1):
+        mk = 0
+        for d in range(21):
+            if (d >> s) & 1:
+                mk |= 3 << pos[d]
+                pos[d] += 1 << s
+        x = (x & ~mk) | ((x & mk) << (1 << s))
+    return x
+
+
+def decode_closed_form(r, k, bits):
+    """boss_kernels.hpp: dummy_decode_fast -- 3 r = 12 m + 7 W - 4 S + 3 c inverted through the low 10
+    bits of 3 r (mod 2^bits, the device's u64 / u128 word); None where the kernel walks char by char."""
+    M = (1 << bits) - 1
+    V = (3 * r) & M
+    eps = V & 1023
+    W = ((V - eps) * pow(7, -1, 1 << bits)) & M
+    t = eps + 4 * sum((W >> (2 * j)) & 3 for j in range(bits // 2))
+    m, c = t // 12, (t % 12) // 3
+    if t % 3 or m + 5 > k or W >> (2 * k):
+        return None
+    lo = k - m
+    if W & ((1 << (2 * lo)) - 1):
+        return None
+    ones = 0x1249249249249249
+    x = c + 1
+    for pi in range(3):
+        d0 = 21 * pi
+        if d0 >= k:
+            break
+        a, b = max(lo - d0, 0), min(k - d0, 21)
+        o = (ones & ((1 << (3 * b)) - 1) & ~((1 << (3 * a)) - 1)) if a < b else 0
+        x |= (_spread21((W >> (2 * d0)) & ((1 << 42) - 1)) + o) << (63 * pi + 3)
+    return x
+
+
+@pytest.mark.parametrize("k", [5, 6, 7])
+def test_closed_form_decode_every_dummy(k):
+    # every dummy of a small k: the closed form returns the walk's key or defers to it (sinks and the
+    # last 4 source levels only)
+    for x in dummies(k):
+        r = encode(x, k)
+        got = decode_closed_form(r, k, 64)
+        m = sum(1 for j in range(1, k + 1) if (x >> (3 * j)) & 7)
+        if got is None:
+            assert m > k - 5, (k, x)
+        else:
+            assert got == x == decode(r, k)
+
+
+@pytest.mark.parametrize("k,bits", [(30, 64), (31, 128), (47, 128), (62, 128)])
+def test_closed_form_decode_random_sources(k, bits):
+    # random source dummies at the widths the device decodes (u64 ranks to k = 30, u128 to k = 62)
+    import random
+    rng = random.Random(k)
+    for _ in range(3000):
+        m = rng.randint(0, k - 1)
+        node = [rng.randint(1, 4) for _ in range(m)] + [0] * (k - m)
+        x = lifted(node, rng.randint(1, 4), k)
+        got = decode_closed_form(encode(x, k), k, bits)
+        assert got == x if m <= k - 5 else got is None
