@@ -1353,14 +1353,78 @@ __global__ __launch_bounds__(256) void merge_kernel(const Key<LA> *__restrict__ 
  * that matched so far is bigger (lifted chars are >= 1).  So X = b's chars - 1 above that $,
  * zeros from it down.
  */
+// 21 2-bit digits (bits 2d, 2d + 1) spread to 3-bit slots (bits 3d, 3d + 1): five mask-and-shift steps,
+// the units whose index has bit s set moving up 2^s places, highest s first (so no unit passes another)
+struct SpreadMasks {
+    uint64_t m[5];
+};
+__host__ __device__ constexpr SpreadMasks make_spread_masks() {
+    SpreadMasks r{};
+    int pos[21] = {};
+    for (int d = 0; d < 21; ++d) pos[d] = 2 * d;
+    for (int s = 4, i = 0; s >= 0; --s, ++i) {
+        uint64_t mk = 0;
+        for (int d = 0; d < 21; ++d)
+            if ((d >> s) & 1) {
+                mk |= 3ull << pos[d];
+                pos[d] += 1 << s;
+            }
+        r.m[i] = mk;
+    }
+    return r;
+}
+// the same units at their positions after each spread step (compress21 runs the steps backwards)
+__host__ __device__ constexpr SpreadMasks make_compress_masks() {
+    SpreadMasks r{};
+    int pos[21] = {};
+    for (int d = 0; d < 21; ++d) pos[d] = 2 * d;
+    for (int s = 4, i = 0; s >= 0; --s, ++i) {
+        uint64_t mk = 0;
+        for (int d = 0; d < 21; ++d)
+            if ((d >> s) & 1) {
+                pos[d] += 1 << s;
+                mk |= 3ull << pos[d];
+            }
+        r.m[i] = mk;
+    }
+    return r;
+}
+// 21 values in 3-bit slots (low 2 bits each) packed to 2-bit digits: spread21 inverted
+__device__ __forceinline__ uint64_t compress21(uint64_t x) {
+    constexpr SpreadMasks M = make_compress_masks();
+#pragma unroll
+    for (int i = 4; i >= 0; --i) x = (x & ~M.m[i]) | ((x & M.m[i]) >> (16 >> i));
+    return x;
+}
+__device__ __forceinline__ uint64_t spread21(uint64_t x) {
+    constexpr SpreadMasks M = make_spread_masks();
+#pragma unroll
+    for (int i = 0; i < 5; ++i) x = (x & ~M.m[i]) | ((x & M.m[i]) << (16 >> i));
+    return x;
+}
+
 template <int L2, int L3>
 __device__ __forceinline__ Key<L2> unlift_floor(const Key<L3> &b, unsigned K) {
+    // (round 5) by 21-slot pieces instead of char by char: every slot minus 1 (a $ stays 0), packed to
+    // 2-bit digits (compress21), then the digits at and below the highest $ slot cleared -- the walk
+    // cost one 3-bit extract and one shifted OR of a K-char key per char (configs[2]: 54 ms of
+    // dummy_rank_kernel for 6.6e8 dummies)
+    constexpr uint64_t ONES = 0x1249249249249249ull;  // 001 in every 3-bit slot (21 slots)
     Key<L2> x = Key<L2>::zero();
-    for (int i = (int)K - 1; i >= 0; --i) {
-        const uint32_t ch = char_at(b, (unsigned)i, 3);
-        if (ch == 0) break;
-        x = x | shl(Key<L2>::from(ch - 1), 2 * i);
+    int zs = -1;  // the highest $ slot
+#pragma unroll
+    for (int pi = 0; pi < 5; ++pi) {  // K <= 105 chars
+        const unsigned s0 = 21u * pi;
+        if (s0 >= K || 63 * pi >= 64 * L3) break;
+        const unsigned ns = K - s0 < 21u ? K - s0 : 21u;
+        const uint64_t vm = ns == 21u ? (1ull << 63) - 1 : (1ull << (3 * ns)) - 1;
+        const uint64_t v = shr(b, 63 * pi).w[0] & vm;
+        const uint64_t nz = (v | (v >> 1) | (v >> 2)) & ONES & vm;
+        const uint64_t z = ~nz & ONES & vm;
+        if (z) zs = (int)s0 + (63 - __clzll((long long)z)) / 3;
+        if (2 * s0 < 64 * L2) x = x | shl(Key<L2>::from(compress21(v - nz)), 2 * s0);
     }
+    if (zs >= 0) x = x & ~Key<L2>::lowmask(2 * (unsigned)(zs + 1));
     return x;
 }
 
@@ -1391,13 +1455,16 @@ __global__ __launch_bounds__(256) void dummy_rank_kernel(
     const Key<L3> node = shr(x, 3), grp = shr(x, 6);
     const uint32_t c = (uint32_t)(x.w[0] & 7);
     bool bad = false;
-    // the real edges of x's chars-2..k group sit next to r (at most 16: 4 first chars x 4 labels)
-    for (uint64_t i = r; i < na && i < r + 16; ++i) {
+    // the real edges of x's chars-2..k group sit next to r (at most 16: 4 first chars x 4 labels); a
+    // dummy with $ in char slot 2 (a source of level >= 2) has no real edge in its group: real edges
+    // have no $ (skipped: two lifted real edges a dummy)
+    const bool near = K < 3 || char_at(x, 2, 3) != 0;
+    for (uint64_t i = r; near && i < na && i < r + 16; ++i) {
         const Key<L3> y = lift_fast<L3>(a[i], K);
         if (shr(y, 6) != grp) break;
         bad |= shr(y, 3) == node || (c && (uint32_t)(y.w[0] & 7) == c);
     }
-    for (uint64_t i = r; i > 0 && i + 16 > r; --i) {
+    for (uint64_t i = r; near && i > 0 && i + 16 > r; --i) {
         const Key<L3> y = lift_fast<L3>(a[i - 1], K);
         if (shr(y, 6) != grp) break;
         bad |= shr(y, 3) == node || (c && (uint32_t)(y.w[0] & 7) == c);
@@ -1817,33 +1884,6 @@ __host__ __device__ constexpr R inv_odd(R a) {
     return x;
 }
 
-// 21 2-bit digits (bits 2d, 2d + 1) spread to 3-bit slots (bits 3d, 3d + 1): five mask-and-shift steps,
-// the units whose index has bit s set moving up 2^s places, highest s first (so no unit passes another)
-struct SpreadMasks {
-    uint64_t m[5];
-};
-__host__ __device__ constexpr SpreadMasks make_spread_masks() {
-    SpreadMasks r{};
-    int pos[21] = {};
-    for (int d = 0; d < 21; ++d) pos[d] = 2 * d;
-    for (int s = 4, i = 0; s >= 0; --s, ++i) {
-        uint64_t mk = 0;
-        for (int d = 0; d < 21; ++d)
-            if ((d >> s) & 1) {
-                mk |= 3ull << pos[d];
-                pos[d] += 1 << s;
-            }
-        r.m[i] = mk;
-    }
-    return r;
-}
-__device__ __forceinline__ uint64_t spread21(uint64_t x) {
-    constexpr SpreadMasks M = make_spread_masks();
-#pragma unroll
-    for (int i = 0; i < 5; ++i) x = (x & ~M.m[i]) | ((x & M.m[i]) << (16 >> i));
-    return x;
-}
-
 // The rank of a source dummy with m <= k - 5 real chars inverted in closed form: 3 r = 12 m + 7 W - 4 S + 3 c
 // with 7 W a multiple of 4^(k - m) >= 2^10 and 0 <= 12 m - 4 S + 3 c < 2^10, so the low 10 bits of 3 r are
 // eps = 12 m - 4 S + 3 c, W = (3 r - eps) / 7 (exact: times the inverse of 7), S = the digit sum of W, and
@@ -1877,38 +1917,73 @@ __device__ __forceinline__ bool dummy_decode_fast(R r, unsigned k, Key<L3> &out)
     return true;
 }
 
+// the char-by-char walk down the rank trie (any dummy: sinks, every source level)
+template <int L3, typename R>
+__device__ __forceinline__ Key<L3> dummy_decode_walk(R r, unsigned k, R T) {
+    // the real chars r_1, r_2, ... enter at the bottom of x one by one (r_p ends up at node
+    // position k - p + 1); then one shift leaves the $ run and the label below them
+    Key<L3> x = Key<L3>::zero();
+    unsigned m = 0;
+    uint64_t label = 0;  // $ for a sink
+    for (unsigned p = 1; p <= k; ++p) {
+        if (r < 4) {  // a source of level k - (p - 1): its label
+            label = (uint64_t)r + 1;
+            break;
+        }
+        r -= 4;
+        T = (T - 4) >> 2;  // T(p): strings below one real char at depth p
+        const R rp = (R)(r >= T) + (R)(r >= 2 * T) + (R)(r >= 3 * T);
+        r -= rp * T;
+        x = shl(x, 3) | Key<L3>::from((uint64_t)rp + 1);
+        ++m;
+    }
+    return shl(x, 3 * (k - m) + 3) | Key<L3>::from(label);
+}
+
+// Every block decodes a contiguous chunk of the dummies 256 at a time in closed form; the ones it
+// leaves (sinks, the last 4 source levels: ~8 % at configs[2]) go to an LDS list that the whole block
+// walks when it fills and at the chunk's end.  Walked where they lie, those few lanes held nearly every
+// wave in the walk's ~k-step loop (63 ms for 6.6e8 dummies at configs[2] with or without the closed
+// form), and a global list cost one atomic per wave on one counter (+58 ms).
 template <int L3, int LR = 1>
-__global__ void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n, unsigned k, Key<L3> *__restrict__ out) {
+__global__ __launch_bounds__(256) void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n, unsigned k,
+                                                           Key<L3> *__restrict__ out) {
     using R = RankWord<LR>;
-    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    constexpr uint32_t LCAP = 2048;
+    __shared__ uint32_t s_list[LCAP];
+    __shared__ uint32_t s_n;
     const R T0 = dummy_rank_space_t<R>(k);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-        R r = rank_word<LR>(in[i]), T = T0;
-        {
+    const uint64_t per = ((n + gridDim.x - 1) / gridDim.x + 255) & ~255ull;
+    const uint64_t c0 = (uint64_t)blockIdx.x * per, c1 = min(n, c0 + per);
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    for (uint64_t base = c0; base < c1; base += 256) {
+        const uint64_t i = base + threadIdx.x;
+        bool walk = false;
+        if (i < c1) {
             Key<L3> f;
-            if (dummy_decode_fast<L3, R>(r, k, f)) {  // (round 5: 61 -> ? ms at configs[2])
-                out[i] = f;
-                continue;
-            }
+            if (dummy_decode_fast<L3, R>(rank_word<LR>(in[i]), k, f)) out[i] = f;
+            else walk = true;
         }
-        // the real chars r_1, r_2, ... enter at the bottom of x one by one (r_p ends up at node
-        // position k - p + 1); then one shift leaves the $ run and the label below them
-        Key<L3> x = Key<L3>::zero();
-        unsigned m = 0;
-        uint64_t label = 0;  // $ for a sink
-        for (unsigned p = 1; p <= k; ++p) {
-            if (r < 4) {  // a source of level k - (p - 1): its label
-                label = (uint64_t)r + 1;
-                break;
-            }
-            r -= 4;
-            T = (T - 4) >> 2;  // T(p): strings below one real char at depth p
-            const R rp = (R)(r >= T) + (R)(r >= 2 * T) + (R)(r >= 3 * T);
-            r -= rp * T;
-            x = shl(x, 3) | Key<L3>::from((uint64_t)rp + 1);
-            ++m;
+        const uint64_t bal = __ballot(walk);
+        if (bal) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)bal) - 1;
+            uint32_t pos = 0;
+            if (__lane_id() == leader) pos = atomicAdd(&s_n, (uint32_t)__popcll(bal));
+            pos = __shfl(pos, leader, 64);
+            if (walk) s_list[pos + popc_below(bal)] = (uint32_t)(i - c0);
         }
-        out[i] = shl(x, 3 * (k - m) + 3) | Key<L3>::from(label);
+        __syncthreads();
+        const uint32_t cnt = s_n;
+        if (cnt > LCAP - 256 || base + 256 >= c1) {  // (block-uniform: read after the barrier)
+            for (uint32_t j = threadIdx.x; j < cnt; j += 256) {
+                const uint64_t x = c0 + s_list[j];
+                out[x] = dummy_decode_walk<L3, R>(rank_word<LR>(in[x]), k, T0);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) s_n = 0;
+            __syncthreads();
+        }
     }
 }
 

@@ -2433,6 +2433,7 @@ static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3
     HIP_CHECK(hipGetLastError());
     const uint64_t D = read_u64(c, &c.small->total);
     Key<L3> *outk = (void *)rb == (void *)xa ? xb : xa;
+    // (a block per 256 dummies up to 16384 blocks, each a contiguous chunk)
     dummy_decode_kernel<L3, LR><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
                                   dim3(256), 0, c.stream>>>(rb, D, kb, outk);
     HIP_CHECK(hipGetLastError());
