@@ -159,8 +159,9 @@ const char *mtg_last_error(void);
 mtg_boss_ctor *mtg_boss_ctor_create(const mtg_boss_params *params);
 void mtg_boss_ctor_destroy(mtg_boss_ctor *ctor);
 uint64_t mtg_boss_ctor_get_k(const mtg_boss_ctor *ctor);
-/* frees the device blocks the constructor's workspace keeps idle between builds (timings'
-   cached_bytes); a build also frees, when it ends, the kept blocks it did not reuse */
+/* frees the device memory the constructor holds between builds: the blocks its workspace keeps idle
+   (timings' cached_bytes) and the last build's stage buffers; the last build's device chunk arrays
+   (W, last, weights) stay valid.  A build also frees, when it ends, the kept blocks it did not reuse */
 int mtg_boss_ctor_trim(mtg_boss_ctor *ctor);
 
 /* n sequences, seqs[i] of lens[i] bytes, counts[i] (NULL = all 1).  Copies the input. */

@@ -442,7 +442,8 @@ class BOSSChunkConstructor:
         return t
 
     def trim(self):
-        """Free the device blocks the workspace keeps idle between builds (mtg_boss_ctor_trim)."""
+        """Free the device memory held between builds -- idle workspace blocks and the last build's stage
+        buffers; its device chunk arrays stay valid (mtg_boss_ctor_trim)."""
         _check(lib().mtg_boss_ctor_trim(self._h))
 
 

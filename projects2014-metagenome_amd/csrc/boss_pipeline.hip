@@ -133,12 +133,13 @@ class Workspace {
     }
     // the buffers a build's sort, rc, dummy and emit stages hold (not its input, look-back descriptors
     // or pass-A histograms): a build in rounds frees the previous build's before sizing its rounds
-    void release_stage_buffers() {
+    void release_stage_buffers(bool keep_outputs = false) {
+        // keep_outputs (mtg_boss_ctor_trim): the last build's device chunk arrays (W, last, weights) stay
         for (Slot sl : {KA, KB, CA, CB, SUMS, BUCKETS, FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, FB_K, FB_V,
                         RC_ALT, RC_ALTC, REAL, REALC, INFLAG, XA, XAC, XB, XBC, QSEND, QRECV, QFLAG, DSRC, DSEND,
                         DRECV, RC_SENDC, LAST_BITS, W4, WN, DPOS, DWL, CANON, CANONC, CANON_IDX, SPEC_A, SPEC_B,
                         SPEC_AC, SPEC_BC, KA2})
-            release(sl);
+            if (!keep_outputs || (sl != OW && sl != OLAST && sl != OWEIGHTS)) release(sl);
     }
     // a slot gives its buffer back (batched builds drop their round buffers before the later stages
     // grow).  The block is kept for the next get() of about its size rather than freed: freeing and
@@ -4916,6 +4917,12 @@ int mtg_boss_ctor_trim(mtg_boss_ctor *c) {
     std::lock_guard<std::mutex> lock(c->mu);
     try {
         HIP_CHECK(hipSetDevice(c->device));
+        // the last build's stage buffers too (its device chunk arrays stay valid): a configs[2] build
+        // holds ~200 GB in them, and a second constructor in the same process had 110 MiB left
+        c->ctx.ws.release_stage_buffers(true);
+        note_bucket_index(c->ctx, nullptr, 0, nullptr, 0);
+        c->ctx.gap.valid = false;
+        c->ctx.gidx = Ctx::GroupIndex{};
         c->ctx.ws.drop_cache();
         c->ctx.timings.cached_bytes = 0;
         return MTG_OK;
