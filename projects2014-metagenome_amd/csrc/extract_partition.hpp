@@ -323,18 +323,19 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
     __syncthreads();  // every count is read before the offsets overwrite them
+    // (the run reservations stay in flight across the LDS scatter, as in extract_partition_fast_kernel)
+    unsigned long long gq[PER], be[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
+        gq[q] = 0, be[q] = 0;
         if (i < nb) {
             s_cnt[i] = off;
             const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
-            unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
-            if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
-                atomicOr(error, 2u);            // write past its range (the host raises)
-                g = ~0ull;
+            if (c[q]) {
+                gq[q] = atomicAdd(&cursor[ci], (unsigned long long)c[q]);
+                be[q] = bend[ci];
             }
-            s_gbase[i] = g;
         }
         off += c[q];
     }
@@ -345,6 +346,18 @@ __global__ __launch_bounds__(BLOCK_) void extract_partition_kernel(
             const uint32_t pos = s_cnt[key_prefix(kk[j], 2 * K, b)] + r[j];
             s_keys[pos] = kk[j];
             if (COUNTED) s_vals[pos] = cc[j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nb) {
+            unsigned long long g = gq[q];
+            if (c[q] && g + c[q] > be[q]) {  // pass A counted this bucket differently: never
+                atomicOr(error, 2u);          // write past its range (the host raises)
+                g = ~0ull;
+            }
+            s_gbase[i] = g;
         }
     }
     __syncthreads();
@@ -487,20 +500,20 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
     __syncthreads();  // every count is read before the run bases overwrite them
+    // (round 5) the run reservations are issued here and consumed after the LDS scatter below, so their
+    // round trip to the cursors overlaps the scatter instead of stalling the workgroup before it
+    unsigned long long gq[PER], be[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
+        gq[q] = 0, be[q] = 0;
         if (i < nb) {
             s_off[i] = (uint16_t)off;
             const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
-            unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
-            if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
-                atomicOr(povf ? povf : error, povf ? 1u : 2u);  // write past its range
-                g = ~0ull;
-            } else if (bdelta) {
-                g += (unsigned long long)bdelta[i];
+            if (c[q]) {
+                gq[q] = atomicAdd(&cursor[ci], (unsigned long long)c[q]);
+                be[q] = bend[ci];
             }
-            s_gbase[i] = g;
         }
         off += c[q];
     }
@@ -508,6 +521,20 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
 #pragma unroll
     for (int j = 0; j < PPT; ++j)
         if (m & (1u << j)) s_keys[s_off[(uint32_t)(kk[j] >> bshift)] + r[j]] = kk[j];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nb) {
+            unsigned long long g = gq[q];
+            if (c[q] && g + c[q] > be[q]) {  // pass A counted this bucket differently: never
+                atomicOr(povf ? povf : error, povf ? 1u : 2u);  // write past its range
+                g = ~0ull;
+            } else if (bdelta) {
+                g += (unsigned long long)bdelta[i];
+            }
+            s_gbase[i] = g;
+        }
+    }
     __syncthreads();
     for (uint32_t p = tid; p < total; p += BLOCK) {
         const uint64_t key = s_keys[p];
@@ -636,18 +663,19 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
     __syncthreads();  // every count is read before the run bases overwrite them
+    // (the run reservations stay in flight across the LDS scatter, as in extract_partition_fast_kernel)
+    unsigned long long gq[PER], be[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
+        gq[q] = 0, be[q] = 0;
         if (i < nb) {
             s_off[i] = (uint16_t)off;
             const size_t ci = (size_t)(tile / per_stripe) * nb + i;  // this tile's stripe
-            unsigned long long g = c[q] ? atomicAdd(&cursor[ci], (unsigned long long)c[q]) : 0;
-            if (c[q] && g + c[q] > bend[ci]) {  // pass A counted this bucket differently: never
-                atomicOr(error, 2u);            // write past its range
-                g = ~0ull;
+            if (c[q]) {
+                gq[q] = atomicAdd(&cursor[ci], (unsigned long long)c[q]);
+                be[q] = bend[ci];
             }
-            s_gbase[i] = g;
         }
         off += c[q];
     }
@@ -655,6 +683,18 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
 #pragma unroll
     for (int j = 0; j < PPT; ++j)
         if (m & (1u << j)) s_keys[s_off[digit(kk[j])] + r[j]] = kk[j];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < nb) {
+            unsigned long long g = gq[q];
+            if (c[q] && g + c[q] > be[q]) {  // pass A counted this bucket differently: never
+                atomicOr(error, 2u);          // write past its range
+                g = ~0ull;
+            }
+            s_gbase[i] = g;
+        }
+    }
     __syncthreads();
     for (uint32_t p = tid; p < total; p += BLOCK) {
         const ulonglong2 key = s_keys[p];

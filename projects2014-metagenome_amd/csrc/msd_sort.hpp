@@ -311,17 +311,19 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
     }
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+    // (round 5) the run reservations are issued here and consumed after the LDS scatter below, so their
+    // round trip to the cursors overlaps the scatter
+    unsigned long long gq[PER], be[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
+        gq[q] = 0, be[q] = 0;
         if (i < wsize) {
             s_loff[i] = off;
-            unsigned long long gb = c[q] ? atomicAdd(&cursor[(size_t)(wbase + i) * cstride], (unsigned long long)c[q]) : 0;
-            if (bend && c[q] && gb + c[q] > bend[wbase + i]) {
-                *povf = 1u;
-                gb = ~0ull;  // this run is not written
+            if (c[q]) {
+                gq[q] = atomicAdd(&cursor[(size_t)(wbase + i) * cstride], (unsigned long long)c[q]);
+                if (bend) be[q] = bend[wbase + i];
             }
-            s_gbase[i] = gb;
         }
         off += c[q];
     }
@@ -333,6 +335,18 @@ __global__ __launch_bounds__(BLOCK) void msd_partition_kernel(
             const uint32_t pos = s_loff[lb] + r[j];
             s_keys[pos] = k[j];
             if (HAS_VAL) s_vals[pos] = v[j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid * PER + q;
+        if (i < wsize) {
+            unsigned long long gb = gq[q];
+            if (bend && c[q] && gb + c[q] > be[q]) {
+                *povf = 1u;
+                gb = ~0ull;  // this run is not written
+            }
+            s_gbase[i] = gb;
         }
     }
     __syncthreads();
