@@ -641,12 +641,15 @@ __global__ __launch_bounds__(512) void rc_partition_gapped_kernel(
     }
     uint32_t total;
     uint32_t off = block_exclusive_sum<BLOCK>(sum, s_scan, &total);
+    // (the run reservations stay in flight across the LDS scatter, as in the partition passes)
+    unsigned long long gq[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid * PER + q;
+        gq[q] = 0;
         if (i < nbk) {
             s_loff[i] = off;
-            s_gbase[i] = c[q] ? atomicAdd(&cursor[i], (unsigned long long)c[q]) : 0;
+            if (c[q]) gq[q] = atomicAdd(&cursor[i], (unsigned long long)c[q]);
         }
         off += c[q];
     }
@@ -654,6 +657,9 @@ __global__ __launch_bounds__(512) void rc_partition_gapped_kernel(
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
         if (r[j] != 0xFFFFFFFFu) s_keys[s_loff[bits_at(k[j], 2 * K - hb, hb)] + r[j]] = k[j];
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if (tid * PER + q < nbk) s_gbase[tid * PER + q] = gq[q];
     __syncthreads();
     for (uint32_t q = tid; q < total; q += BLOCK) {
         const Key<L> key = s_keys[q];
@@ -803,7 +809,7 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
     const Key<L> m3 = Key<L>::from(3);
     uint8_t *s_hitb = reinterpret_cast<uint8_t *>(s_hit);
 
-    if (tid < 4) {
+    if (L != 1 && tid < 4) {
         // key range of the sink probes of label c = tid, read off the bucket index
         const Key<L> c = shl(Key<L>::from(tid), 2 * (K - 1));
         const Key<L> lo = (shr(keys[base], 2) | c) & ~m3;
@@ -840,6 +846,48 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
             }
         }
     }
+    if constexpr (L == 1) {
+        // (round 5) wave w finds and stages label class w on its own, into its quarter of s_r: no block-wide
+        // pass over the four range sizes and two barriers fewer before the search (a class over a quarter,
+        // ~5e-4 of them at configs[1], takes the global searches)
+        constexpr uint32_t QC = T::CAP / 4;
+        const uint32_t w = tid >> 6, lane = tid & 63;
+        uint32_t alo = 0, ahi = 0, cnt = 0;
+        if (lane == 0) {
+            const Key<L> c = shl(Key<L>::from(w), 2 * (K - 1));
+            const Key<L> lo = (shr(keys[base], 2) | c) & ~m3;
+            const Key<L> hi = shr(keys[base + tn - 1], 2) | c | m3;
+            const uint64_t blo = bits_at(shr(lo, bshift), 0, 32), bhi = bits_at(shr(hi, bshift), 0, 32);
+            const uint64_t a = start[blo], b = start[bhi + 1];
+            alo = (uint32_t)a, ahi = (uint32_t)(a >> 32);
+            cnt = (uint32_t)min(b - a, (uint64_t)0xFFFFFFFFu);
+        }
+        const uint64_t a = (uint64_t)__shfl(alo, 0, 64) | ((uint64_t)__shfl(ahi, 0, 64) << 32);
+        cnt = __shfl(cnt, 0, 64);
+        const uint32_t off = cnt <= QC ? w * QC : ~0u;
+        if (lane == 0) {
+            s_lo[w] = a;
+            s_cnt[w] = cnt;
+            s_off[w] = off;
+        }
+        if (off != ~0u && !(ABL & 4)) {
+            if ((((uintptr_t)look) & 15) == 0) {
+                const uint64_t a0 = a & ~1ull, e = a + cnt;
+                for (uint64_t i = a0 + 2ull * lane; i < e; i += 128) {
+                    if (i + 1 < nl) {  // (never past the array's last key)
+                        const ulonglong2 v = *(const ulonglong2 *)(look + i);
+                        if (i >= a) s_r[off + (uint32_t)(i - a)] = Key<L>::from(v.x);
+                        if (i + 1 < e) s_r[off + (uint32_t)(i + 1 - a)] = Key<L>::from(v.y);
+                    } else if (i >= a) {
+                        s_r[off + (uint32_t)(i - a)] = look[i];
+                    }
+                }
+            } else {
+                for (uint32_t j = lane; j < cnt; j += 64) s_r[off + j] = look[a + j];
+            }
+        }
+        __syncthreads();
+    } else {
     __syncthreads();
     if (tid == 0) {
         uint32_t cum = 0;
@@ -877,6 +925,7 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         for (uint32_t j = tid; j < cnt; j += 256) s_r[off + j] = look[a + j];
     }
     __syncthreads();
+    }
     uint32_t fw = 0;  // this thread's flag bytes, byte q = edge j0 + q
 #pragma unroll
     for (int q2 = 0; q2 < PER; ++q2) {
