@@ -1157,7 +1157,6 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     __shared__ Key<L> s_c[CAP];  // canonical keys of the range
     __shared__ uint32_t s_rv[COUNTED ? CAP : 1], s_sv[COUNTED ? CAP : 1], s_cv[COUNTED ? CAP : 1];
     __shared__ uint32_t s_hist[256], s_fill[256];
-    __shared__ int s_hb;
     // index gaps longer than IGAP entries between two consecutive outputs, filled by the whole workgroup
     // after the merge (a thread filling them alone serialized groups that span many sparse buckets: an
     // 8-rank super-k-mer build's rc merge took 0.1-0.8 s per launch)
@@ -1187,9 +1186,20 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         }
         return;
     }
-    for (uint32_t i = tid; i < nr; i += LB) {
-        s_r[i] = keys[g0 + i];
-        if (COUNTED) s_rv[i] = vals[g0 + i];
+    // (round 5) the group's rc keys stay in registers until their counting sort scatters them (no raw copy
+    // in LDS, one barrier fewer); the wave maxima of their highest differing bit go to per-wave words
+    constexpr int PR = (CAP + LB - 1) / LB;
+    constexpr int NWV = LB / 64;
+    __shared__ int s_wmax[NWV];
+    Key<L> rk[PR];
+    uint32_t rv[PR];
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        const uint32_t i = tid + q * LB;
+        if (i < nr) {
+            rk[q] = keys[g0 + i];
+            if (COUNTED) rv[q] = vals[g0 + i];
+        }
     }
     const uint64_t cr = cgap ? cgap[gb0] : c0;
     for (uint32_t i = tid; i < nc; i += LB) {
@@ -1200,26 +1210,33 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         s_hist[tid] = 0;
         s_fill[tid] = 0;
     }
-    if (tid == 0) {
-        s_hb = -1;
-        s_gn = 0;
-    }
-    __syncthreads();
-    if (nr) {
-        const Key<L> ref = s_r[0];
+    if (tid == 0) s_gn = 0;
+    {
         int hb_local = -1;
-        for (uint32_t i = tid; i < nr; i += LB) {
-            Key<L> dx;
+        if (nr) {
+            const Key<L> ref = keys[g0];  // the same key for every lane
 #pragma unroll
-            for (int w = 0; w < L; ++w) dx.w[w] = s_r[i].w[w] ^ ref.w[w];
-            hb_local = max(hb_local, key_msb(dx));
+            for (int q = 0; q < PR; ++q) {
+                if (tid + q * LB < nr) {
+                    Key<L> dx;
+#pragma unroll
+                    for (int w = 0; w < L; ++w) dx.w[w] = rk[q].w[w] ^ ref.w[w];
+                    hb_local = max(hb_local, key_msb(dx));
+                }
+            }
         }
-        wave_atomic_max(&s_hb, hb_local);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) hb_local = max(hb_local, __shfl_xor(hb_local, o, 64));
+        if (__lane_id() == 0) s_wmax[tid >> 6] = hb_local;
     }
     __syncthreads();
-    const int hb = s_hb;
+    int hb = -1;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) hb = max(hb, s_wmax[w]);
     const unsigned dshift = hb >= 7 ? (unsigned)(hb - 7) : 0u;
-    for (uint32_t i = tid; i < nr; i += LB) atomicAdd(&s_hist[bits_at(s_r[i], dshift, 8)], 1u);
+#pragma unroll
+    for (int q = 0; q < PR; ++q)
+        if (tid + q * LB < nr) atomicAdd(&s_hist[bits_at(rk[q], dshift, 8)], 1u);
     __syncthreads();
     if (tid < 64) {
         const uint32_t a0 = s_hist[4 * tid], a1 = s_hist[4 * tid + 1], a2 = s_hist[4 * tid + 2], a3 = s_hist[4 * tid + 3];
@@ -1231,11 +1248,14 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         s_hist[4 * tid + 3] = bb + a0 + a1 + a2;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < nr; i += LB) {
-        const uint32_t d = bits_at(s_r[i], dshift, 8);
-        const uint32_t p = s_hist[d] + atomicAdd(&s_fill[d], 1u);
-        s_s[p] = s_r[i];
-        if (COUNTED) s_sv[p] = s_rv[i];
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        if (tid + q * LB < nr) {
+            const uint32_t d = bits_at(rk[q], dshift, 8);
+            const uint32_t p = s_hist[d] + atomicAdd(&s_fill[d], 1u);
+            s_s[p] = rk[q];
+            if (COUNTED) s_sv[p] = rv[q];
+        }
     }
     __syncthreads();
     for (uint32_t p = tid; p < nr; p += LB) {
