@@ -580,6 +580,8 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
     }
 }
 
+__global__ void set_u64_kernel(uint64_t *p, uint64_t a) { *p = a; }
+
 __global__ void set_pair_kernel(uint64_t *p, uint64_t a, uint64_t b) {
     p[0] = a;
     p[1] = b;
@@ -862,8 +864,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
                 HIP_CHECK(hipGetLastError());
             }
             constexpr int CAP = MergeLocalTraits<L>::CAP;
-            uint32_t *gflag = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);
-            HIP_CHECK(hipMemsetAsync(gflag, 0, nb * 4, c.stream));
+            uint32_t *olist = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);  // the overflowing groups
             HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
             uint64_t *istart = rm->istart;
             // the canonical keys where they are: compact, or still in their own bucket layout (c.gap,
@@ -873,30 +874,24 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             const uint64_t *cgap = gapped ? c.gap.bstart : nullptr;
             bucket_pieces(0, nb, [&](uint64_t g0, unsigned cnt) {
                 local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
-                    sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                    sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, olist,
                     &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, g0, c.merge_it);
                 HIP_CHECK(hipGetLastError());
             });
             uint32_t novf = 0;
             HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
             HIP_CHECK(hipStreamSynchronize(c.stream));
-            if (novf) {  // the few big groups again with twice the LDS arrays
-                std::vector<uint32_t> fl(nb), list;
-                HIP_CHECK(hipMemcpyAsync(fl.data(), gflag, nb * 4, hipMemcpyDeviceToHost, c.stream));
-                HIP_CHECK(hipStreamSynchronize(c.stream));
-                for (uint64_t g = 0; g < nb; ++g)
-                    if (fl[g]) list.push_back((uint32_t)g);
-                uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
-                HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
+            if (novf) {  // the few big groups again with twice the LDS arrays, from the device-side list
+                const uint32_t nlist = novf;
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-                bucket_pieces(0, list.size(), [&](uint64_t g0, unsigned cnt) {
+                bucket_pieces(0, nlist, [&](uint64_t g0, unsigned cnt) {
                     local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
-                        sa, sac, bstart, nullptr, dlist + g0, ck, rm->cv, cidx.start, rm->out, rm->outc, gflag,
+                        sa, sac, bstart, nullptr, olist + g0, ck, rm->cv, cidx.start, rm->out, rm->outc, nullptr,
                         &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, 0, c.merge_it);
                     HIP_CHECK(hipGetLastError());
                 });
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
-                HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
+                HIP_CHECK(hipStreamSynchronize(c.stream));
             }
             if (novf) {
                 if (c.debug) fprintf(stderr, "[mtg debug] speculative rc level: %u groups overflowed, exact level\n", novf);
@@ -908,10 +903,10 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             ++c.timings.spec_levels;
             if (fine) ++c.timings.spec_fine_levels;
             if (gapped) c.gap.valid = false;  // merged: the canonical set is not needed compact
-            if (istart) {  // index end = the merged count
+            if (istart) {  // index end = the merged count (a kernel argument: no host copy to wait for)
                 const uint64_t R = n + rm->nc;
-                HIP_CHECK(hipMemcpyAsync(istart + (1ull << rm->ib), &R, 8, hipMemcpyHostToDevice, c.stream));
-                HIP_CHECK(hipStreamSynchronize(c.stream));  // R is a host local
+                set_u64_kernel<<<dim3(1), dim3(1), 0, c.stream>>>(istart + (1ull << rm->ib), R);
+                HIP_CHECK(hipGetLastError());
                 note_bucket_index(c, rm->out, R, istart, nbits - rm->ib);
             }
             if (c.debug)
@@ -1201,46 +1196,39 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             if (fuse && ngroups) {
                 // sort the rc groups and merge them with the canonical keys in one pass
                 constexpr int CAP = MergeLocalTraits<L>::CAP;
-                uint32_t *gflag = (uint32_t *)c.ws.get(Workspace::MSD_OVF, ngroups * 4);
-                HIP_CHECK(hipMemsetAsync(gflag, 0, ngroups * 4, c.stream));
+                uint32_t *olist = (uint32_t *)c.ws.get(Workspace::MSD_OVF, ngroups * 4);  // overflowing groups
                 HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
                 uint64_t *istart = rm->istart && rm->ib >= b ? rm->istart : nullptr;
                 bucket_pieces(0, ngroups, [&](uint64_t g0, unsigned cnt) {
                     local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                         *keys, COUNTED ? *vals : nullptr, gstart, gbucket, nullptr, rm->ck, rm->cv, cstart, rm->out,
-                        rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr, nullptr, g0,
+                        rm->outc, olist, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr, nullptr, g0,
                         c.merge_it);
                     HIP_CHECK(hipGetLastError());
                 });
                 uint32_t novf = 0;
                 HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
                 HIP_CHECK(hipStreamSynchronize(c.stream));
-                if (novf) {  // the few big groups again with twice the LDS arrays
-                    std::vector<uint32_t> fl(ngroups), list;
-                    HIP_CHECK(hipMemcpyAsync(fl.data(), gflag, ngroups * 4, hipMemcpyDeviceToHost, c.stream));
-                    HIP_CHECK(hipStreamSynchronize(c.stream));
-                    for (uint64_t g = 0; g < ngroups; ++g)
-                        if (fl[g]) list.push_back((uint32_t)g);
-                    uint32_t *dlist = (uint32_t *)c.ws.get(Workspace::MSD_GLIST, list.size() * 4);
-                    HIP_CHECK(hipMemcpyAsync(dlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, c.stream));
+                if (novf) {  // the few big groups again with twice the LDS arrays, from the device-side list
+                    const uint32_t nlist = novf;
                     HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
-                    bucket_pieces(0, list.size(), [&](uint64_t g0, unsigned cnt) {
+                    bucket_pieces(0, nlist, [&](uint64_t g0, unsigned cnt) {
                         local_merge_kernel<L, COUNTED, 2 * CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
-                            *keys, COUNTED ? *vals : nullptr, gstart, gbucket, dlist + g0, rm->ck, rm->cv, cstart,
-                            rm->out, rm->outc, gflag, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr,
+                            *keys, COUNTED ? *vals : nullptr, gstart, gbucket, olist + g0, rm->ck, rm->cv, cstart,
+                            rm->out, rm->outc, nullptr, &c.small->counter, b, nbits, rm->ib, istart, nullptr, nullptr,
                             nullptr, 0, c.merge_it);
                         HIP_CHECK(hipGetLastError());
                     });
                     HIP_CHECK(hipMemcpyAsync(&novf, &c.small->counter, 4, hipMemcpyDeviceToHost, c.stream));
-                    HIP_CHECK(hipStreamSynchronize(c.stream));  // `list` outlives the copy
-                    if (c.debug) fprintf(stderr, "[mtg debug] rc merge: %zu big groups -> %u left\n", list.size(), novf);
+                    HIP_CHECK(hipStreamSynchronize(c.stream));
+                    if (c.debug) fprintf(stderr, "[mtg debug] rc merge: %u big groups -> %u left\n", nlist, novf);
                 }
                 if (!novf) {
                     rm->done = true;
-                    if (istart) {  // index end = the merged count
+                    if (istart) {  // index end = the merged count (a kernel argument: no host copy to wait for)
                         const uint64_t R = n + rm->nc;
-                        HIP_CHECK(hipMemcpyAsync(istart + (1ull << rm->ib), &R, 8, hipMemcpyHostToDevice, c.stream));
-                        HIP_CHECK(hipStreamSynchronize(c.stream));  // R is a host local
+                        set_u64_kernel<<<dim3(1), dim3(1), 0, c.stream>>>(istart + (1ull << rm->ib), R);
+                        HIP_CHECK(hipGetLastError());
                         note_bucket_index(c, rm->out, R, istart, nbits - rm->ib);
                     }
                     return n;  // the rc keys (distinct); rm->out holds U + n

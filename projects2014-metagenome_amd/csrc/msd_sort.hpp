@@ -1135,7 +1135,8 @@ struct MergeLocalTraits {
 };
 
 // CAP: keys per LDS array; glist (optional): the groups to run (the big-CAP rerun of the groups
-// the first launch flagged in gflag); *ovf counts groups left over
+// the first launch listed); *ovf counts groups left over, and gflag (optional) receives their ids at
+// gflag[0 .. *ovf) in any order -- the rerun's glist, no flag array to scan on the host
 template <int L, bool COUNTED, int CAP, int LB = 512>
 __global__ __launch_bounds__(LB) void local_merge_kernel(
     const Key<L> *__restrict__ keys, const uint32_t *__restrict__ vals, const uint64_t *__restrict__ gstart,
@@ -1169,9 +1170,9 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     const uint64_t gb0 = gbucket ? gbucket[g] : g, gb1 = gbucket ? gbucket[g + 1] : g + 1;
     const uint64_t c0 = cstart[gb0], c1 = cstart[gb1];
     if (g1 - g0 > (uint64_t)CAP || c1 - c0 > (uint64_t)CAP) {
-        if (tid == 0) {
-            gflag[g] = 1;
-            atomicAdd(ovf, 1u);
+        if (tid == 0) {  // appended to the overflow list (one entry a group at most: room for every group)
+            const uint32_t p = atomicAdd(ovf, 1u);
+            if (gflag) gflag[p] = (uint32_t)g;
         }
         return;
     }
