@@ -1995,8 +1995,10 @@ __device__ __forceinline__ Key<L3> dummy_decode_walk(R r, unsigned k, R T) {
 // wave in the walk's ~k-step loop (63 ms for 6.6e8 dummies at configs[2] with or without the closed
 // form), and a global list cost one atomic per wave on one counter (+58 ms).
 template <int L3, int LR = 1>
-__global__ __launch_bounds__(256) void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n, unsigned k,
-                                                           Key<L3> *__restrict__ out) {
+__global__ __launch_bounds__(256) void dummy_decode_kernel(const Key<LR> *__restrict__ in, uint64_t n_, unsigned k,
+                                                           Key<L3> *__restrict__ out,
+                                                           const unsigned long long *__restrict__ n_dev = nullptr) {
+    const uint64_t n = n_dev ? *n_dev : n_;  // n_dev: the count as the unique pass left it on the device
     using R = RankWord<LR>;
     constexpr uint32_t LCAP = 2048;
     __shared__ uint32_t s_list[LCAP];

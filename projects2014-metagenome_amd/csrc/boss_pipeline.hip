@@ -524,11 +524,33 @@ static void bucket_index(Ctx &c, const Key<L> *keys, uint64_t n, unsigned shift,
     HIP_CHECK(hipGetLastError());
 }
 
+// exclusive scans of the per-pass digit counts: block p scans hist[p * 256 ..] into start[p * 256 ..]
+__global__ __launch_bounds__(256) void digit_starts_kernel(const unsigned long long *__restrict__ hist,
+                                                           uint64_t *__restrict__ start) {
+    __shared__ uint64_t s_wsum[4];
+    const uint32_t t = threadIdx.x, p = blockIdx.x;
+    const uint64_t v = hist[p * 256 + t];
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if ((t & 63) >= (uint32_t)o) x += y;
+    }
+    if ((t & 63) == 63) s_wsum[t >> 6] = x;
+    __syncthreads();
+    uint64_t before = 0;
+    for (uint32_t w = 0; w < (t >> 6); ++w) before += s_wsum[w];
+    start[p * 256 + t] = before + x - v;
+}
+
 // LSD radix sort of keys[0..n) (and vals) over the low nbits; result left in *keys / *vals
-// (pointers swapped with *alt / *valt as passes ping-pong).
+// (pointers swapped with *alt / *valt as passes ping-pong).  Passes whose digit is the same for every key
+// are skipped.  spec_first: the lowest pass is launched before the histogram reaches the host (the digit
+// starts are scanned on the device), so the copy and the host's look at it overlap that pass -- for
+// inputs whose lowest digit is never constant (the dense dummy ranks); a constant one costs one pass.
 template <int L, bool HAS_VAL>
 static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uint32_t **valt,
-                       uint64_t n, unsigned nbits, bool stats) {
+                       uint64_t n, unsigned nbits, bool stats, bool spec_first = false) {
     if (n < 2) return;
     const int passes = (int)ceil_div(nbits, 8);
     auto *hist = (unsigned long long *)c.ws.get(Workspace::HIST, passes * 256 * 8);
@@ -536,30 +558,17 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
     const uint64_t hgrid = std::min<uint64_t>(ceil_div(n, 256), 4096);
     radix_histogram_kernel<L><<<dim3((unsigned)hgrid), dim3(256), 0, c.stream>>>(*keys, n, passes, hist);
     HIP_CHECK(hipGetLastError());
+    auto *dstart = (uint64_t *)c.ws.get(Workspace::STARTS_DIGIT, passes * 256 * 8);
+    digit_starts_kernel<<<dim3((unsigned)passes), dim3(256), 0, c.stream>>>(hist, dstart);
+    HIP_CHECK(hipGetLastError());
     std::vector<unsigned long long> h(passes * 256);
     HIP_CHECK(hipMemcpyAsync(h.data(), hist, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
-    HIP_CHECK(hipStreamSynchronize(c.stream));
-    std::vector<uint64_t> starts(passes * 256);
-    std::vector<int> active;
-    for (int p = 0; p < passes; ++p) {
-        uint64_t s = 0;
-        bool trivial = false;
-        for (int d = 0; d < 256; ++d) {
-            starts[p * 256 + d] = s;
-            s += h[p * 256 + d];
-            if (h[p * 256 + d] == n) trivial = true;
-        }
-        if (!trivial) active.push_back(p);
-    }
-    if (active.empty()) return;
-    auto *dstart = (uint64_t *)c.ws.get(Workspace::STARTS_DIGIT, passes * 256 * 8);
-    HIP_CHECK(hipMemcpyAsync(dstart, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, c.stream));
-    HIP_CHECK(hipStreamSynchronize(c.stream));  // `starts` is a local: the copy must land first
     constexpr int TILE = SortTraits<L>::TILE;
     const uint64_t tiles = ceil_div(n, TILE);
     if (tiles > 0xFFFFFFFFull) throw std::runtime_error("sort too large");
     EventTimer tm(c.stream);
-    for (int p : active) {
+    std::vector<int> done;
+    auto launch = [&](int p) {
         uint32_t epoch;
         uint64_t *desc = acquire_desc(c, tiles * 256, &epoch);
         HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
@@ -571,12 +580,21 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
         tm.mark();
         std::swap(*keys, *alt);
         if (HAS_VAL) std::swap(*vals, *valt);
+        done.push_back(p);
+    };
+    if (spec_first) launch(0);
+    HIP_CHECK(hipStreamSynchronize(c.stream));  // the histogram on the host (`h` is a local)
+    for (int p = spec_first ? 1 : 0; p < passes; ++p) {
+        bool trivial = false;
+        for (int d = 0; d < 256; ++d)
+            if (h[p * 256 + d] == n) trivial = true;
+        if (!trivial) launch(p);
     }
-    if (stats) {
+    if (stats && !done.empty()) {
         HIP_CHECK(hipStreamSynchronize(c.stream));
-        for (size_t i = 0; i < active.size(); ++i) c.radix_ms += tm.ms(2 * i, 2 * i + 1);
-        c.radix_launches += active.size();
-        c.radix_bytes += (double)active.size() * 2.0 * n * (sizeof(Key<L>) + (HAS_VAL ? 4 : 0));
+        for (size_t i = 0; i < done.size(); ++i) c.radix_ms += tm.ms(2 * i, 2 * i + 1);
+        c.radix_launches += done.size();
+        c.radix_bytes += (double)done.size() * 2.0 * n * (sizeof(Key<L>) + (HAS_VAL ? 4 : 0));
     }
 }
 
@@ -2412,7 +2430,7 @@ static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3
     uint32_t *nv = nullptr;
     const unsigned nbits = dummy_rank_bits(kb);
     // (the real k-mers' MSD partition + LDS-hash unique on these ranks: dummy stage 4.4 -> 6.8 ms)
-    radix_sort<LR, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false);
+    radix_sort<LR, false>(c, &ra, &rb, &nv, &nv, Draw, nbits, false, true);  // (dense ranks: the low digit varies)
     reset_small(c);
     const uint64_t ut = ceil_div(Draw, 2048);
     uint32_t udesc_ep;
@@ -2420,12 +2438,13 @@ static uint64_t sort_unique_dummy_ranks(Ctx &c, unsigned kb, Key<L3> *xa, Key<L3
     unique_kernel<LR, false><<<dim3((unsigned)ut), dim3(256), 0, c.stream>>>(
         ra, nullptr, Draw, rb, nullptr, udesc, udesc_ep, &c.small->counter, &c.small->total, &c.small->error);
     HIP_CHECK(hipGetLastError());
-    const uint64_t D = read_u64(c, &c.small->total);
     Key<L3> *outk = (void *)rb == (void *)xa ? xb : xa;
-    // (a block per 256 dummies up to 16384 blocks, each a contiguous chunk)
-    dummy_decode_kernel<L3, LR><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(D, 256), 16384))),
-                                  dim3(256), 0, c.stream>>>(rb, D, kb, outk);
+    // (a block per 256 dummies up to 16384 blocks, each a contiguous chunk; the grid is sized for Draw and the
+    // kernel reads D from the device, so the copy of D to the host overlaps the decode)
+    dummy_decode_kernel<L3, LR><<<dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(Draw, 256), 16384))),
+                                  dim3(256), 0, c.stream>>>(rb, 0, kb, outk, &c.small->total);
     HIP_CHECK(hipGetLastError());
+    const uint64_t D = read_u64(c, &c.small->total);
     *dk = outk;
     return D;
 }
