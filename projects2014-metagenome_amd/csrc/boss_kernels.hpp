@@ -872,12 +872,23 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         }
         if (off != ~0u && !(ABL & 4)) {
             if ((((uintptr_t)look) & 15) == 0) {
+                // the class's <= QC + 1 keys from the even index at or below a: all of a lane's 16-byte loads in
+                // flight before its LDS stores (a rolled loop waited for each load before issuing the next)
+                constexpr int NI = (int)((QC + 1 + 127) / 128);
                 const uint64_t a0 = a & ~1ull, e = a + cnt;
-                for (uint64_t i = a0 + 2ull * lane; i < e; i += 128) {
-                    if (i + 1 < nl) {  // (never past the array's last key)
-                        const ulonglong2 v = *(const ulonglong2 *)(look + i);
-                        if (i >= a) s_r[off + (uint32_t)(i - a)] = Key<L>::from(v.x);
-                        if (i + 1 < e) s_r[off + (uint32_t)(i + 1 - a)] = Key<L>::from(v.y);
+                ulonglong2 v[NI];
+#pragma unroll
+                for (int q = 0; q < NI; ++q) {
+                    const uint64_t i = a0 + 2ull * lane + 128ull * q;
+                    if (i < e && i + 1 < nl) v[q] = *(const ulonglong2 *)(look + i);  // (never past the last key)
+                }
+#pragma unroll
+                for (int q = 0; q < NI; ++q) {
+                    const uint64_t i = a0 + 2ull * lane + 128ull * q;
+                    if (i >= e) continue;
+                    if (i + 1 < nl) {
+                        if (i >= a) s_r[off + (uint32_t)(i - a)] = Key<L>::from(v[q].x);
+                        if (i + 1 < e) s_r[off + (uint32_t)(i + 1 - a)] = Key<L>::from(v[q].y);
                     } else if (i >= a) {
                         s_r[off + (uint32_t)(i - a)] = look[i];
                     }
@@ -1588,9 +1599,23 @@ __global__ __launch_bounds__(SplitEmitTraits<L2>::BLOCK) void split_emit_kernel(
     // stage A[i0 - HALO, i1 + 1) (clipped to [0, na))
     const int64_t g0 = (int64_t)i0 - HALO;
     const uint32_t ns = (uint32_t)(i1 - i0) + HALO + 1;
-    for (uint32_t q = tid; q < ns; q += BLOCK) {
-        const int64_t g = g0 + q;
-        if (g >= 0 && g < (int64_t)na) s_a[q] = a[g];
+    {
+        // all of a thread's staging loads in flight before the LDS stores (a rolled loop waited for each
+        // load before issuing the next: one 8-byte load per wave in flight)
+        constexpr int SQ = (TILE + HALO + 1 + BLOCK - 1) / BLOCK;
+        Key<L2> st[SQ];
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
+            const uint32_t qq = tid + q * BLOCK;
+            const int64_t g = g0 + qq;
+            if (qq < ns && g >= 0 && g < (int64_t)na) st[q] = a[g];
+        }
+#pragma unroll
+        for (int q = 0; q < SQ; ++q) {
+            const uint32_t qq = tid + q * BLOCK;
+            const int64_t g = g0 + qq;
+            if (qq < ns && g >= 0 && g < (int64_t)na) s_a[qq] = st[q];
+        }
     }
     for (uint32_t q = tid; q < TILE / 32; q += BLOCK) s_bm[q] = 0;
     __syncthreads();

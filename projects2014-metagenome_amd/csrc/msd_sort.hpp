@@ -1203,9 +1203,27 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         }
     }
     const uint64_t cr = cgap ? cgap[gb0] : c0;
-    for (uint32_t i = tid; i < nc; i += LB) {
-        s_c[i] = ck[cr + i];
-        if (COUNTED) s_cv[i] = cv[cr + i];
+    {
+        // the canonical keys' loads all in flight with the rc keys' before the LDS stores (a rolled loop
+        // waited for each load before issuing the next)
+        Key<L> ckr[PR];
+        uint32_t cvr[PR];
+#pragma unroll
+        for (int q = 0; q < PR; ++q) {
+            const uint32_t i = tid + q * LB;
+            if (i < nc) {
+                ckr[q] = ck[cr + i];
+                if (COUNTED) cvr[q] = cv[cr + i];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PR; ++q) {
+            const uint32_t i = tid + q * LB;
+            if (i < nc) {
+                s_c[i] = ckr[q];
+                if (COUNTED) s_cv[i] = cvr[q];
+            }
+        }
     }
     if (tid < 256) {
         s_hist[tid] = 0;
