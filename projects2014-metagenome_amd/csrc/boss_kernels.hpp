@@ -1599,9 +1599,10 @@ __global__ __launch_bounds__(SplitEmitTraits<L2>::BLOCK) void split_emit_kernel(
     // stage A[i0 - HALO, i1 + 1) (clipped to [0, na))
     const int64_t g0 = (int64_t)i0 - HALO;
     const uint32_t ns = (uint32_t)(i1 - i0) + HALO + 1;
-    {
+    if constexpr (L2 == 1) {
         // all of a thread's staging loads in flight before the LDS stores (a rolled loop waited for each
-        // load before issuing the next: one 8-byte load per wave in flight)
+        // load before issuing the next: one 8-byte load per wave in flight).  u64 keys only: the wider
+        // keys' register array spilled (configs[2]: lift + merge 52 -> 67 ms)
         constexpr int SQ = (TILE + HALO + 1 + BLOCK - 1) / BLOCK;
         Key<L2> st[SQ];
 #pragma unroll
@@ -1615,6 +1616,11 @@ __global__ __launch_bounds__(SplitEmitTraits<L2>::BLOCK) void split_emit_kernel(
             const uint32_t qq = tid + q * BLOCK;
             const int64_t g = g0 + qq;
             if (qq < ns && g >= 0 && g < (int64_t)na) s_a[qq] = st[q];
+        }
+    } else {
+        for (uint32_t q = tid; q < ns; q += BLOCK) {
+            const int64_t g = g0 + q;
+            if (g >= 0 && g < (int64_t)na) s_a[q] = a[g];
         }
     }
     for (uint32_t q = tid; q < TILE / 32; q += BLOCK) s_bm[q] = 0;

@@ -1203,9 +1203,9 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
         }
     }
     const uint64_t cr = cgap ? cgap[gb0] : c0;
-    {
+    if constexpr (L == 1) {
         // the canonical keys' loads all in flight with the rc keys' before the LDS stores (a rolled loop
-        // waited for each load before issuing the next)
+        // waited for each load before issuing the next; u64 keys only, the wider ones' registers spill)
         Key<L> ckr[PR];
         uint32_t cvr[PR];
 #pragma unroll
@@ -1223,6 +1223,11 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
                 s_c[i] = ckr[q];
                 if (COUNTED) s_cv[i] = cvr[q];
             }
+        }
+    } else {
+        for (uint32_t i = tid; i < nc; i += LB) {
+            s_c[i] = ck[cr + i];
+            if (COUNTED) s_cv[i] = cv[cr + i];
         }
     }
     if (tid < 256) {
