@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define MTG_BOSS_ABI_VERSION 7
+#define MTG_BOSS_ABI_VERSION 8
 
 /* container types of the reference (kmer::ContainerType) */
 #define MTG_CONTAINER_VECTOR 0
@@ -151,6 +151,10 @@ typedef struct mtg_boss_timings {
     uint64_t cached_bytes;       /* device blocks the workspace keeps idle for the next build (counted in
                                     peak_bytes; freed when a build ends without reusing them, or by
                                     mtg_boss_ctor_trim) */
+    double exchange_hidden_ms;   /* multi-GPU: exchange time spent while the build stream sorted (the pieces of
+                                    exchange 1 in flight under the owner sort of the previous piece) */
+    uint64_t coresident;         /* multi-GPU: ranks sharing this rank's GPU (same host name and PCI bus id);
+                                    they split its free HBM when planning rounds */
 } mtg_boss_timings;
 
 int mtg_boss_abi_version(void);
@@ -290,6 +294,11 @@ int mtg_boss_build_device_dist(mtg_boss_ctor *ctor, mtg_comm *comm, const uint8_
                                mtg_boss_device_chunk *out);
 /* the range split: bounds[0..world] over n_prefixes buckets, balanced on hist (host) */
 int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64_t *bounds);
+/* the identity a rank all-gathers to count the ranks sharing its GPU: a hash of the host name (or
+   MTG_HOST_ID) and the device's PCI bus id; and that count for `rank` over every rank's identity
+   (timings' coresident; the ranks on one GPU split its free HBM when they plan rounds) */
+uint64_t mtg_device_identity(const char *host, const char *pci_bus_id);
+uint32_t mtg_dist_coresident(const uint64_t *ids, int world, int rank);
 
 /*
  * The graph files `metagraph build` writes from a chunk (cli/build.cpp:323-352; DBGSuccinct::serialize,

@@ -88,7 +88,8 @@ class Timings(ctypes.Structure):
                 ("input_ms", ctypes.c_double), ("spilled_bytes", ctypes.c_uint64)] + \
                [(name, ctypes.c_uint64) for name in ("spec_levels", "spec_fine_levels", "spec_fallbacks",
                                                       "collect_mode", "sent_bytes", "spec_l1",
-                                                      "cached_bytes")]
+                                                      "cached_bytes")] + \
+               [("exchange_hidden_ms", ctypes.c_double), ("coresident", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -103,7 +104,7 @@ EXPORTS = ("mtg_boss_abi_version", "mtg_last_error", "mtg_boss_ctor_create",
            "mtg_device_count", "mtg_device_synchronize", "mtg_comm_get_unique_id",
            "mtg_comm_create_rccl", "mtg_comm_create_local", "mtg_comm_destroy", "mtg_comm_rank",
            "mtg_comm_size", "mtg_boss_ctor_build_chunk_dist", "mtg_boss_build_device_dist",
-           "mtg_dist_bounds", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
+           "mtg_dist_bounds", "mtg_device_identity", "mtg_dist_coresident", "mtg_boss_ctor_add_kmc", "mtg_dna_encode_table",
            "mtg_boss_write_dbg", "mtg_sdsl_write", "mtg_boss_read_dbg", "mtg_dbg_file_free",
            "mtg_boss_ctor_add_fasta", "mtg_device_copy", "mtg_kmc_load_device",
            "mtg_device_reads_free", "mtg_kmc_write_device", "mtg_host_pool_bytes",
@@ -171,6 +172,10 @@ def lib():
                                              ctypes.c_uint64, ctypes.c_int]
         L.mtg_dist_bounds.argtypes = [P(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_int,
                                       P(ctypes.c_uint64)]
+        L.mtg_device_identity.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.mtg_device_identity.restype = ctypes.c_uint64
+        L.mtg_dist_coresident.argtypes = [P(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]
+        L.mtg_dist_coresident.restype = ctypes.c_uint32
         L.mtg_dna_encode_table.argtypes = [ctypes.c_char_p]
         L.mtg_boss_ctor_add_fasta.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.mtg_device_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
@@ -641,6 +646,14 @@ def dist_bounds(hist, world):
     _check(lib().mtg_dist_bounds(h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(h), world,
                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
     return out
+
+
+def coresident(hosts_and_buses, rank):
+    """Ranks that share rank's GPU, from every rank's (host name, PCI bus id) -- the count a
+    multi-GPU build plans its HBM share with (timings' coresident)."""
+    ids = np.array([lib().mtg_device_identity(h.encode(), b.encode()) for h, b in hosts_and_buses],
+                   dtype=np.uint64)
+    return int(lib().mtg_dist_coresident(ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(ids), rank))
 
 
 def concatenate(chunks):

@@ -321,7 +321,6 @@ struct Ctx {
     unsigned fused_b1 = 0;         // MTG_FUSED_B1=n: the fused K1's level-1 digit forced to n bits (A/B runs)
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
     bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
-    bool lu_lean = false;          // MTG_LU_LEAN=1: the speculative level's local pass as local_unique_lean_kernel
     bool fast2 = true;             // MTG_FAST2=0: the u128 rounds' pass B as the generic extract_partition_kernel
     int canon_mode = 1;            // the single-build extraction's canonical representative (cmode); the
                                    // super-k-mer owners of a multi-GPU build extract with 2
@@ -371,6 +370,10 @@ struct Ctx {
     // first eighth.)
     bool spec3 = true;
     bool rounds_one_b = false;  // MTG_ROUNDS_ONE_B=1: two collect rounds share one pass B (collect_rounds_fused)
+    // MTG_DIST_PIECES=n: the routed multi-GPU collect sends exchange 1 in n pieces on the exchange stream,
+    // each sorted by its owner while the next one is in flight (routed_pieces); 1 = one exchange, then the sort
+    uint32_t dist_pieces = 4;
+    hipStream_t xstream = nullptr;  // the multi-GPU exchange stream (created by the first distributed build)
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
     bool spec_tiny = false;  // MTG_SPEC_CAPS=tiny: speculative buckets without slack (tests force the
@@ -422,7 +425,6 @@ static void load_knobs(Ctx &c) {
     c.wide_b1 = !is("MTG_WIDE_B1", "0");
     c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
     c.lu_fast = !is("MTG_LU_FAST", "0");
-    c.lu_lean = is("MTG_LU_LEAN", "1");
     c.fast2 = !is("MTG_FAST2", "0");
     if (const char *e = getenv("MTG_MERGE_IT")) c.merge_it = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
@@ -431,6 +433,7 @@ static void load_knobs(Ctx &c) {
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
     c.rounds_one_b = is("MTG_ROUNDS_ONE_B", "1");
+    if (const char *e = getenv("MTG_DIST_PIECES")) c.dist_pieces = (uint32_t)std::max(1L, std::min(16L, atol(e)));
     c.spec_tiny = is("MTG_SPEC_CAPS", "tiny");
     c.spec_lu_fail = is("MTG_SPEC_LU_FAIL", "1");
     c.spec_l1 = !is("MTG_SPEC_L1", "0");
@@ -945,10 +948,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // fraction of them); the others count 0 keys
         HIP_CHECK(hipMemsetAsync(ucount, 0, (nb + 1) * 4, c.stream));
         bucket_pieces(blo, bhi, [&](uint64_t g0, unsigned cnt) {
-            if (!COUNTED && keycas && c.lu_lean)
-                local_unique_lean_kernel<LocalTraits<1>::SLOTS / 2><<<dim3(cnt), dim3(512), 0, c.stream>>>(
-                    (const uint64_t *)sa, bstart, cur, (uint64_t *)sb, ucount, ovf, &c.small->counter, g0);
-            else if (keycas && c.lu_fast)
+            if (keycas && c.lu_fast)
                 local_unique_kernel<1, COUNTED, true, 512, LocalTraits<1>::SLOTS / 2, false, WPE, true, false>
                     <<<dim3(cnt), dim3(512), 0, c.stream>>>(sa, sac, bstart, nullptr, nbits, bb, 0, sb, sbc, ucount, ovf,
                                                             &c.small->counter, cmax, cur, g0);
@@ -2227,10 +2227,13 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     if (one_b) {
         // round 1's buckets start at nr[0] in the pass's layout and at ka2 in memory
         std::vector<long long> delta(nb1, 0);
-        const long long d1 = (long long)(ka2 - ka) - (long long)nr[0];
+        // (two allocations: their distance in elements from the addresses, not a pointer difference)
+        const long long d1 = ((long long)(intptr_t)ka2 - (long long)(intptr_t)ka) / (long long)sizeof(K2) -
+                             (long long)nr[0];
         for (uint32_t b = (uint32_t)bb[1]; b < nb1; ++b) delta[b] = d1;
         long long *dd = (long long *)c.ws.get(Workspace::ROUND_DELTA, nb1 * 8);
         HIP_CHECK(hipMemcpyAsync(dd, delta.data(), nb1 * 8, hipMemcpyHostToDevice, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // `delta` is a block-local host vector
         const uint32_t *dh1_all = nullptr;
         const uint64_t n = fused_pass_b<L, COUNTED>(c, K, canonical, cmax, in, A, b1, nullptr, ka, ca, &dh1_all, dd);
         if (n != N) throw std::runtime_error("the collect rounds' pass B differs from its histogram");
@@ -2841,6 +2844,7 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
                             Workspace::RC_ALTC, Workspace::SPEC_A, Workspace::SPEC_B, Workspace::SPEC_AC,
                             Workspace::SPEC_BC})
                 c.ws.release(sl);
+            c.gidx = Ctx::GroupIndex{};  // it indexed the CANON block given back above
         }
     }
     ensure_compact(c);  // (a no-op unless the canonical set is still in buckets)
@@ -2939,10 +2943,30 @@ struct Dist {
     uint32_t coresident = 1;  // ranks on this rank's GPU (dist_coresident), the HBM they share
 };
 
+// a GPU's identity across hosts: FNV-1a of the host name and the device's PCI bus id (identical nodes
+// repeat the same bus ids, so the bus id alone made every rank at the same slot of another node look
+// co-resident -- ADVICE r5).  MTG_HOST_ID replaces the host name (the two-process tests play two hosts)
+static uint64_t device_identity(const char *host, const char *bus) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const char *s) {
+        for (const char *q = s; *q; ++q) h = (h ^ (uint8_t)*q) * 1099511628211ull;
+    };
+    mix(host);
+    mix("|");
+    mix(bus);
+    return h;
+}
+
+static uint32_t coresident_count(const uint64_t *ids, int P, uint64_t mine) {
+    uint32_t n = 0;
+    for (int r = 0; r < P; ++r) n += ids[r] == mine;
+    return std::max<uint32_t>(n, 1);
+}
+
 // the ranks that share this rank's GPU (threads of one process on its device, or several processes
-// on one card): an all-gather of a hash of the device's PCI bus id.  The rounds planners give each
-// of them an equal share of the free HBM -- each planning for the whole free memory over-committed
-// it (8 co-resident ranks of the round-4 simulation ran out of memory)
+// on one card): an all-gather of device_identity.  The rounds planners give each of them an equal
+// share of the free HBM -- each planning for the whole free memory over-committed it (8 co-resident
+// ranks of the round-4 simulation ran out of memory)
 static uint32_t dist_coresident(Ctx &c, Dist &d) {
     if (d.P <= 1) return 1;
     int dev = 0;
@@ -2952,17 +2976,17 @@ static uint32_t dist_coresident(Ctx &c, Dist &d) {
         (void)hipGetLastError();
         snprintf(bus, sizeof(bus), "device %d", dev);
     }
-    uint64_t h = 1469598103934665603ull;  // FNV-1a
-    for (const char *q = bus; *q; ++q) h = (h ^ (uint8_t)*q) * 1099511628211ull;
+    char host[256] = {};
+    if (const char *e = getenv("MTG_HOST_ID")) snprintf(host, sizeof(host), "%s", e);
+    else if (gethostname(host, sizeof(host) - 1) != 0) snprintf(host, sizeof(host), "?");
+    const uint64_t h = device_identity(host, bus);
     uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, (1 + (uint64_t)d.P) * 8);
     HIP_CHECK(hipMemcpyAsync(dv, &h, 8, hipMemcpyHostToDevice, c.stream));
     d.comm.allgather_u64(dv, dv + 1, 1, c.stream);
     std::vector<uint64_t> all(d.P);
     HIP_CHECK(hipMemcpyAsync(all.data(), dv + 1, (uint64_t)d.P * 8, hipMemcpyDeviceToHost, c.stream));
     HIP_CHECK(hipStreamSynchronize(c.stream));  // `h` is a host local
-    uint32_t n = 0;
-    for (uint64_t v : all) n += v == h;
-    return std::max<uint32_t>(n, 1);
+    return coresident_count(all.data(), d.P, h);
 }
 
 // a rank's HBM budget for planning its rounds: memory_preallocated, else its share of the free HBM
@@ -3319,6 +3343,156 @@ static bool dist_window_input(Ctx &c, Dist &d, unsigned K, const BuildInput &in)
     return any_other == 0;
 }
 
+// Exchange 1 in pieces, hidden behind the owner sort.  Every owner's level-1 bucket interval is cut
+// into Q consecutive sub-intervals balanced on the global histogram; piece q carries sub-interval q of
+// every owner -- from each rank one contiguous slice of its scattered array per owner, at pass B's bucket
+// cursors -- so the Q all-to-alls go out back to back on the exchange stream while the build stream
+// sorts piece q - 1 (level 2 + LDS unique over its buckets, the single build's passes) and appends its
+// distinct keys to the owned canonical set in BOSS order (the pieces are consecutive key ranges).  The
+// reference has no runtime exchange (it shards by suffix, cli/build.cpp:106-148); the merge semantics are
+// SortedMultiset's (sorted_multiset.cpp:54-84), the same as the one-exchange path.  The send counts of all
+// pieces are known after pass B, so one all-gather sizes every receive before the first piece leaves.
+// Returns the owned distinct keys (in the CANON slot); *hidden_ms = exchange time overlapped with sorting.
+template <bool COUNTED>
+static uint64_t routed_pieces(Ctx &c, Dist &d, unsigned K, uint32_t cmax, const Key<1> *ka, const uint32_t *ca,
+                              const std::vector<unsigned long long> &cur, uint64_t nr, uint32_t nb1, unsigned B1,
+                              unsigned OB, const std::vector<uint64_t> &bounds, const std::vector<uint64_t> &gh1,
+                              const std::vector<uint64_t> &H, Key<1> **out, uint32_t **outc, double *xspan_ms,
+                              double *hidden_ms, Tracer &tr) {
+    using K2 = Key<1>;
+    constexpr uint32_t NBH = 1u << FUSED_HB;
+    const int P = d.P;
+    const uint32_t Q = c.dist_pieces;
+    std::vector<std::vector<uint64_t>> sub(P);
+    for (int o = 0; o < P; ++o) {
+        const uint64_t o0 = std::min<uint64_t>(bounds[o] << (B1 - OB), nb1);
+        const uint64_t o1 = std::min<uint64_t>(bounds[o + 1] << (B1 - OB), nb1);
+        sub[o] = balanced_bounds(gh1.data() + o0, o1 - o0, (int)Q);
+        for (auto &v : sub[o]) v += o0;
+    }
+    auto at = [&](uint64_t b) -> uint64_t { return b >= nb1 ? nr : cur[b]; };
+    // this rank's slices: piece-major, then owner; every rank's counts -> the matrix
+    const size_t V = (size_t)Q * P;
+    std::vector<uint64_t> scnt(V), soff(V);
+    for (uint32_t q = 0; q < Q; ++q)
+        for (int o = 0; o < P; ++o) {
+            soff[q * P + o] = at(sub[o][q]);
+            scnt[q * P + o] = at(sub[o][q + 1]) - soff[q * P + o];
+        }
+    uint64_t *dm = (uint64_t *)c.ws.get(Workspace::XMAT, (V + V * P) * 8);
+    HIP_CHECK(hipMemcpyAsync(dm, scnt.data(), V * 8, hipMemcpyHostToDevice, c.stream));
+    const int e0 = d.tm->mark();
+    d.comm.allgather_u64(dm, dm + V, V, c.stream);
+    d.xev.push_back({e0, d.tm->mark()});
+    std::vector<uint64_t> mat(V * P);
+    HIP_CHECK(hipMemcpyAsync(mat.data(), dm + V, V * P * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    // receive layout: piece-major, then source rank
+    std::vector<uint64_t> rcnt(V), roff(V), pbase(Q + 1, 0);
+    uint64_t n1 = 0;
+    for (uint32_t q = 0; q < Q; ++q) {
+        pbase[q] = n1;
+        for (int i = 0; i < P; ++i) {
+            rcnt[q * P + i] = mat[(size_t)i * V + q * P + d.me];
+            roff[q * P + i] = n1;
+            n1 += rcnt[q * P + i];
+        }
+    }
+    pbase[Q] = n1;
+    // every buffer the pieces touch is sized before the first one leaves (a workspace slot that grows
+    // synchronizes the device, which would wait for the exchange)
+    K2 *xa = (K2 *)c.ws.get(Workspace::XA, std::max<uint64_t>(n1, 1) * sizeof(K2));
+    K2 *xb = (K2 *)c.ws.get(Workspace::XB, std::max<uint64_t>(n1, 1) * sizeof(K2));
+    uint32_t *xac = COUNTED ? (uint32_t *)c.ws.get(Workspace::XAC, std::max<uint64_t>(n1, 1) * 4) : nullptr;
+    uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, std::max<uint64_t>(n1, 1) * 4) : nullptr;
+    K2 *acc = (K2 *)c.ws.get(Workspace::CANON, std::max<uint64_t>(n1, 1) * sizeof(K2));
+    uint32_t *accc = COUNTED ? (uint32_t *)c.ws.get(Workspace::CANONC, std::max<uint64_t>(n1, 1) * 4) : nullptr;
+    uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
+    if (!c.xstream) HIP_CHECK(hipStreamCreateWithFlags(&c.xstream, hipStreamNonBlocking));
+    hipStream_t xs = c.xstream;
+    // events: pass B done (build stream); exchange start + each piece's end (exchange stream); each sort's end
+    std::vector<hipEvent_t> ev(2 * Q + 2);
+    for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
+    struct EvFree {
+        std::vector<hipEvent_t> &v;
+        ~EvFree() {
+            for (auto e : v) (void)hipEventDestroy(e);
+        }
+    } ev_free{ev};
+    hipEvent_t ev_b = ev[0], ev_x0 = ev[1];
+    hipEvent_t *ev_x = ev.data() + 2, *ev_s = ev.data() + 2 + Q;
+    HIP_CHECK(hipEventRecord(ev_b, c.stream));
+    HIP_CHECK(hipStreamWaitEvent(xs, ev_b, 0));
+    HIP_CHECK(hipEventRecord(ev_x0, xs));
+    for (uint32_t q = 0; q < Q; ++q) {
+        d.comm.alltoallv_async(ka, &scnt[q * P], &soff[q * P], xa, &rcnt[q * P], &roff[q * P], sizeof(K2), xs);
+        if (COUNTED) d.comm.alltoallv_async(ca, &scnt[q * P], &soff[q * P], xac, &rcnt[q * P], &roff[q * P], 4, xs);
+        HIP_CHECK(hipEventRecord(ev_x[q], xs));
+        for (int j = 0; j < P; ++j)
+            if (j != d.me) c.timings.n_sent += scnt[q * P + j];
+    }
+    tr("exchange 1 issued", n1);
+    std::vector<std::vector<uint32_t>> hown(Q, std::vector<uint32_t>(nb1, 0));  // live until the end (async copies)
+    uint64_t off = 0;
+    for (uint32_t q = 0; q < Q; ++q) {
+        HIP_CHECK(hipStreamWaitEvent(c.stream, ev_x[q], 0));
+        const uint64_t rb0 = sub[d.me][q], rb1 = sub[d.me][q + 1];
+        uint64_t nown = 0;
+        for (uint32_t i = 0; i < NBH; ++i) {
+            const uint32_t b = i >> (FUSED_HB - B1);
+            if (b >= rb0 && b < rb1) {
+                hown[q][b] += (uint32_t)H[i];
+                nown += H[i];
+            }
+        }
+        const uint64_t nq = pbase[q + 1] - pbase[q];
+        if (nown != nq) throw std::runtime_error("received k-mers differ from the global histogram of the owned piece");
+        uint64_t Ur = 0;
+        K2 *pa = xa + pbase[q], *pb = xb + pbase[q];
+        uint32_t *pac = COUNTED ? xac + pbase[q] : nullptr, *pbc = COUNTED ? xbc + pbase[q] : nullptr;
+        if (nq) {
+            HIP_CHECK(hipMemcpyAsync(dh1, hown[q].data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
+            const double spread = (double)nb1 / (double)std::max<uint64_t>(1, rb1 - rb0);
+            const double dup = estimate_dup<1>(c, pa, nq, 8.0) / spread;
+            MsdPlan plan = msd_plan<1>(c, nq, 2 * K, dup);
+            unsigned T = plan.levels ? plan.digit_end[plan.levels] : 0;
+            T = std::min(2 * K, std::max(T, B1 + 1));
+            MsdPlan fp{};
+            fp.levels = 1 + (T - B1 + MSD_DBITS - 1) / MSD_DBITS;
+            fp.digit_end[1] = B1;
+            for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
+            c.track_partition = q == 0;
+            Ur = msd_sort_unique<1, COUNTED>(c, &pa, &pb, &pac, &pbc, nq, 2 * K, cmax, dup, dh1, false, nullptr, true,
+                                             nullptr, &fp);
+            c.track_partition = false;
+            if (Ur) {
+                HIP_CHECK(hipMemcpyAsync(acc + off, pa, Ur * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+                if (COUNTED) HIP_CHECK(hipMemcpyAsync(accc + off, pac, Ur * 4, hipMemcpyDeviceToDevice, c.stream));
+            }
+        }
+        HIP_CHECK(hipEventRecord(ev_s[q], c.stream));
+        off += Ur;
+        tr("piece sorted", nq, Ur);
+    }
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    HIP_CHECK(hipStreamSynchronize(xs));
+    // exchange wall time and the part of it the build stream spent sorting: piece q's exposed wait is how
+    // far it ended after the build stream became free (pass B for piece 0, the sort of piece q - 1 after)
+    float span = 0;
+    HIP_CHECK(hipEventElapsedTime(&span, ev_x0, ev_x[Q - 1]));
+    double exposed = 0;
+    for (uint32_t q = 0; q < Q; ++q) {
+        float t = 0;
+        HIP_CHECK(hipEventElapsedTime(&t, q ? ev_s[q - 1] : ev_b, ev_x[q]));
+        exposed += std::max(0.0f, t);
+    }
+    *xspan_ms = span;
+    *hidden_ms = std::max(0.0, (double)span - exposed);
+    *out = acc;
+    *outc = accc;
+    return off;
+}
+
 template <bool COUNTED>
 static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                                 Key<1> **xa_out, uint32_t **xac_out, uint64_t *U_out, std::vector<uint64_t> *bounds,
@@ -3515,6 +3689,18 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
         }
         if (rounds == 1) *ev_extract = tm.mark();
         tr("extract + scatter", nr);
+        if (rounds == 1 && d.P > 1 && c.dist_pieces > 1) {
+            // exchange 1 in pieces under the owner sort (routed_pieces)
+            double span = 0, hidden = 0;
+            U = routed_pieces<COUNTED>(c, d, K, cmax, ka, ca, cur, nr, nb1, B1, OB, *bounds, gh1, H, &xa, &xac, &span,
+                                       &hidden, tr);
+            c.timings.exchange_ms += span;
+            c.timings.exchange_hidden_ms += hidden;
+            for (auto sl : {Workspace::XA, Workspace::XB, Workspace::XAC, Workspace::XBC, Workspace::SPEC_A,
+                            Workspace::SPEC_B})
+                c.ws.release(sl);
+            break;
+        }
         // exchange 1: owner o gets the rank's buckets of its prefixes [bounds[o], bounds[o + 1]) (of
         // this round: the other buckets are empty)
         std::vector<std::vector<uint64_t>> soff(1, std::vector<uint64_t>(d.P + 1));
@@ -3741,6 +3927,7 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
     const uint64_t sent0 = comm.sent_bytes;
     if (d.P > MAX_RANKS) throw std::runtime_error("more ranks than the routing kernels support");
     d.coresident = dist_coresident(c, d);
+    T.coresident = d.coresident;
     T.world = (uint64_t)d.P;
     T.n_batches = 1;
     // ranges on the top m node chars, m <= k - 1 keeps every emission group inside one rank
@@ -4911,6 +5098,10 @@ void mtg_boss_ctor_destroy(mtg_boss_ctor *c) {
     if (c->ctx.stream) (void)hipStreamSynchronize(c->ctx.stream);
     if (c->ctx.small) (void)hipFree(c->ctx.small);
     if (c->ctx.stream) (void)hipStreamDestroy(c->ctx.stream);
+    if (c->ctx.xstream) {
+        (void)hipStreamSynchronize(c->ctx.xstream);
+        (void)hipStreamDestroy(c->ctx.xstream);
+    }
     delete c;
 }
 
@@ -5754,6 +5945,15 @@ int mtg_boss_ctor_build_chunk_dist(mtg_boss_ctor *c, mtg_comm *comm, mtg_boss_ch
         return MTG_ERR_ARGUMENT;
     }
     return build_chunk_impl(c, comm->comm.get(), out);
+}
+
+uint64_t mtg_device_identity(const char *host, const char *pci_bus_id) {
+    return device_identity(host ? host : "", pci_bus_id ? pci_bus_id : "");
+}
+
+uint32_t mtg_dist_coresident(const uint64_t *ids, int world, int rank) {
+    if (!ids || world < 1 || rank < 0 || rank >= world) return 0;
+    return coresident_count(ids, world, ids[rank]);
 }
 
 int mtg_dist_bounds(const uint64_t *hist, uint64_t n_prefixes, int world, uint64_t *bounds) {

@@ -52,9 +52,23 @@ class Comm {
             if (j != rank_) sent_bytes += scnt[j] * esz;
         alltoallv_impl(d_send, scnt, soff, d_recv, rcnt, roff, esz, s);
     }
+    // the same exchange enqueued on stream s without blocking the host where the transport allows it
+    // (RCCL: grouped send/recv; LocalComm: copies ordered after the senders' events on their streams), so
+    // the caller can sort on another stream meanwhile; the caller orders every later use of d_send and
+    // d_recv after s.  A transport that cannot (the host-staged callbacks) completes it before returning
+    void alltoallv_async(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                         const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) {
+        for (int j = 0; j < size_; ++j)
+            if (j != rank_) sent_bytes += scnt[j] * esz;
+        alltoallv_async_impl(d_send, scnt, soff, d_recv, rcnt, roff, esz, s);
+    }
     uint64_t sent_bytes = 0;  // bytes this rank sent to others through alltoallv
     virtual void alltoallv_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
                                 const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) = 0;
+    virtual void alltoallv_async_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                                      const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) {
+        alltoallv_impl(d_send, scnt, soff, d_recv, rcnt, roff, esz, s);
+    }
     // a build's device work starts / ends on stream s (LocalComm's serial mode hands the device over)
     virtual void begin_build(hipStream_t) {}
     virtual void end_build(hipStream_t) {}
@@ -156,6 +170,11 @@ class RcclComm : public Comm {
                                     comm_, s));
         }
         RCCL_CHECK(api.GroupEnd());
+    }
+    // grouped send/recv only enqueue: the host returns at once, the transfers run on s
+    void alltoallv_async_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                              const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
+        alltoallv_impl(d_send, scnt, soff, d_recv, rcnt, roff, esz, s);
     }
 
   private:
@@ -272,6 +291,8 @@ struct LocalGroup {
     struct Slot {
         const void *ptr = nullptr;
         std::vector<uint64_t> soff, scnt;
+        hipEvent_t ready = nullptr;  // async all-to-all: the send buffer is complete on its rank's stream
+        hipEvent_t done = nullptr;   // async all-to-all: this rank's copies out of its peers' buffers ended
     };
     std::vector<Slot> slots;
     std::vector<std::vector<uint64_t>> host;
@@ -398,8 +419,64 @@ class LocalComm : public Comm {
         wait();  // nobody reuses its send buffer while a peer still copies from it
         hold();
     }
+    ~LocalComm() override {
+        if (ev_ready_) (void)hipEventDestroy(ev_ready_);
+        if (ev_done_) (void)hipEventDestroy(ev_done_);
+    }
+    // the all-to-all ordered by events instead of host waits: every rank publishes its send buffer with an
+    // event recorded on its stream s at the call, each receiver's copy kernel waits for its senders'
+    // events on ITS stream s, and each sender's s then waits for every receiver's copy-done event (its
+    // send buffer stays valid until then).  The two host barriers only exchange pointers and event
+    // handles, so the host returns with the copies still queued.  An event is re-recorded only in the
+    // next call, after the barrier every peer passes once it has queued its waits on the old record.
+    void alltoallv_async_impl(const void *d_send, const uint64_t *scnt, const uint64_t *soff, void *d_recv,
+                              const uint64_t *rcnt, const uint64_t *roff, size_t esz, hipStream_t s) override {
+        if (g_->serial || size_ > kLocalCopyMax) {  // serial mode times each rank's device work alone
+            alltoallv_impl(d_send, scnt, soff, d_recv, rcnt, roff, esz, s);
+            return;
+        }
+        if (!ev_ready_) {
+            COMM_HIP(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
+            COMM_HIP(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+        }
+        COMM_HIP(hipEventRecord(ev_ready_, s));
+        auto &slot = g_->slots[rank_];
+        slot.ptr = d_send;
+        slot.soff.assign(soff, soff + size_);
+        slot.scnt.assign(scnt, scnt + size_);
+        slot.ready = ev_ready_;
+        wait();
+        LocalCopyBatch batch{};
+        uint64_t most = 0;
+        for (int i = 0; i < size_; ++i) {
+            const auto &src = g_->slots[i];
+            if (src.scnt[rank_] != rcnt[i]) {
+                const std::string msg = "local all-to-all: rank " + std::to_string(rank_) + " expects " +
+                                        std::to_string(rcnt[i]) + " elements from rank " + std::to_string(i) +
+                                        ", which sends " + std::to_string(src.scnt[rank_]);
+                g_->fail(msg);
+                throw std::runtime_error(msg);
+            }
+            if (i != rank_ && rcnt[i]) COMM_HIP(hipStreamWaitEvent(s, src.ready, 0));
+            batch.src[i] = (const char *)src.ptr + src.soff[rank_] * esz;
+            batch.dst[i] = (char *)d_recv + roff[i] * esz;
+            batch.bytes[i] = rcnt[i] * esz;
+            most = std::max<uint64_t>(most, rcnt[i] * esz);
+        }
+        if (most) {
+            const unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((most + 16383) / 16384, 2048));
+            local_copy_kernel<<<dim3(gx, (unsigned)size_), dim3(256), 0, s>>>(batch);
+            COMM_HIP(hipGetLastError());
+        }
+        COMM_HIP(hipEventRecord(ev_done_, s));
+        slot.done = ev_done_;
+        wait();
+        for (int j = 0; j < size_; ++j)
+            if (j != rank_ && scnt[j]) COMM_HIP(hipStreamWaitEvent(s, g_->slots[j].done, 0));
+    }
 
   private:
+    hipEvent_t ev_ready_ = nullptr, ev_done_ = nullptr;
     // serial mode: take / hand over the device (the stream is drained before every hand-over)
     void hold() {
         if (!g_->serial || held_) return;

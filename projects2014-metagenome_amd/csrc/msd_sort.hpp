@@ -936,187 +936,6 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 }
 
 /*
- * local_unique_kernel's hot instance, lean (round 5): the uncounted u64 speculative final level
- * (spec_final_level), one bucket per group [gstart[g], gend[g]) of a 2^bb-bucket level, no key-range
- * slices.  What it drops against the generic kernel, per key: 64-bit group indices (a group's keys are
- * addressed by 32-bit offsets from its first 16-byte pair), the slice test, the 64-bit multiply of the
- * hash (the key's low word xor its bits 29.., one 32-bit multiply: the bucket's top bits are common to
- * every key of the group), and the fully unrolled probe chain (a rolled loop, capped at 64 probes: a
- * longer chain reports an overflow and the caller runs the exact level).  The distinct keys are then
- * compacted, counting-sorted on the 8 bits below their highest differing bit and ranked as there.
- */
-template <int SLOTS = 4096>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) void local_unique_lean_kernel(
-    const uint64_t *__restrict__ keys, const uint64_t *__restrict__ gstart, const unsigned long long *__restrict__ gend,
-    uint64_t *__restrict__ tmp, uint32_t *__restrict__ ucount, uint32_t *__restrict__ overflow,
-    uint32_t *__restrict__ novf, uint64_t g_base) {
-    constexpr int LB = 512;
-    constexpr uint32_t LIMIT = SLOTS / 2;
-    constexpr int HB = __builtin_ctz(SLOTS);
-    constexpr uint64_t EMPTY = ~0ull;
-    constexpr int BP = 2;  // 16-byte pairs per thread and load batch (4 keys: no spill at 64 VGPRs)
-    __shared__ uint64_t s_key[SLOTS];
-    __shared__ uint16_t s_slot[LIMIT];
-    __shared__ uint32_t s_hist[256];
-    __shared__ uint32_t s_fill[256];
-    __shared__ uint32_t s_distinct;
-    __shared__ int s_hb;
-    const uint64_t g = g_base + blockIdx.x;
-    const uint64_t g0 = gstart[g], g1 = gend[g];
-    const uint32_t tid = threadIdx.x;
-    if (g0 >= g1) {
-        if (tid == 0) ucount[g] = 0;
-        return;
-    }
-    for (int i = tid; i < SLOTS; i += LB) s_key[i] = EMPTY;
-    if (tid < 256) {
-        s_hist[tid] = 0;
-        s_fill[tid] = 0;
-    }
-    if (tid == 0) {
-        s_distinct = 0;
-        s_hb = -1;
-    }
-    __syncthreads();
-    const uint64_t a0 = g0 & ~1ull;
-    const uint32_t lo = (uint32_t)(g0 - a0), n = (uint32_t)(g1 - a0);  // the group: offsets [lo, n) from a0
-    const uint64_t *__restrict__ kp = keys + a0;
-    bool ovf = false;
-    for (uint32_t ib = 2 * tid; ib < n; ib += 2 * LB * BP) {
-        uint64_t kb[2 * BP];
-        uint32_t valid = 0;
-#pragma unroll
-        for (int q = 0; q < BP; ++q) {
-            const uint32_t i = ib + (uint32_t)q * 2 * LB;
-            kb[2 * q] = kb[2 * q + 1] = 0;
-            if (i + 1 < n) {
-                const ulonglong2 v = *(const ulonglong2 *)(kp + i);
-                kb[2 * q] = v.x;
-                kb[2 * q + 1] = v.y;
-                valid |= ((uint32_t)(i >= lo) | 2u) << (2 * q);
-            } else if (i < n) {
-                kb[2 * q] = kp[i];
-                valid |= (uint32_t)(i >= lo) << (2 * q);
-            }
-        }
-        uint32_t dpos[2 * BP];  // (position among the wave's new keys of the batch << 16 | slot), ~0 = not new
-        uint32_t wnew = 0;
-#pragma unroll
-        for (int q = 0; q < 2 * BP; ++q) {
-            int32_t ins = -1;
-            if ((valid >> q) & 1u) {
-                const uint64_t key = kb[q];
-                const uint32_t mix = (uint32_t)key ^ __builtin_amdgcn_alignbit((uint32_t)(key >> 32), (uint32_t)key, 29);
-                uint32_t h = (mix * 0x9E3779B1u) >> (32 - HB);
-                uint64_t old = atomicCAS((unsigned long long *)&s_key[h], (unsigned long long)EMPTY,
-                                         (unsigned long long)key);
-                uint32_t probes = 0;
-#pragma nounroll
-                while (old != EMPTY && old != key) {
-                    if (++probes == 64) {
-                        ovf = true;
-                        break;
-                    }
-                    h = (h + 1) & (SLOTS - 1);
-                    old = atomicCAS((unsigned long long *)&s_key[h], (unsigned long long)EMPTY, (unsigned long long)key);
-                }
-                if (old == EMPTY) ins = (int32_t)h;
-            }
-            const uint64_t m = __ballot(ins >= 0);
-            dpos[q] = ins >= 0 ? ((wnew + popc_below(m)) << 16 | (uint32_t)ins) : ~0u;
-            wnew += (uint32_t)__popcll(m);
-        }
-        if (wnew) {  // the batch's new keys of the wave: one LDS atomic, positions known
-            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1;
-            uint32_t wb = 0;
-            if (__lane_id() == leader) wb = atomicAdd(&s_distinct, wnew);
-            wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, (int)leader);
-#pragma unroll
-            for (int q = 0; q < 2 * BP; ++q) {
-                if (dpos[q] != ~0u) {
-                    const uint32_t pos = wb + (dpos[q] >> 16);
-                    if (pos < LIMIT) s_slot[pos] = (uint16_t)(dpos[q] & 0xFFFFu);
-                    else ovf = true;
-                }
-            }
-        }
-    }
-    if (__syncthreads_or(ovf) || s_distinct > LIMIT) {
-        if (tid == 0) {
-            overflow[g] = 1;
-            ucount[g] = 0;
-            atomicAdd(novf, 1u);
-        }
-        return;
-    }
-    const uint32_t D = s_distinct;
-    // gather the D recorded slots, then write them compacted to s_key[0..D)
-    constexpr int PERL = (LIMIT + LB - 1) / LB;
-    uint64_t kk[PERL];
-#pragma unroll
-    for (int q = 0; q < PERL; ++q) {
-        const uint32_t i = tid + q * LB;
-        if (i < D) kk[q] = s_key[s_slot[i]];
-    }
-    __syncthreads();
-    int hb_local = -1;
-#pragma unroll
-    for (int q = 0; q < PERL; ++q) {
-        const uint32_t i = tid + q * LB;
-        if (i < D) s_key[i] = kk[q];
-    }
-    __syncthreads();
-    {
-        const uint64_t r0 = s_key[0];
-#pragma unroll
-        for (int q = 0; q < PERL; ++q)
-            if (tid + q * LB < D) {
-                const uint64_t dx = kk[q] ^ r0;
-                hb_local = max(hb_local, dx ? 63 - __clzll((long long)dx) : -1);
-            }
-        wave_atomic_max(&s_hb, hb_local);
-    }
-    __syncthreads();
-    const int hb = s_hb;
-    const unsigned dshift = hb >= 7 ? (unsigned)(hb - 7) : 0u;
-    uint64_t *scratch = s_key + LIMIT;  // free half of the table
-#pragma unroll
-    for (int q = 0; q < PERL; ++q)
-        if (tid + q * LB < D) atomicAdd(&s_hist[(uint32_t)(kk[q] >> dshift) & 0xFFu], 1u);
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
-        const uint32_t c0 = s_hist[4 * tid], c1 = s_hist[4 * tid + 1], c2 = s_hist[4 * tid + 2],
-                       c3 = s_hist[4 * tid + 3];
-        const uint32_t sum4 = c0 + c1 + c2 + c3;
-        const uint32_t bb = wave_inclusive_sum(sum4) - sum4;
-        s_hist[4 * tid] = bb;
-        s_hist[4 * tid + 1] = bb + c0;
-        s_hist[4 * tid + 2] = bb + c0 + c1;
-        s_hist[4 * tid + 3] = bb + c0 + c1 + c2;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PERL; ++q)
-        if (tid + q * LB < D) {
-            const uint32_t d = (uint32_t)(kk[q] >> dshift) & 0xFFu;
-            scratch[s_hist[d] + atomicAdd(&s_fill[d], 1u)] = kk[q];
-        }
-    __syncthreads();
-    for (uint32_t p = tid; p < D; p += LB) {
-        const uint64_t key = scratch[p];
-        const uint32_t d = (uint32_t)(key >> dshift) & 0xFFu;
-        const uint32_t b0 = s_hist[d], b1 = b0 + s_fill[d];
-        uint32_t rank = 0;
-        for (uint32_t j = b0; j < b1; ++j) rank += scratch[j] < key;
-        tmp[g0 + b0 + rank] = key;
-    }
-    if (tid == 0) {
-        ucount[g] = D;
-        overflow[g] = 0;
-    }
-}
-
-/*
  * The reverse-complement sort's local pass fused with the merge into the real edges
  * (add_reverse_complements, boss_chunk_construct.cpp:179-222): one workgroup per group of the rc
  * partition sorts the group's rc keys in LDS (distinct input: the counting sort + rank of

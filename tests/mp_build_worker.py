@@ -33,7 +33,8 @@ def main():
     t = ctor.timings()
     np.savez(out_path, W=ch.W, last=ch.last, F=ch.F,
              weights=ch.weights if ch.weights is not None else np.zeros(0, dtype=np.uint32),
-             n_real=ch.n_real, n_dummy=ch.n_dummy, world=t.world, n_sent=t.n_sent, batches=t.n_batches)
+             n_real=ch.n_real, n_dummy=ch.n_dummy, world=t.world, n_sent=t.n_sent, batches=t.n_batches,
+             coresident=t.coresident, hidden_ms=t.exchange_hidden_ms)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -46,7 +46,7 @@ def test_library_targets_gfx950():
 
 
 def test_abi_version():
-    assert boss.lib().mtg_boss_abi_version() == 7
+    assert boss.lib().mtg_boss_abi_version() == 8
 
 
 def test_invalid_arguments_fail_like_reference():
@@ -72,3 +72,15 @@ def test_bad_suffix_and_unknown_container_are_not_silently_accepted():
         boss.IBOSSChunkConstructor.initialize(3, filter_suffix="ACGT")
     with pytest.raises(RuntimeError, match="unknown container"):
         boss.IBOSSChunkConstructor.initialize(10, container_type=7)
+
+
+def test_coresident_count_tells_hosts_apart():
+    # identical nodes repeat the same PCI bus ids: a rank at the same slot of another host shares no
+    # HBM with this one (the bus id alone counted it co-resident and halved the budget)
+    bus = "0000:05:00.0"
+    assert boss.coresident([("nodeA", bus), ("nodeB", bus)], 0) == 1
+    assert boss.coresident([("nodeA", bus), ("nodeB", bus)], 1) == 1
+    # two ranks on one card of one host, a third on another card
+    ranks = [("nodeA", bus), ("nodeA", bus), ("nodeA", "0000:15:00.0"), ("nodeB", bus)]
+    assert [boss.coresident(ranks, r) for r in range(4)] == [2, 2, 1, 1]
+    assert boss.lib().mtg_device_identity(b"nodeA", bus.encode()) != boss.lib().mtg_device_identity(b"nodeB", bus.encode())

@@ -242,3 +242,21 @@ def test_dist_rounds_large_multi_tile(monkeypatch, collect):
     reads = _random_reads(78, 30000, 150, 400000, n_rate=0.0005)
     for P, canonical in ((2, True), (4, False), (8, True)):
         check_dist(30, reads, P, canonical, bits=8)
+
+
+@pytest.mark.parametrize("pieces", ["1", "2", "7"])
+def test_dist_exchange_pieces(monkeypatch, pieces):
+    # exchange 1 of the routed collect in pieces on the exchange stream, each piece sorted while the next
+    # is in flight (routed_pieces; 4 by default, 1 = one exchange then the sort): exact for every count,
+    # with counted keys, on lopsided ranks, and the overlap is reported
+    monkeypatch.setenv("MTG_DIST_PIECES", pieces)
+    reads = _random_reads(91, 20000, 150, 300000, n_rate=0.0005)
+    for P, canonical, bits in ((2, True, 0), (3, True, 8), (5, False, 16)):
+        ctors = []
+        check_dist(30, reads, P, canonical, bits, ctors_out=ctors)
+        for c in ctors:
+            t = c.timings()
+            assert t.exchange_ms > 0 and t.exchange_hidden_ms >= 0
+            if pieces == "1":
+                assert t.exchange_hidden_ms == 0
+    check_dist(30, reads[:3000], 4, True, 8, split="last")

@@ -27,7 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(tmp_path, reads, k, canonical, bits, world=2, env=None):
+def _run(tmp_path, reads, k, canonical, bits, world=2, env=None, rank_env=None):
     data, off = O.pack_sequences(reads)
     rp = str(tmp_path / "reads.npz")
     np.savez(rp, data=np.frombuffer(data, dtype=np.uint8), offsets=off)
@@ -36,7 +36,8 @@ def _run(tmp_path, reads, k, canonical, bits, world=2, env=None):
     e = dict(os.environ, **(env or {}))
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_build_worker.py"), str(r), str(world),
                                str(port), rp, outs[r], str(k), "1" if canonical else "0", str(bits)],
-                              env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                              env=dict(e, **(rank_env[r] if rank_env else {})), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT)
              for r in range(world)]
     logs = []
     for p in procs:
@@ -73,3 +74,17 @@ def test_two_process_gloo_exchange(tmp_path, k, canonical, bits, rounds):
     assert all(int(z["n_sent"]) > 0 for _, z in chunks)  # the ranks did exchange
     if rounds:
         assert all(int(z["batches"]) == rounds for _, z in chunks)
+
+
+@pytest.mark.parametrize("hosts", [("hostA", "hostA"), ("hostA", "hostB")])
+def test_two_process_coresident_count(tmp_path, hosts):
+    # both processes run on the box's one GPU: as one host they share it (coresident 2, each plans with
+    # half the free HBM); told they are two hosts (MTG_HOST_ID), the same PCI bus id no longer makes
+    # them co-resident.  The chunk is the oracle's either way
+    reads = _random_reads(77, 2000, 150, 20000, n_rate=0.001)
+    chunks = _run(tmp_path, reads, 30, True, 8, rank_env=[{"MTG_HOST_ID": h} for h in hosts])
+    want_n = 2 if hosts[0] == hosts[1] else 1
+    assert all(int(z["coresident"]) == want_n for _, z in chunks)
+    got = boss.concatenate([c for c, _ in chunks])
+    want = O.build_chunk(30, reads, canonical=True, bits_per_count=8)
+    assert np.array_equal(got.W, want.W) and np.array_equal(got.weights, want.weights)

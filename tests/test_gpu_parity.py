@@ -166,6 +166,35 @@ def test_device_build_matches_host_build():
         L.mtg_device_free(d)
 
 
+def test_trim_keeps_device_chunk_and_next_build():
+    # mtg_boss_ctor_trim frees the idle workspace blocks and the stage buffers but keeps the device
+    # chunk arrays (W, last, weights) valid; a second build on the same constructor is exact again
+    reads = _random_reads(5, 3000, 150, 40000, n_rate=0.001)
+    k = 30
+    data = b"".join(r + b"$" for r in reads)
+    L = boss.lib()
+    d = L.mtg_device_alloc(0, len(data))
+    try:
+        assert L.mtg_memcpy_h2d(d, data, len(data)) == 0
+        want = O.build_chunk(k, reads, canonical=True, bits_per_count=8)
+        ctor = boss.IBOSSChunkConstructor.initialize(k, both_strands=True, bits_per_count=8)
+        for rep in range(2):
+            dc = ctor.build_device(d, len(data))
+            ctor.trim()
+            assert ctor.timings().cached_bytes == 0
+            W = np.empty(dc.n, dtype=np.uint8)
+            last = np.empty(dc.n, dtype=np.uint8)
+            wt = np.empty(dc.n, dtype=np.uint32)
+            L.mtg_memcpy_d2h(W.ctypes.data, dc.W, dc.n)
+            L.mtg_memcpy_d2h(last.ctypes.data, dc.last, dc.n)
+            L.mtg_memcpy_d2h(wt.ctypes.data, dc.weights, dc.n * 4)
+            assert np.array_equal(W, want.W) and np.array_equal(last, want.last), rep
+            assert np.array_equal(wt, want.weights), rep
+            assert list(dc.F) == list(want.F), rep
+    finally:
+        L.mtg_device_free(d)
+
+
 @pytest.mark.parametrize("env", [{"MTG_EMIT": "slow"}, {"MTG_SORT": "lsd"}, {"MTG_FUSED_MIN": "0"}, {"MTG_DUMMY_SORT": "lifted"},
                                  {"MTG_FUSED": "0"}, {"MTG_FUSED_EMIT": "0"}, {"MTG_DUMMY_BITMAP": "1"},
                                  {"MTG_RC_FUSE": "0"}])
