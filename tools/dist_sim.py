@@ -32,6 +32,8 @@ def main():
                     help="one rank owns the device at a time (MTG_LOCAL_SERIAL): the step is the SUM of the "
                          "ranks' work, and each rank's device time is measured alone")
     ap.add_argument("--only-single", action="store_true", help="the single build only (its kernel profile)")
+    ap.add_argument("--pieces", type=int, default=None,
+                    help="exchange-1 pieces of the routed collect (MTG_DIST_PIECES; default: the library's)")
     ap.add_argument("--collect", default=None, choices=["routed", "superkmer", "local"],
                     help="the multi-GPU collect (MTG_DIST_COLLECT; default: the library's)")
     args = ap.parse_args()
@@ -61,6 +63,8 @@ def main():
 
     if args.serial:
         os.environ["MTG_LOCAL_SERIAL"] = "1"
+    if args.pieces:
+        os.environ["MTG_DIST_PIECES"] = str(args.pieces)
     if args.collect and args.collect != "routed":
         os.environ["MTG_DIST_COLLECT"] = args.collect
     comms = boss.Comm.local_group(P)
@@ -90,7 +94,7 @@ def main():
     per_rank = [c.timings().as_dict() for c in ctors]
     held = [cm.held_ms() / args.steps for cm in comms]
     keys = ("extract_ms", "sort_ms", "unique_ms", "rc_ms", "dummy_ms", "merge_ms", "emit_ms",
-            "total_ms", "exchange_ms")
+            "total_ms", "exchange_ms", "exchange_hidden_ms")
     print(json.dumps({
         "ranks": P, "reads_per_rank": args.reads, "rows": rows_single,
         "single_ms": t_single * 1e3, "dist_wall_ms": t_dist * 1e3, "serial": args.serial,
@@ -101,6 +105,7 @@ def main():
         "max_rank_ratio": round(P * max(held) / (t_single * 1e3), 3) if args.serial and t_single else None,
         "single_stages": {k: round(ts[k], 2) for k in keys if k in ts},
         "rank_stages": [{k: round(t[k], 2) for k in keys} for t in per_rank],
+        "pieces": os.environ.get("MTG_DIST_PIECES", "default"),
         "n_sent": [t["n_sent"] for t in per_rank],
         "sent_bytes": [t["sent_bytes"] for t in per_rank],
         "n_real": [t["n_real"] for t in per_rank],
