@@ -3696,9 +3696,9 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
                                        &hidden, tr);
             c.timings.exchange_ms += span;
             c.timings.exchange_hidden_ms += hidden;
-            for (auto sl : {Workspace::XA, Workspace::XB, Workspace::XAC, Workspace::XBC, Workspace::SPEC_A,
-                            Workspace::SPEC_B})
-                c.ws.release(sl);
+            // (the piece buffers stay in their slots for the next build of the same shape: given back, they
+            // went to the rc stage's requests and the next build allocated and freed them again, +3.7 ms a
+            // rank at P = 8)
             break;
         }
         // exchange 1: owner o gets the rank's buckets of its prefixes [bounds[o], bounds[o + 1]) (of

@@ -9,7 +9,7 @@ python3 "$R/tools/overlap.py" "$OUT/trace" > "$OUT/overlap.txt" 2>&1; tail -12 "
 cd "$R"
 for P in 2 8; do
   N=$((20000000 / P))
-  for pc in 1 4; do
+  for pc in 1 2 4; do
     timeout -k 10 300 python3 tools/dist_sim.py --ranks $P --reads $N --steps 3 --serial --pieces $pc > "$OUT/s${P}_p${pc}.json" 2> "$OUT/s${P}_p${pc}.err" || { echo "sim P=$P rc=$?"; tail -5 "$OUT/s${P}_p${pc}.err"; exit 1; }
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].split('/')[-1], 'held', d['rank_held_ms'], 'work', d['work_ratio'], 'single', round(d['single_ms'],2))" "$OUT/s${P}_p${pc}.json"
   done

@@ -24,11 +24,13 @@ for r in rows:
 tot_copy = tot_hidden = 0.0
 for th, ks in sorted(by_thread.items()):
     ks.sort()
-    copies = [k for k in ks if k[3] == "local_copy_kernel"]
+    copies = [k for k in ks if k[3].endswith("local_copy_kernel")]
     if not copies:
         continue
-    xstreams = {k[2] for k in copies}
-    # the exchange stream is the one the pieces' copies run on while build kernels run elsewhere
+    # the exchange stream runs nothing but copies (the build stream also runs the blocking exchanges' copies)
+    other = {k[2] for k in ks if not k[3].endswith("local_copy_kernel")}
+    xstreams = {k[2] for k in copies} - other
+    copies = [k for k in copies if k[2] in xstreams]
     work = [k for k in ks if k[2] not in xstreams]
     print("rank thread %s: %d kernels, %d exchange copies on stream(s) %s" % (th, len(ks), len(copies),
                                                                               sorted(xstreams)))
