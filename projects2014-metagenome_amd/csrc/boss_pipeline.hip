@@ -4086,6 +4086,21 @@ static void run_pipeline_dist(Ctx &c, Comm &comm, unsigned k, bool canonical, un
             rm.ib = bucket_bits<L2>(U + nrc, 2 * K);
             rm.istart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << rm.ib) + 2) * 8);
             const double dupm = nrc ? 2.0 * (double)nrc / ((double)d.P * (double)(nrc + U)) : 1.0;
+            if (nrc && U && !COUNTED) {
+                // the fused merge's speculative final level reads the owned canonical keys through their
+                // bucket index over that level's bits: the owner sort's own index when its final bits are
+                // the rc sort's, else one index pass here (the exchange pieces sort in several groups)
+                const MsdPlan rp = msd_plan<L2>(c, nrc, 2 * K, dupm);
+                const unsigned fb = rp.levels ? rp.digit_end[rp.levels] : 0;
+                if (fb && fb <= 26 &&
+                    !(c.gidx.keys == (const void *)xa && c.gidx.n == U && c.gidx.bits == fb && c.gidx.nbits == 2 * K)) {
+                    const uint64_t nbk = 1ull << fb;
+                    uint64_t *gi = (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nbk + 2) * 8);
+                    bucket_index<L2>(c, xa, U, 2 * K - fb, nbk, gi);
+                    HIP_CHECK(hipMemcpyAsync(gi + nbk + 1, gi + nbk, 8, hipMemcpyDeviceToDevice, c.stream));
+                    c.gidx = Ctx::GroupIndex{xa, U, fb, 2 * K, gi};
+                }
+            }
             uint64_t nr = 0;
             if (nrc)
                 nr = msd_sort_unique<L2, COUNTED>(c, &rkeys, &ralt, &rcc, &rcalt, nrc, 2 * K, cmax, dupm, nullptr, true,

@@ -54,6 +54,41 @@ __global__ __launch_bounds__(256) void copy_os8(const uint4 *__restrict__ s, uin
     for (int q = 0; q < 8; ++q) if (b0 + 256 * q < n) d[b0 + 256 * q] = v[q];
 }
 
+// e: one-shot, ONE 16 B per thread (the plain float4 copy)
+__global__ __launch_bounds__(256) void copy_os1(const uint4 *__restrict__ s, uint4 *__restrict__ d, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) d[i] = s[i];
+}
+// f: one-shot, 2 x 16 B per thread
+__global__ __launch_bounds__(256) void copy_os2(const uint4 *__restrict__ s, uint4 *__restrict__ d, uint64_t n) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * 512 + threadIdx.x;
+    uint4 v[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) if (b0 + 256 * q < n) v[q] = s[b0 + 256 * q];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) if (b0 + 256 * q < n) d[b0 + 256 * q] = v[q];
+}
+// g: one-shot 4 x 16 B with 16-byte nontemporal vector loads / stores (one instruction each)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int PER>
+__global__ __launch_bounds__(256) void copy_osv_nt(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, uint64_t n) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * (256 * PER) + threadIdx.x;
+    u32x4 v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) if (b0 + 256 * q < n) v[q] = __builtin_nontemporal_load(s + b0 + 256 * q);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) if (b0 + 256 * q < n) __builtin_nontemporal_store(v[q], d + b0 + 256 * q);
+}
+// h: one-shot 4 x 16 B, plain loads, nontemporal 16-byte stores
+__global__ __launch_bounds__(256) void copy_os4_ntst(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, uint64_t n) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    u32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) if (b0 + 256 * q < n) v[q] = s[b0 + 256 * q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) if (b0 + 256 * q < n) __builtin_nontemporal_store(v[q], d + b0 + 256 * q);
+}
+
 int main(int argc, char **argv) {
     const double gib = argc > 1 ? atof(argv[1]) : 4.0;
     const uint64_t bytes = (uint64_t)(gib * (1ull << 30)), n = bytes / 16;
@@ -86,6 +121,14 @@ int main(int argc, char **argv) {
     run("one-shot 4 x 16 B", [&] { copy_os4<<<dim3((unsigned)((n + 1023) / 1024)), dim3(256)>>>(s, d, n); });
     run("one-shot 4 x 16 B nt", [&] { copy_os4_nt<<<dim3((unsigned)((n + 1023) / 1024)), dim3(256)>>>(s, d, n); });
     run("one-shot 8 x 16 B", [&] { copy_os8<<<dim3((unsigned)((n + 2047) / 2048)), dim3(256)>>>(s, d, n); });
+    run("one-shot 1 x 16 B", [&] { copy_os1<<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(s, d, n); });
+    run("one-shot 2 x 16 B", [&] { copy_os2<<<dim3((unsigned)((n + 511) / 512)), dim3(256)>>>(s, d, n); });
+    const u32x4 *sv = (const u32x4 *)s;
+    u32x4 *dv = (u32x4 *)d;
+    run("one-shot 1 x 16 B nt-v", [&] { copy_osv_nt<1><<<dim3((unsigned)((n + 255) / 256)), dim3(256)>>>(sv, dv, n); });
+    run("one-shot 2 x 16 B nt-v", [&] { copy_osv_nt<2><<<dim3((unsigned)((n + 511) / 512)), dim3(256)>>>(sv, dv, n); });
+    run("one-shot 4 x 16 B nt-v", [&] { copy_osv_nt<4><<<dim3((unsigned)((n + 1023) / 1024)), dim3(256)>>>(sv, dv, n); });
+    run("one-shot 4 x 16 B nt-store", [&] { copy_os4_ntst<<<dim3((unsigned)((n + 1023) / 1024)), dim3(256)>>>(sv, dv, n); });
     run("hipMemcpyAsync D2D", [&] { CK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice)); });
     return 0;
 }
