@@ -361,3 +361,43 @@ def test_config3_share_dist_equals_single():
     a, b = out
     assert a[:3] == b[:3]
     assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+
+
+# configs[2] at its full size (k = 63, u128 keys, 100 M genome-sampled reads, 8.8e9 windows; the
+# canonical rounds of the fused u128 extraction, collect_mode 2): the oracle would take hours, so the
+# build is checked by order invariance -- the same reads in reverse order give the same arrays -- and
+# by its size identities (k odd: no palindromes, so the real edges are twice the canonical k-mers)
+@pytest.mark.timeout(900)
+def test_cfg3_full_size_order_invariant():
+    torch = pytest.importorskip("torch")
+    import gc
+    dev = torch.device("cuda", 0)
+    n_reads, L = 100_000_000, 150
+    seq = bench.make_reads_device(torch, n_reads, L, 1000, "genome", 10.0, dev)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    out = []
+    for rep in range(2):
+        if rep == 1:  # the reads in reverse order, each keeping its '$' separator (the first order freed)
+            seq = seq.view(n_reads, L + 1).flip(0).reshape(-1).contiguous()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        ctor = boss.IBOSSChunkConstructor.initialize(62, both_strands=True)
+        dc = ctor.build_device(seq.data_ptr(), seq.numel())
+        t = ctor.timings()
+        assert t.n_extracted == n_reads * (L - 63 + 1)
+        assert t.collect_mode == 2 and t.n_batches >= 2, (t.collect_mode, t.n_batches)
+        assert dc.n == t.n_rows == 1 + dc.n_real + dc.n_dummy
+        assert dc.n_real == 2 * t.n_unique
+        W, last, _ = _device_arrays(dc, 0)
+        F = [int(f) for f in dc.F]
+        assert W[0] == 0 and last[0] == 0 and last[-1] == 1
+        assert F == sorted(F) and F[4] <= dc.n - 1
+        out.append((dc.n, dc.n_real, F, W, last))
+        del dc, ctor
+        gc.collect()
+    del seq
+    torch.cuda.empty_cache()
+    a, b = out
+    assert a[:3] == b[:3]
+    assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
