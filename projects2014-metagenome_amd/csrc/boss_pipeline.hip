@@ -603,6 +603,12 @@ static void radix_sort(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals, uin
 
 __global__ void set_u64_kernel(uint64_t *p, uint64_t a) { *p = a; }
 
+// p[i] = v for i in [lo, hi)
+__global__ __launch_bounds__(256) void fill_u64_kernel(uint64_t *__restrict__ p, uint64_t lo, uint64_t hi, uint64_t v) {
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += T) p[i] = v;
+}
+
 __global__ void set_pair_kernel(uint64_t *p, uint64_t a, uint64_t b) {
     p[0] = a;
     p[1] = b;
@@ -893,7 +899,33 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             const bool gapped = c.gap.valid && c.gap.dst == (const void *)rm->ck;
             const Key<L> *ck = gapped ? (const Key<L> *)c.gap.keys : rm->ck;
             const uint64_t *cgap = gapped ? c.gap.bstart : nullptr;
-            bucket_pieces(0, nb, [&](uint64_t g0, unsigned cnt) {
+            // only the buckets either key set can occupy (a rank of a multi-GPU build owns ~1/P of them: the
+            // other workgroups only wrote index entries, 0.8 ms a rank-step at P = 8); the index entries
+            // outside them are 0 below and the merged count above
+            uint64_t mlo = 0, mhi = nb;
+            if (bp && !g1 && !gapped && rm->nc) {
+                Key<L> e[4];
+                HIP_CHECK(hipMemcpyAsync(&e[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipMemcpyAsync(&e[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipMemcpyAsync(&e[2], rm->ck, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipMemcpyAsync(&e[3], rm->ck + (rm->nc - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+                HIP_CHECK(hipStreamSynchronize(c.stream));
+                auto top = [&](const Key<L> &x) { return bits_at(shr(x, nbits - bp), 0, 32); };
+                mlo = std::min(top(e[0]), top(e[2])) << (bb - bp);
+                mhi = std::min<uint64_t>(nb, (std::max(top(e[1]), top(e[3])) + 1) << (bb - bp));
+                if (istart && mlo < mhi) {
+                    const uint64_t ilo = mlo << (rm->ib - bb), ihi = mhi << (rm->ib - bb), iend = 1ull << rm->ib;
+                    if (ilo) fill_u64_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(ilo, 256), 4096)), dim3(256), 0,
+                                               c.stream>>>(istart, 0, ilo, 0);
+                    if (ihi < iend)
+                        fill_u64_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(iend - ihi, 256), 4096)), dim3(256),
+                                          0, c.stream>>>(istart, ihi, iend, n + rm->nc);
+                    HIP_CHECK(hipGetLastError());
+                } else if (mlo >= mhi) {
+                    mlo = 0, mhi = nb;
+                }
+            }
+            bucket_pieces(mlo, mhi, [&](uint64_t g0, unsigned cnt) {
                 local_merge_kernel<L, COUNTED, CAP><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                     sa, sac, bstart, nullptr, nullptr, ck, rm->cv, cidx.start, rm->out, rm->outc, olist,
                     &c.small->counter, bb, nbits, rm->ib, istart, cur, gbase, cgap, g0, c.merge_it);
