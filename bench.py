@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # k=63 / 100 M-read u128 build that does not fit HBM in one pass and runs in key ranges)
 CONFIGS = {
     "cfg2": {"k": 31, "reads": 10_000_000},
-    "cfg3": {"k": 63, "reads": 100_000_000, "host_steps": 0, "cpu_sample_reads": 500_000,
+    "cfg3": {"k": 63, "reads": 100_000_000, "host_steps": 0, "cpu_sample_reads": 5_000_000,
              "steps": 2, "warmup": 1},
     # configs[3]: k=31, 1 B reads over 8 GPUs = 125 M reads per GPU on one shared genome (10x over
     # all ranks' reads); one share does not fit one pass, so every rank collects in key batches
