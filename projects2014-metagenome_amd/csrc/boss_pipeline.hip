@@ -66,7 +66,7 @@ class Workspace {
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
         FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, RC_L1START, RC_L1CUR, RC_TILEG,
-        KA2, ROUND_DELTA, NSLOTS
+        KA2, ROUND_DELTA, XA2, XAC2, CA2, NSLOTS
     };
     ~Workspace() {
         for (auto &b : bufs_)
@@ -138,7 +138,7 @@ class Workspace {
         for (Slot sl : {KA, KB, CA, CB, SUMS, BUCKETS, FLAGS, DA, DB, STREAM, SCOUNT, OW, OLAST, OWEIGHTS, FB_K, FB_V,
                         RC_ALT, RC_ALTC, REAL, REALC, INFLAG, XA, XAC, XB, XBC, QSEND, QRECV, QFLAG, DSRC, DSEND,
                         DRECV, RC_SENDC, LAST_BITS, W4, WN, DPOS, DWL, CANON, CANONC, CANON_IDX, SPEC_A, SPEC_B,
-                        SPEC_AC, SPEC_BC, KA2})
+                        SPEC_AC, SPEC_BC, KA2, XA2, XAC2, CA2})
             if (!keep_outputs || (sl != OW && sl != OLAST && sl != OWEIGHTS)) release(sl);
     }
     // a slot gives its buffer back (batched builds drop their round buffers before the later stages
@@ -3525,6 +3525,127 @@ static uint64_t routed_pieces(Ctx &c, Dist &d, unsigned K, uint32_t cmax, const 
     return off;
 }
 
+// The routed collect's rounds with every exchange in flight under compute (configs[3]'s shares, 125 M
+// reads a GPU, collect in rounds).  Round r's exchange 1 goes out on the exchange stream as soon as its
+// pass B ends, so it runs under pass B of round r + 1 and under the owner sort of round r - 1; the send
+// buffers (KA / KA2) and receive buffers (XA / XA2) alternate between even and odd rounds, and each is
+// reused only once the exchange or sort that read it has ended (stream events).  Build-stream order:
+// B0, B1, S0, B2, S1, ...; exchange-stream order: X0, X1, X2, ... (X_r after B_r and S_r-2).  Every
+// round's send counts are known from pass A's histogram, so one all-gather sizes every receive.
+// The merge semantics are the serial rounds' (sorted_multiset.cpp:54-84); the reference has no runtime
+// exchange (cli/build.cpp:106-148).  *span_ms / *hidden_ms: exchange time, and the part of it the build
+// stream spent computing.
+template <bool COUNTED, class Layout, class PassB, class Sort, class Append>
+static void routed_rounds_pipelined(Ctx &c, Dist &d, uint32_t R, Layout &round_layout, PassB &pass_b,
+                                    Sort &owner_sort, Append &append, const std::vector<std::vector<uint64_t>> &sub,
+                                    uint32_t nb1, Tracer &tr, double *span_ms, double *hidden_ms) {
+    using K2 = Key<1>;
+    const int P = d.P;
+    std::vector<BucketSel> sel(R);
+    std::vector<std::vector<unsigned long long>> cur(R);
+    std::vector<uint64_t> nr(R);
+    for (uint32_t r = 0; r < R; ++r) nr[r] = round_layout(r, sel[r], cur[r]);
+    auto at = [&](uint32_t r, uint64_t b) -> uint64_t { return b >= nb1 ? nr[r] : cur[r][b]; };
+    // this rank's slices (round-major, then owner) and every rank's counts
+    const size_t V = (size_t)R * P;
+    std::vector<uint64_t> scnt(V), soff(V);
+    for (uint32_t r = 0; r < R; ++r)
+        for (int o = 0; o < P; ++o) {
+            soff[r * P + o] = at(r, sub[o][r]);
+            scnt[r * P + o] = at(r, sub[o][r + 1]) - soff[r * P + o];
+        }
+    uint64_t *dm = (uint64_t *)c.ws.get(Workspace::XMAT, (V + V * P) * 8);
+    HIP_CHECK(hipMemcpyAsync(dm, scnt.data(), V * 8, hipMemcpyHostToDevice, c.stream));
+    const int e0 = d.tm->mark();
+    d.comm.allgather_u64(dm, dm + V, V, c.stream);
+    d.xev.push_back({e0, d.tm->mark()});
+    std::vector<uint64_t> mat(V * P);
+    HIP_CHECK(hipMemcpyAsync(mat.data(), dm + V, V * P * 8, hipMemcpyDeviceToHost, c.stream));
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    std::vector<uint64_t> rcnt(V), roff(V), n1(R, 0);
+    for (uint32_t r = 0; r < R; ++r)
+        for (int i = 0; i < P; ++i) {
+            rcnt[r * P + i] = mat[(size_t)i * V + r * P + d.me];
+            roff[r * P + i] = n1[r];
+            n1[r] += rcnt[r * P + i];
+        }
+    // the buffers of both parities, sized before the first exchange leaves (a slot that grows synchronizes
+    // the device)
+    uint64_t mk[2] = {1, 1}, mx[2] = {1, 1}, mb = 1;
+    for (uint32_t r = 0; r < R; ++r) {
+        mk[r & 1] = std::max(mk[r & 1], nr[r]);
+        mx[r & 1] = std::max(mx[r & 1], n1[r]);
+        mb = std::max(mb, n1[r]);
+    }
+    K2 *ka[2] = {(K2 *)c.ws.get(Workspace::KA, mk[0] * sizeof(K2)), (K2 *)c.ws.get(Workspace::KA2, mk[1] * sizeof(K2))};
+    K2 *xr[2] = {(K2 *)c.ws.get(Workspace::XA, mx[0] * sizeof(K2)), (K2 *)c.ws.get(Workspace::XA2, mx[1] * sizeof(K2))};
+    K2 *xb = (K2 *)c.ws.get(Workspace::XB, mb * sizeof(K2));
+    uint32_t *ca[2] = {nullptr, nullptr}, *xrc[2] = {nullptr, nullptr}, *xbc = nullptr;
+    if (COUNTED) {
+        ca[0] = (uint32_t *)c.ws.get(Workspace::CA, mk[0] * 4);
+        ca[1] = (uint32_t *)c.ws.get(Workspace::CA2, mk[1] * 4);
+        xrc[0] = (uint32_t *)c.ws.get(Workspace::XAC, mx[0] * 4);
+        xrc[1] = (uint32_t *)c.ws.get(Workspace::XAC2, mx[1] * 4);
+        xbc = (uint32_t *)c.ws.get(Workspace::XBC, mb * 4);
+    }
+    if (!c.xstream) HIP_CHECK(hipStreamCreateWithFlags(&c.xstream, hipStreamNonBlocking));
+    hipStream_t xs = c.xstream;
+    // per round: pass B done, exchange start / end (exchange stream), build stream free before the sort's wait,
+    // sort + append done
+    std::vector<hipEvent_t> ev(5 * (size_t)R);
+    for (auto &e : ev) HIP_CHECK(hipEventCreate(&e));
+    struct EvFree {
+        std::vector<hipEvent_t> &v;
+        ~EvFree() {
+            for (auto e : v) (void)hipEventDestroy(e);
+        }
+    } ev_free{ev};
+    hipEvent_t *evB = ev.data(), *evXs = evB + R, *evX = evXs + R, *evC = evX + R, *evS = evC + R;
+    std::vector<std::vector<uint32_t>> hown(R);  // the owner sorts' level-1 counts (copied asynchronously)
+    auto issue = [&](uint32_t r) {  // pass B of round r, then its exchange
+        const int p = r & 1;
+        if (r >= 2) HIP_CHECK(hipStreamWaitEvent(c.stream, evX[r - 2], 0));  // ka[p] read by exchange r - 2
+        pass_b(&sel[r], cur[r], ka[p], ca[p]);
+        HIP_CHECK(hipEventRecord(evB[r], c.stream));
+        tr("rounds: pass B", r, nr[r]);
+        HIP_CHECK(hipStreamWaitEvent(xs, evB[r], 0));
+        if (r >= 2) HIP_CHECK(hipStreamWaitEvent(xs, evS[r - 2], 0));  // xr[p] read by the sort of round r - 2
+        HIP_CHECK(hipEventRecord(evXs[r], xs));
+        d.comm.alltoallv_async(ka[p], &scnt[r * P], &soff[r * P], xr[p], &rcnt[r * P], &roff[r * P], sizeof(K2), xs);
+        if (COUNTED)
+            d.comm.alltoallv_async(ca[p], &scnt[r * P], &soff[r * P], xrc[p], &rcnt[r * P], &roff[r * P], 4, xs);
+        HIP_CHECK(hipEventRecord(evX[r], xs));
+        for (int j = 0; j < P; ++j)
+            if (j != d.me) c.timings.n_sent += scnt[r * P + j];
+    };
+    issue(0);
+    for (uint32_t r = 1; r <= R; ++r) {
+        if (r < R) issue(r);
+        const uint32_t q = r - 1;
+        HIP_CHECK(hipEventRecord(evC[q], c.stream));
+        HIP_CHECK(hipStreamWaitEvent(c.stream, evX[q], 0));
+        K2 *pa = xr[q & 1], *pb = xb;
+        uint32_t *pac = xrc[q & 1], *pbc = xbc;
+        const uint64_t rb0 = sub[d.me][q], rb1 = sub[d.me][q + 1];
+        const uint64_t Ur = owner_sort(&pa, &pb, &pac, &pbc, n1[q], rb0, rb1, hown[q], q == 0, false);
+        append(pa, pac, Ur, rb0, rb1);
+        HIP_CHECK(hipEventRecord(evS[q], c.stream));
+        tr("rounds: exchange + owner sort", q, Ur);
+    }
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    HIP_CHECK(hipStreamSynchronize(xs));
+    double span = 0, exposed = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        float t = 0;
+        HIP_CHECK(hipEventElapsedTime(&t, evXs[r], evX[r]));
+        span += t;
+        HIP_CHECK(hipEventElapsedTime(&t, evC[r], evX[r]));
+        exposed += std::max(0.0f, t);
+    }
+    *span_ms = span;
+    *hidden_ms = std::max(0.0, span - exposed);
+}
+
 template <bool COUNTED>
 static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                                 Key<1> **xa_out, uint32_t **xac_out, uint64_t *U_out, std::vector<uint64_t> *bounds,
@@ -3620,25 +3741,32 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     // any rank needs).  The key-range collect (collect_ranges_dist) re-scanned every read per range
     // and extracted both strands.
     uint32_t rounds = 1;
+    bool pipe_ok = false;  // the rounds' exchanges pipelined (routed_rounds_pipelined)
     {
         uint64_t want = c.force_ranges;
+        const double budget = dist_budget(c, d);
+        const double per_key = 8.0 + (COUNTED ? 4.0 : 0.0);
         if (!want) {
-            const double budget = dist_budget(c, d);
-            const double per_key = 8.0 + (COUNTED ? 4.0 : 0.0);
             // one pass: the rank's keys, the received runs and their ping-pong buffer, plus ~3 N of later
             // stages (the owned canonical set, its rc keys, the real edges) at low duplication
             const double need = (double)N * per_key * 3.0;
             want = need * 2.0 <= budget ? 1 : (uint64_t)std::ceil(need / (0.45 * budget));
         }
-        uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, (1 + (uint64_t)d.P) * 8);
-        HIP_CHECK(hipMemcpyAsync(dv, &want, 8, hipMemcpyHostToDevice, c.stream));
-        d.comm.allgather_u64(dv, dv + 1, 1, c.stream);
-        std::vector<uint64_t> all(d.P);
-        HIP_CHECK(hipMemcpyAsync(all.data(), dv + 1, (uint64_t)d.P * 8, hipMemcpyDeviceToHost, c.stream));
-        HIP_CHECK(hipStreamSynchronize(c.stream));  // `want` is a host local
-        uint64_t r = 1;
-        for (uint64_t v : all) r = std::max(r, v);
+        // every rank's wish, key count and budget: all ranks then take the same count and decide alike
+        // whether two rounds' send and receive buffers fit (5 round-sized buffers instead of 3)
+        const uint64_t mine[3] = {want, N, (uint64_t)budget};
+        uint64_t *dv = (uint64_t *)c.ws.get(Workspace::XMAT, (3 + 3 * (uint64_t)d.P) * 8);
+        HIP_CHECK(hipMemcpyAsync(dv, mine, 24, hipMemcpyHostToDevice, c.stream));
+        d.comm.allgather_u64(dv, dv + 3, 3, c.stream);
+        std::vector<uint64_t> all(3 * (size_t)d.P);
+        HIP_CHECK(hipMemcpyAsync(all.data(), dv + 3, all.size() * 8, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // `mine` is a host local
+        uint64_t r = 1, nmax = 0;
+        for (int i = 0; i < d.P; ++i) r = std::max(r, all[3 * i]), nmax = std::max(nmax, all[3 * i + 1]);
         rounds = (uint32_t)std::min<uint64_t>(r, 64);
+        pipe_ok = c.dist_pieces > 1;
+        for (int i = 0; i < d.P && pipe_ok && !c.force_ranges; ++i)
+            pipe_ok = 5.0 * (double)nmax / rounds * per_key <= 0.6 * (double)all[3 * i + 2];
     }
     // global level-1 counts, and every owner's bucket interval cut into the rounds
     std::vector<uint64_t> gh1(nb1, 0);
@@ -3665,60 +3793,131 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
     K2 *xa = nullptr;
     uint32_t *xac = nullptr;
     uint64_t U = 0;
-    for (uint32_t r = 0; r < rounds; ++r) {
-        BucketSel sel;
+    // the round's level-1 layout of this rank's k-mers: bucket starts (and ends at nb1 + i) of the buckets
+    // its mask keeps (every bucket in a one-round build)
+    auto round_layout = [&](uint32_t r, BucketSel &sel, std::vector<unsigned long long> &cur) -> uint64_t {
         for (int o = 0; o < d.P; ++o) sel.add(sub[o][r], sub[o][r + 1]);
-        const BucketSel *rs = rounds > 1 ? &sel : nullptr;
-        // pass B: this rank's k-mers (of the round's buckets) scattered by their top B1 bits (the single
-        // build's fused pass)
         std::vector<uint32_t> h1(nb1, 0);
         for (uint32_t i = 0; i < NBH; ++i) {
             const uint32_t b = i >> (FUSED_HB - B1);
-            if (!rs || rs->has(b)) h1[b] += hl[i];
+            if (rounds == 1 || sel.has(b)) h1[b] += hl[i];
         }
-        std::vector<unsigned long long> cur(2 * nb1);
+        cur.assign(2 * nb1, 0);
         unsigned long long nr = 0;
         for (uint32_t i = 0; i < nb1; ++i) {
             cur[i] = nr;
             nr += h1[i];
         }
         for (uint32_t i = 0; i < nb1; ++i) cur[nb1 + i] = cur[i] + h1[i];
+        return nr;
+    };
+    // pass B: this rank's k-mers (of the round's buckets) scattered by their top B1 bits into ka (the single
+    // build's fused pass)
+    auto pass_b = [&](const BucketSel *rs, const std::vector<unsigned long long> &cur, K2 *ka, uint32_t *ca) {
+        if (!nrows) return;
+        uint32_t *dsel = nullptr;
+        if (rs) {
+            dsel = (uint32_t *)c.ws.get(Workspace::FUSED_SEL, sizeof(rs->m));
+            HIP_CHECK(hipMemcpyAsync(dsel, rs->m, sizeof(rs->m), hipMemcpyHostToDevice, c.stream));
+        }
+        unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
+        HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
+        auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
+        unsigned long long *send = scur + (size_t)stripes * nb1;
+        stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, FUSED_HB, B1, stripes, rps, dcur,
+                                                                     scur, send, dsel);
+        HIP_CHECK(hipGetLastError());
+        if (!COUNTED && B1 > 9) {
+            launch_part_fast<512, 1024>(c, K, dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), in.seq,
+                                        in.seq_len, K, cmode, B1, per_stripe, scur, send, ka, &c.small->error,
+                                        (const uint32_t *)dsel, (uint32_t *)nullptr);
+        } else if (!COUNTED) {
+            launch_part_fast<512, 512>(c, K, dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), in.seq,
+                                       in.seq_len, K, cmode, B1, per_stripe, scur, send, ka, &c.small->error,
+                                       (const uint32_t *)dsel, (uint32_t *)nullptr);
+        } else {
+            if (B1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
+            const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
+            extract_partition_kernel<1, COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+                in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
+                B1, per_stripe, scur, send, ka, ca, &c.small->error, dsel);
+        }
+        HIP_CHECK(hipGetLastError());
+        cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
+            scur, send, stripes * nb1, &c.small->error);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(c.stream));  // cur / sel are host memory
+    };
+    // the owner's sort of one round's (or piece's) received keys: level 1 is the routing digit (its counts
+    // from the global pass-A histogram over the owned buckets [rb0, rb1)), level 2 partitions the runs in any
+    // order; returns the distinct keys, left in *pa
+    auto owner_sort = [&](K2 **pa, K2 **pb, uint32_t **pac, uint32_t **pbc, uint64_t n1, uint64_t rb0, uint64_t rb1,
+                          std::vector<uint32_t> &hown, bool track, bool gidx) -> uint64_t {
+        hown.assign(nb1, 0);
+        uint64_t nown = 0;
+        for (uint32_t i = 0; i < NBH; ++i) {
+            const uint32_t b = i >> (FUSED_HB - B1);
+            if (b >= rb0 && b < rb1) {
+                hown[b] += (uint32_t)H[i];
+                nown += H[i];
+            }
+        }
+        if (nown != n1) throw std::runtime_error("received k-mers differ from the global histogram of the owned range");
+        if (!n1) return 0;
+        uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
+        HIP_CHECK(hipMemcpyAsync(dh1, hown.data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
+        const double spread = (double)nb1 / (double)std::max<uint64_t>(1, rb1 - rb0);
+        const double dup = estimate_dup<1>(c, *pa, n1, 8.0) / spread;
+        MsdPlan plan = msd_plan<1>(c, n1, 2 * K, dup);
+        unsigned T = plan.levels ? plan.digit_end[plan.levels] : 0;
+        T = std::min(2 * K, std::max(T, B1 + 1));  // at least one partition pass after the routing digit
+        MsdPlan fp{};
+        fp.levels = 1 + (T - B1 + MSD_DBITS - 1) / MSD_DBITS;
+        fp.digit_end[1] = B1;
+        for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
+        c.track_partition = track;
+        c.want_gidx = gidx;
+        const uint64_t u = msd_sort_unique<1, COUNTED>(c, pa, pb, pac, pbc, n1, 2 * K, cmax, dup, dh1, false, nullptr,
+                                                       true, nullptr, &fp);
+        c.want_gidx = false;
+        c.track_partition = false;
+        return u;
+    };
+    // the rounds' distinct keys appended to the owned canonical set (sized from the first filled round's
+    // share of the owner's range, +25 %)
+    auto append = [&](const K2 *src, const uint32_t *srcc, uint64_t Ur, uint64_t rb0, uint64_t rb1) {
+        if (off + Ur > cap) {
+            uint64_t gr = 0, go = 0;
+            for (uint64_t b = rb0; b < rb1; ++b) gr += gh1[b];
+            for (uint64_t b = ob0; b < ob1; ++b) go += gh1[b];
+            const uint64_t want = off == 0 && gr ? (uint64_t)((double)Ur / (double)gr * (double)go * 1.25) + Ur
+                                                 : (off + Ur) + (off + Ur) / 4;
+            cap = std::max(want, off + Ur);
+            acc = (K2 *)c.ws.get(Workspace::CANON, cap * sizeof(K2), off * sizeof(K2), c.stream);
+            if (COUNTED) accc = (uint32_t *)c.ws.get(Workspace::CANONC, cap * 4, off * 4, c.stream);
+        }
+        if (Ur) {
+            HIP_CHECK(hipMemcpyAsync(acc + off, src, Ur * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+            if (COUNTED) HIP_CHECK(hipMemcpyAsync(accc + off, srcc, Ur * 4, hipMemcpyDeviceToDevice, c.stream));
+        }
+        off += Ur;
+    };
+    const bool pipe_rounds = rounds > 1 && d.P > 1 && pipe_ok;
+    if (pipe_rounds) {
+        double span = 0, hidden = 0;
+        routed_rounds_pipelined<COUNTED>(c, d, rounds, round_layout, pass_b, owner_sort, append, sub, nb1, tr, &span,
+                                         &hidden);
+        c.timings.exchange_ms += span;
+        c.timings.exchange_hidden_ms += hidden;
+    }
+    for (uint32_t r = 0; r < (pipe_rounds ? 0u : rounds); ++r) {
+        BucketSel sel;
+        std::vector<unsigned long long> cur;
+        const uint64_t nr = round_layout(r, sel, cur);
+        const BucketSel *rs = rounds > 1 ? &sel : nullptr;
         K2 *ka = (K2 *)c.ws.get(Workspace::KA, std::max<uint64_t>(nr, 1) * 8);
         uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, std::max<uint64_t>(nr, 1) * 4) : nullptr;
-        if (nrows) {
-            uint32_t *dsel = nullptr;
-            if (rs) {
-                dsel = (uint32_t *)c.ws.get(Workspace::FUSED_SEL, sizeof(rs->m));
-                HIP_CHECK(hipMemcpyAsync(dsel, rs->m, sizeof(rs->m), hipMemcpyHostToDevice, c.stream));
-            }
-            unsigned long long *dcur = (unsigned long long *)c.ws.get(Workspace::FUSED_CUR, cur.size() * 8);
-            HIP_CHECK(hipMemcpyAsync(dcur, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, c.stream));
-            auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, (size_t)stripes * nb1 * 16);
-            unsigned long long *send = scur + (size_t)stripes * nb1;
-            stripe_cursor_kernel<<<dim3(nb1), dim3(256), 0, c.stream>>>(rows, nrows, FUSED_HB, B1, stripes, rps, dcur,
-                                                                         scur, send, dsel);
-            HIP_CHECK(hipGetLastError());
-            if (!COUNTED && B1 > 9) {
-                launch_part_fast<512, 1024>(c, K, dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), in.seq,
-                                            in.seq_len, K, cmode, B1, per_stripe, scur, send, ka, &c.small->error,
-                                            (const uint32_t *)dsel, (uint32_t *)nullptr);
-            } else if (!COUNTED) {
-                launch_part_fast<512, 512>(c, K, dim3((unsigned)xcd_grid(ceil_div(npos, 16 * 512))), dim3(512), in.seq,
-                                           in.seq_len, K, cmode, B1, per_stripe, scur, send, ka, &c.small->error,
-                                           (const uint32_t *)dsel, (uint32_t *)nullptr);
-            } else {
-                if (B1 > 9) throw std::runtime_error("the counted pass B takes at most 9 bits");
-                const uint64_t ftiles = ceil_div(npos, FusedTraits<COUNTED, 512>::TILE);
-                extract_partition_kernel<1, COUNTED, 512><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
-                    in.seq, in.seq_len, K, cmode, in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax,
-                    B1, per_stripe, scur, send, ka, ca, &c.small->error, dsel);
-            }
-            HIP_CHECK(hipGetLastError());
-            cursor_check_kernel<<<dim3((unsigned)ceil_div((uint64_t)stripes * nb1, 256)), dim3(256), 0, c.stream>>>(
-                scur, send, stripes * nb1, &c.small->error);
-            HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipStreamSynchronize(c.stream));  // cur / sel are host memory
-        }
+        pass_b(rs, cur, ka, ca);
         if (rounds == 1) *ev_extract = tm.mark();
         tr("extract + scatter", nr);
         if (rounds == 1 && d.P > 1 && c.dist_pieces > 1) {
@@ -3755,61 +3954,21 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
         tr("exchange 1", n1);
         // the owner's level-1 counts: the global pass-A histogram over its buckets (of this round)
         const uint64_t rb0 = rs ? sub[d.me][r] : ob0, rb1 = rs ? sub[d.me][r + 1] : ob1;
-        std::vector<uint32_t> hown(nb1, 0);
-        uint64_t nown = 0;
-        for (uint32_t i = 0; i < NBH; ++i) {
-            const uint32_t b = i >> (FUSED_HB - B1);
-            if (b >= rb0 && b < rb1) {
-                hown[b] += (uint32_t)H[i];
-                nown += H[i];
-            }
-        }
-        if (nown != n1) throw std::runtime_error("received k-mers differ from the global histogram of the owned range");
-        uint32_t *dh1 = (uint32_t *)c.ws.get(Workspace::HIST1, nb1 * 4);
-        HIP_CHECK(hipMemcpyAsync(dh1, hown.data(), nb1 * 4, hipMemcpyHostToDevice, c.stream));
-        // plan: the keys fill (rb1 - rb0) of the nb1 level-1 buckets; level 1 is "done" (the buckets are
-        // known from the histogram), level 2 partitions the P runs in one pass (any input order)
+        std::vector<uint32_t> hown;
         uint64_t Ur = 0;
         if (n1) {
             K2 *xb = (K2 *)c.ws.get(Workspace::XB, n1 * sizeof(K2));
             uint32_t *xbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::XBC, n1 * 4) : nullptr;
-            const double spread = (double)nb1 / (double)std::max<uint64_t>(1, rb1 - rb0);
-            const double dup = estimate_dup<1>(c, xa, n1, 8.0) / spread;
-            MsdPlan plan = msd_plan<1>(c, n1, 2 * K, dup);
-            unsigned T = plan.levels ? plan.digit_end[plan.levels] : 0;
-            T = std::min(2 * K, std::max(T, B1 + 1));  // at least one partition pass after the routing digit
-            MsdPlan fp{};
-            fp.levels = 1 + (T - B1 + MSD_DBITS - 1) / MSD_DBITS;
-            fp.digit_end[1] = B1;
-            for (unsigned l = 2; l <= fp.levels; ++l) fp.digit_end[l] = B1 + (T - B1) * (l - 1) / (fp.levels - 1);
-            c.track_partition = r == 0;
-            c.want_gidx = canonical && rounds == 1;
-            Ur = msd_sort_unique<1, COUNTED>(c, &xa, &xb, &xac, &xbc, n1, 2 * K, cmax, dup, dh1, false, nullptr, true,
-                                             nullptr, &fp);
-            c.want_gidx = false;
-            c.track_partition = false;
+            Ur = owner_sort(&xa, &xb, &xac, &xbc, n1, rb0, rb1, hown, r == 0, canonical && rounds == 1);
+        } else {
+            owner_sort(&xa, &xa, &xac, &xac, 0, rb0, rb1, hown, false, false);  // (checks the count)
         }
         tr("owner sort", Ur);
         if (rounds == 1) {
             U = Ur;
             break;
         }
-        if (off + Ur > cap) {
-            // first filled round: size the owned set from its share of the owner's range (+25 %)
-            uint64_t gr = 0, go = 0;
-            for (uint64_t b = rb0; b < rb1; ++b) gr += gh1[b];
-            for (uint64_t b = ob0; b < ob1; ++b) go += gh1[b];
-            const uint64_t want = off == 0 && gr ? (uint64_t)((double)Ur / (double)gr * (double)go * 1.25) + Ur
-                                                 : (off + Ur) + (off + Ur) / 4;
-            cap = std::max(want, off + Ur);
-            acc = (K2 *)c.ws.get(Workspace::CANON, cap * sizeof(K2), off * sizeof(K2), c.stream);
-            if (COUNTED) accc = (uint32_t *)c.ws.get(Workspace::CANONC, cap * 4, off * 4, c.stream);
-        }
-        if (Ur) {
-            HIP_CHECK(hipMemcpyAsync(acc + off, xa, Ur * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
-            if (COUNTED) HIP_CHECK(hipMemcpyAsync(accc + off, xac, Ur * 4, hipMemcpyDeviceToDevice, c.stream));
-        }
-        off += Ur;
+        append(xa, xac, Ur, rb0, rb1);
     }
     if (rounds > 1) {
         if (!acc) {

@@ -260,3 +260,24 @@ def test_dist_exchange_pieces(monkeypatch, pieces):
             if pieces == "1":
                 assert t.exchange_hidden_ms == 0
     check_dist(30, reads[:3000], 4, True, 8, split="last")
+
+
+@pytest.mark.parametrize("pieces", ["1", "4"])
+@pytest.mark.parametrize("rounds", ["2", "5"])
+def test_dist_rounds_exchange_pipelined(monkeypatch, pieces, rounds):
+    # the routed rounds with each round's exchange in flight under the next round's pass B and the
+    # previous round's owner sort (routed_rounds_pipelined: alternating send / receive buffers ordered
+    # by stream events), and the serial rounds (MTG_DIST_PIECES=1): both exact, counted and not
+    monkeypatch.setenv("MTG_RANGES", rounds)
+    monkeypatch.setenv("MTG_DIST_PIECES", pieces)
+    reads = _random_reads(93, 12000, 150, 200000, n_rate=0.0005)
+    for P, canonical, bits in ((2, True, 0), (3, True, 8), (4, False, 16)):
+        ctors = []
+        check_dist(30, reads, P, canonical, bits, ctors_out=ctors)
+        for c in ctors:
+            t = c.timings()
+            assert t.n_batches == int(rounds) and t.collect_mode == 2
+            assert t.exchange_ms > 0 and t.exchange_hidden_ms >= 0
+            if pieces == "1":
+                assert t.exchange_hidden_ms == 0
+    check_dist(30, reads[:2000], 3, True, 8, split="last")

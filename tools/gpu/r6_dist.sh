@@ -11,8 +11,10 @@ for P in 2 8; do
   N=$((20000000 / P))
   for pc in 1 2 4; do
     timeout -k 10 300 python3 tools/dist_sim.py --ranks $P --reads $N --steps 3 --serial --pieces $pc > "$OUT/s${P}_p${pc}.json" 2> "$OUT/s${P}_p${pc}.err" || { echo "sim P=$P rc=$?"; tail -5 "$OUT/s${P}_p${pc}.err"; exit 1; }
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].split('/')[-1], 'held', d['rank_held_ms'], 'work', d['work_ratio'], 'single', round(d['single_ms'],2))" "$OUT/s${P}_p${pc}.json"
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].split('/')[-1], 'held', d['rank_held_ms'], 'work', d['work_ratio'], 'single', round(d['single_ms'],2), 'sent GB', round(max(d['sent_bytes'])/1e9,3))" "$OUT/s${P}_p${pc}.json"
   done
+  timeout -k 10 300 python3 tools/dist_sim.py --ranks $P --reads $N --steps 3 --serial --collect local > "$OUT/s${P}_local.json" 2> "$OUT/s${P}_local.err" || { echo "sim local P=$P rc=$?"; tail -5 "$OUT/s${P}_local.err"; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].split('/')[-1], 'held', d['rank_held_ms'], 'work', d['work_ratio'], 'sent GB', round(max(d['sent_bytes'])/1e9,3))" "$OUT/s${P}_local.json"
   timeout -k 10 300 python3 tools/dist_sim.py --ranks $P --reads $N --steps 3 --no-single > "$OUT/c${P}.json" 2> "$OUT/c${P}.err" || { echo "conc P=$P rc=$?"; tail -5 "$OUT/c${P}.err"; exit 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1].split('/')[-1], 'wall', round(d['dist_wall_ms'],2), [ (s['exchange_ms'], s['exchange_hidden_ms']) for s in d['rank_stages']])" "$OUT/c${P}.json"
 done
