@@ -396,10 +396,11 @@ def fasta_path(args, kb, boss, steps, n_reads, files=8):
 
 
 def measured_copy_peak(torch, boss, device, nbytes=4 << 30, reps=10):
-    """Achievable HBM bandwidth on this GPU: the library's one-shot nontemporal 16-byte-lane copy
-    kernel (mtg_device_copy; tools/copy_bench.hip compares copy shapes) over `nbytes` (read + write), timed with HIP events on torch's current
-    stream; the second roofline denominator BASELINE.md asks for (the best of torch's copy_ and
-    that kernel)."""
+    """Achievable HBM bandwidth on this GPU: the library's copy kernel (mtg_device_copy: one 16-byte
+    nontemporal load + store per thread, 6.44 TB/s on the MI355X in tools/copy_bench.hip, which compares
+    copy shapes; profiles/r6_copy_bench.txt) over `nbytes` (read + write), timed with HIP events on
+    torch's current stream; the second roofline denominator BASELINE.md asks for (the best of torch's
+    copy_ and that kernel)."""
     src = torch.empty(nbytes, dtype=torch.uint8, device=device)
     dst = torch.empty_like(src)
     src.fill_(1)
@@ -658,8 +659,8 @@ def main():
                      "traffic_source": traffic_src,
                      "peak_measured": copy_peak,
                      "frac_measured": achieved / copy_peak if copy_peak else None,
-                     "peak_measured_how": "best of a one-shot nontemporal 16-byte-lane copy kernel and torch copy_ "
-                                          "over 4 GiB (read + write), HIP events",
+                     "peak_measured_how": "best of a copy kernel with one 16-byte nontemporal load + store per "
+                                          "thread and torch copy_ over 4 GiB (read + write), HIP events",
                      "kernel": "msd_partition_kernel (K2 level-2 MSD partition pass; level 1 runs "
                                "inside the fused K1 extract_partition_kernel)",
                      "pass_ms": pass_ms, "bytes_per_launch": pass_bytes},

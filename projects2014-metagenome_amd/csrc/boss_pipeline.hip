@@ -6308,37 +6308,25 @@ int mtg_memcpy_d2h(void *dst, const void *src, uint64_t bytes) {
     return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
 }
 
-// streaming copy: 4 x 16 B in flight per thread per iteration, grid-stride
-// One-shot streaming copy: each thread moves 4 x 16 B at block-strided offsets (every load and
-// store instruction is a fully coalesced 16 KiB per workgroup) with nontemporal loads and stores.
-// Measured on MI355X (tools/copy_bench.hip, 4 GiB): 6.0 TB/s, against 4.9 TB/s for a grid-stride
-// loop and for hipMemcpyAsync D2D -- the bench's achievable-bandwidth figure.
-__global__ __launch_bounds__(256) void copy16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n) {
-    const uint64_t b0 = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-    uint64_t v[8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (b0 + 256 * q < n) {
-            const uint64_t *p = reinterpret_cast<const uint64_t *>(src + b0 + 256 * q);
-            v[2 * q] = __builtin_nontemporal_load(p);
-            v[2 * q + 1] = __builtin_nontemporal_load(p + 1);
-        }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (b0 + 256 * q < n) {
-            uint64_t *p = reinterpret_cast<uint64_t *>(dst + b0 + 256 * q);
-            __builtin_nontemporal_store(v[2 * q], p);
-            __builtin_nontemporal_store(v[2 * q + 1], p + 1);
-        }
+// The bench's achievable-bandwidth copy: one 16-byte nontemporal vector load and store per thread
+// (global_load_dwordx4 / global_store_dwordx4 nt), a workgroup per 4 KiB.  tools/copy_bench.hip on
+// MI355X, 4 GiB (profiles/r6_copy_bench.txt): 6.44 TB/s -- above the guide's 6.29 float4 copy -- against
+// 6.21 for plain 16-byte accesses, 5.85 for round 5's 4 x (2 x 8-byte nt) per thread (the kernel this
+// replaces: its 8-byte nt halves), 4.6-4.95 for grid-stride loops, 4.96 for hipMemcpyAsync D2D.
+typedef unsigned int mtg_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void copy16_kernel(const mtg_u32x4 *__restrict__ src, mtg_u32x4 *__restrict__ dst,
+                                                     uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 int mtg_device_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
     if (!dst || !src || (bytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15)) return MTG_ERR_ARGUMENT;
     const uint64_t n = bytes / 16;
     if (!n) return MTG_OK;
-    if (ceil_div(n, 1024) > 0x7fffffffull) return MTG_ERR_ARGUMENT;
-    const unsigned grid = (unsigned)ceil_div(n, 1024);
-    copy16_kernel<<<dim3(grid), dim3(256), 0, (hipStream_t)stream>>>((const uint4 *)src, (uint4 *)dst, n);
+    if (ceil_div(n, 256) > 0x7fffffffull) return MTG_ERR_ARGUMENT;
+    const unsigned grid = (unsigned)ceil_div(n, 256);
+    copy16_kernel<<<dim3(grid), dim3(256), 0, (hipStream_t)stream>>>((const mtg_u32x4 *)src, (mtg_u32x4 *)dst, n);
     return hipGetLastError() == hipSuccess ? MTG_OK : MTG_ERR_DEVICE;
 }
 
