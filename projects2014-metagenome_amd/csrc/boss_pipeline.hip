@@ -377,6 +377,7 @@ struct Ctx {
     // MTG_DIST_PIECES=n: the routed multi-GPU collect sends exchange 1 in n pieces on the exchange stream,
     // each sorted by its owner while the next one is in flight (routed_pieces); 1 = one exchange, then the sort
     uint32_t dist_pieces = 4;
+    bool dist_pieces_set = false;  // MTG_DIST_PIECES given: exactly that many (else fewer for small shares)
     hipStream_t xstream = nullptr;  // the multi-GPU exchange stream (created by the first distributed build)
     bool spec_final = true;  // MTG_SPEC=0: the exact final MSD level (histogram pass) instead of the
                              // sample-sized one (spec_final_level)
@@ -437,7 +438,10 @@ static void load_knobs(Ctx &c) {
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
     c.rounds_one_b = is("MTG_ROUNDS_ONE_B", "1");
-    if (const char *e = getenv("MTG_DIST_PIECES")) c.dist_pieces = (uint32_t)std::max(1L, std::min(16L, atol(e)));
+    if (const char *e = getenv("MTG_DIST_PIECES")) {
+        c.dist_pieces = (uint32_t)std::max(1L, std::min(16L, atol(e)));
+        c.dist_pieces_set = true;
+    }
     c.spec_tiny = is("MTG_SPEC_CAPS", "tiny");
     c.spec_lu_fail = is("MTG_SPEC_LU_FAIL", "1");
     c.spec_l1 = !is("MTG_SPEC_L1", "0");
@@ -3401,12 +3405,11 @@ template <bool COUNTED>
 static uint64_t routed_pieces(Ctx &c, Dist &d, unsigned K, uint32_t cmax, const Key<1> *ka, const uint32_t *ca,
                               const std::vector<unsigned long long> &cur, uint64_t nr, uint32_t nb1, unsigned B1,
                               unsigned OB, const std::vector<uint64_t> &bounds, const std::vector<uint64_t> &gh1,
-                              const std::vector<uint64_t> &H, Key<1> **out, uint32_t **outc, double *xspan_ms,
-                              double *hidden_ms, Tracer &tr) {
+                              const std::vector<uint64_t> &H, uint32_t Q, Key<1> **out, uint32_t **outc,
+                              double *xspan_ms, double *hidden_ms, Tracer &tr) {
     using K2 = Key<1>;
     constexpr uint32_t NBH = 1u << FUSED_HB;
     const int P = d.P;
-    const uint32_t Q = c.dist_pieces;
     std::vector<std::vector<uint64_t>> sub(P);
     for (int o = 0; o < P; ++o) {
         const uint64_t o0 = std::min<uint64_t>(bounds[o] << (B1 - OB), nb1);
@@ -3940,11 +3943,16 @@ static bool dist_collect_routed(Ctx &c, Dist &d, unsigned K, bool canonical, uin
         pass_b(rs, cur, ka, ca);
         if (rounds == 1) *ev_extract = tm.mark();
         tr("extract + scatter", nr);
-        if (rounds == 1 && d.P > 1 && c.dist_pieces > 1) {
-            // exchange 1 in pieces under the owner sort (routed_pieces)
+        // exchange 1 in pieces under the owner sort (routed_pieces): pieces of at least 2^28 keys an owner
+        // (each piece's sort pays ~0.7 ms of its own launches and host reads, more than a smaller piece's
+        // sort can hide), exactly MTG_DIST_PIECES when given; the same count on every rank (global totals)
+        const uint32_t Q = c.dist_pieces_set ? c.dist_pieces
+                                             : (uint32_t)std::min<uint64_t>(c.dist_pieces,
+                                                                            std::max<uint64_t>(1, Nall / d.P >> 28));
+        if (rounds == 1 && d.P > 1 && Q > 1) {
             double span = 0, hidden = 0;
-            U = routed_pieces<COUNTED>(c, d, K, cmax, ka, ca, cur, nr, nb1, B1, OB, *bounds, gh1, H, &xa, &xac, &span,
-                                       &hidden, tr);
+            U = routed_pieces<COUNTED>(c, d, K, cmax, ka, ca, cur, nr, nb1, B1, OB, *bounds, gh1, H, Q, &xa, &xac,
+                                       &span, &hidden, tr);
             c.timings.exchange_ms += span;
             c.timings.exchange_hidden_ms += hidden;
             // (the piece buffers stay in their slots for the next build of the same shape: given back, they
