@@ -618,7 +618,7 @@ def main():
     # profile of the same command, not measured in this process)
     traffic, traffic_src = None, None
     default_workload = args.config is None and args.k == 31 and args.reads == 10_000_000 and not args.count_width
-    for tag in (("r5", "r4", "r3", "r2", "r1") if default_workload else ()):  # the stored profile is of the default workload
+    for tag in (("r6", "r5", "r4", "r3", "r2", "r1") if default_workload else ()):  # the stored profile is of the default workload
         prof = os.path.join(ROOT, "profiles", "%s_partition_traffic.json" % tag)
         if os.path.exists(prof):
             try:
