@@ -1089,6 +1089,12 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     const Ctx::GroupIndex saved_gidx = c.gidx;  // the canonical sort's, for the fused rc merge below
     c.gidx = Ctx::GroupIndex{};
     if (n == 0) return 0;
+    // *alt == nullptr (the single build after the speculative level-1 layout): the ping-pong buffer is taken
+    // only by a path that needs it -- an exact level or the group passes -- never by the speculative level
+    auto lazy_alt = [&]() {
+        if (!*alt) *alt = (Key<L> *)c.ws.get(Workspace::KB, n * sizeof(Key<L>));
+        if (COUNTED && !*valt) *valt = (uint32_t *)c.ws.get(Workspace::CB, n * 4);
+    };
     constexpr uint32_t LIMIT = LocalTraits<L>::LIMIT;
     constexpr int TILE = MsdTraits<L>::TILE;
     const uint64_t tiles = ceil_div(n, TILE);
@@ -1100,6 +1106,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     uint64_t *bstart = nullptr;
     uint64_t nbuckets = 1;
     auto run_level = [&](unsigned lev) {
+        lazy_alt();
         if (digit_end[lev] == 0) digit_end[lev] = std::min(nbits, digit_end[lev - 1] + 8);
         const unsigned bb = digit_end[lev], bp = digit_end[lev - 1];
         nbuckets = 1ull << bb;
@@ -1162,6 +1169,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         b = bb;
     };
     if (runs && runs->size() >= 2 && runs->size() <= 129 && levels) {
+        lazy_alt();
         // bucket layout of the top T bits straight from the runs' own order
         const unsigned T = digit_end[levels];
         const uint32_t P = (uint32_t)runs->size() - 1;
@@ -1203,6 +1211,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         }
     }
 
+    lazy_alt();
     while (true) {
         // groups of consecutive buckets holding <= G keys; bigger buckets stand alone
         const uint64_t G = LIMIT / 4;
@@ -1893,14 +1902,16 @@ static uint64_t fused_pass_b_spec(Ctx &c, unsigned K, bool canonical, const Buil
     }
     const uint64_t C1 = read_u64(c, (const unsigned long long *)(sst + nseg));
     if (C1 % T2) throw std::logic_error("spec level 1: segments not tile-aligned");
-    {  // the padded array and its ping-pong buffer must fit next to everything else
+    {  // the padded array must fit next to everything else
         const uint64_t fr = c.ws.free_bytes();
-        const double need = 16.0 * (double)C1, have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::KA) +
-                                                       (double)c.ws.held_slot(Workspace::KB);
+        const double need = 8.0 * (double)C1, have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::KA);
         if (need > have) return ~0ull;
     }
     *ka = (Key<1> *)c.ws.get(Workspace::KA, std::max<uint64_t>(C1, 1) * 8);
-    *kb = (Key<1> *)c.ws.get(Workspace::KB, std::max<uint64_t>(C1, 1) * 8);
+    // no ping-pong buffer: the speculative level 2 partitions into its own buckets (SPEC_A / SPEC_B); the
+    // exact level, when the speculative one falls back, takes it then (msd_sort_unique: lazy_alt) -- 10.7 GB
+    // less held at configs[1]; the rc stage takes KB at its own size (U keys)
+    *kb = nullptr;
     auto *scur = (unsigned long long *)c.ws.get(Workspace::STRIPE_CUR, nseg * 16);
     unsigned long long *send = scur + nseg;
     spec_l1_cursor_kernel<<<dim3((unsigned)ceil_div(nseg, 256)), dim3(256), 0, c.stream>>>(sst, caps, nb1, S, scur,
@@ -2876,6 +2887,8 @@ static void run_pipeline(Ctx &c, unsigned k, bool canonical, unsigned bits,
         // when that changes its size)
         rm.ib = bucket_bits<L2>(2 * U, 2 * K);
         rm.istart = (uint64_t *)c.ws.get(Workspace::BUCKETS, ((1ull << rm.ib) + 2) * 8);
+        if (!kb) kb = (K2 *)c.ws.get(Workspace::KB, std::max<uint64_t>(U, 1) * sizeof(K2));  // (speculative layout)
+        if (COUNTED && !cb) cb = (uint32_t *)c.ws.get(Workspace::CB, std::max<uint64_t>(U, 1) * 4);
         const uint64_t Urc = stage_rc<L2, COUNTED>(c, K, cbits, cmax, ka, ca, U, kb, cb, &rk, &rkc, &rm);
         R = U + Urc;
         if (!rm.done) {
