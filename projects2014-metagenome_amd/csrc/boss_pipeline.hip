@@ -1106,7 +1106,6 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
     uint64_t *bstart = nullptr;
     uint64_t nbuckets = 1;
     auto run_level = [&](unsigned lev) {
-        lazy_alt();
         if (digit_end[lev] == 0) digit_end[lev] = std::min(nbits, digit_end[lev - 1] + 8);
         const unsigned bb = digit_end[lev], bp = digit_end[lev - 1];
         nbuckets = 1ull << bb;
@@ -1144,6 +1143,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             b = bb;
             return;
         }
+        lazy_alt();  // (a partition level writes *alt)
         auto *cur = (unsigned long long *)c.ws.get(Workspace::MSD_CURSOR, nbuckets * 8);
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nbuckets * 8, hipMemcpyDeviceToDevice, c.stream));
         EventTimer tm(c.stream);
