@@ -39,7 +39,7 @@ CONFIGS = {
     # configs[3]: k=31, 1 B reads over 8 GPUs = 125 M reads per GPU on one shared genome (10x over
     # all ranks' reads); one share does not fit one pass, so every rank collects in key batches
     "cfg4": {"k": 31, "reads": 125_000_000, "host_steps": 0, "fasta_reads": 0,
-             "cpu_sample_reads": 500_000, "steps": 2, "warmup": 1},
+             "cpu_sample_reads": 5_000_000, "steps": 2, "warmup": 1},
     # configs[4]: --count-kmers (SortedMultiset<uint8_t> saturating merge, 8-bit weights) on a KMC1
     # database of the canonical k=31 counts of every rank's reads (written by the builder's own GPU
     # counter, untimed), decoded into HBM before the timed region; across ranks the records of one
