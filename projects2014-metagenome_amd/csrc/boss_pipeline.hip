@@ -69,38 +69,40 @@ class Workspace {
         KA2, ROUND_DELTA, XA2, XAC2, CA2, NSLOTS
     };
     ~Workspace() {
-        for (auto &b : bufs_)
-            if (b.ptr) (void)hipFree(b.ptr);
-        for (auto &b : cache_) (void)hipFree(b.ptr);
+        // every device block once, by its base (a slot or kept entry may be a piece of one: carve)
+        for (auto &r : roots_)
+            if (r.base) (void)hipFree(r.base);
     }
     void *get(Slot s, size_t bytes, size_t keep = 0, hipStream_t stream = nullptr) {
         Buf &b = bufs_[s];
         bytes = std::max<size_t>(bytes, 256);
         if (b.cap < bytes) {
             size_t cap = 0;
-            void *p = take_cached(bytes, &cap);
+            int root = -1;
+            void *p = take_cached(bytes, &cap, &root);
             if (!p) {
                 cap = bytes + bytes / 8;
                 const auto t0 = std::chrono::steady_clock::now();
-                bool dropped = false;
-                if (hipMalloc(&p, cap) != hipSuccess) {
-                    (void)hipGetLastError();
-                    // no room for a new block: a kept block that holds the request, however big (freeing
-                    // kept blocks is what costs: ~12 ms per GB while the driver clears them, 2.3 s a build
-                    // at configs[2] when every failed allocation dropped the whole cache), and only then
-                    // kept blocks freed one at a time, largest first
-                    p = take_cached(bytes, &cap, true);
-                    while (!p && !cache_.empty()) {
+                bool dropped = false, carved = false;
+                if (carve_always) {
+                    p = take_cached(bytes, &cap, &root, true);
+                    carved = p != nullptr;
+                }
+                if (!p && !try_malloc(&p, cap, &root)) {
+                    // no room for a new block: a piece carved off a kept block that holds the request (the
+                    // rest stays kept: the later stages of a batched build fit in the blocks its rounds gave
+                    // back instead of each taking a whole one), and only then kept blocks freed one at a
+                    // time, largest first (freeing kept blocks is what costs: ~12 ms per GB while the driver
+                    // clears them, 2.3 s a build at configs[2] when every failed allocation dropped the
+                    // whole cache).  MTG_WS_CARVE=1 (tests): carve before any new block
+                    p = take_cached(bytes, &cap, &root, true);
+                    carved = p != nullptr;
+                    while (!p && !cache_.empty() && drop_largest()) {
                         dropped = true;
-                        drop_largest();
                         cap = bytes + bytes / 8;
-                        if (hipMalloc(&p, cap) != hipSuccess) {
-                            (void)hipGetLastError();
-                            p = nullptr;
-                        }
+                        if (!try_malloc(&p, cap, &root)) p = nullptr;
                     }
-                    if (!p && hipMalloc(&p, cap) != hipSuccess) {
-                        (void)hipGetLastError();
+                    if (!p && !try_malloc(&p, cap, &root)) {
                         size_t fr = 0, tot = 0;
                         (void)hipMemGetInfo(&fr, &tot);
                         throw std::runtime_error("HIP error out of memory: workspace slot " + std::to_string((int)s) +
@@ -110,19 +112,22 @@ class Workspace {
                                                  " MiB)");
                     }
                 }
+                if (carved) ++carves_;
                 if (trace && cap >= (1ull << 28))
-                    fprintf(stderr, "[mtg trace] workspace slot %d: new %lu MiB%s, %.1f ms (held %lu MiB, kept %lu MiB)\n",
-                            (int)s, (unsigned long)(cap >> 20), dropped ? " after dropping the kept blocks" : "",
+                    fprintf(stderr, "[mtg trace] workspace slot %d: %s %lu MiB%s, %.1f ms (held %lu MiB, kept %lu MiB)\n",
+                            (int)s, carved ? "carved" : "new", (unsigned long)(cap >> 20),
+                            dropped ? " after dropping the kept blocks" : "",
                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
                             (unsigned long)(held() >> 20), (unsigned long)(cached() >> 20));
             }
             if (keep && b.ptr) HIP_CHECK(hipMemcpyAsync(p, b.ptr, keep, hipMemcpyDeviceToDevice, stream));
             if (b.ptr) {
                 HIP_CHECK(hipDeviceSynchronize());
-                cache_.push_back(b);
+                give_back(b);
             }
             b.ptr = p;
             b.cap = cap;
+            b.root = root;
             ++gen_[s];
         }
         return b.ptr;
@@ -150,10 +155,11 @@ class Workspace {
         Buf &b = bufs_[s];
         if (b.ptr) {
             HIP_CHECK(hipDeviceSynchronize());
-            cache_.push_back(b);
+            give_back(b);
         }
         b.ptr = nullptr;
         b.cap = 0;
+        b.root = -1;
         ++gen_[s];
     }
     // every byte the workspace holds, in slots and kept blocks
@@ -173,32 +179,38 @@ class Workspace {
         HIP_CHECK(hipMemGetInfo(&fr, &tot));
         return (uint64_t)fr + cached();
     }
-    void drop_largest() {
-        if (cache_.empty()) return;
+    // the largest kept whole block freed (a block partly carved out to a slot stays); false: none
+    bool drop_largest() {
+        size_t big = cache_.size();
+        for (size_t i = 0; i < cache_.size(); ++i)
+            if (whole(cache_[i]) && (big == cache_.size() || cache_[i].cap > cache_[big].cap)) big = i;
+        if (big == cache_.size()) return false;
         HIP_CHECK(hipDeviceSynchronize());
-        size_t big = 0;
-        for (size_t i = 1; i < cache_.size(); ++i)
-            if (cache_[i].cap > cache_[big].cap) big = i;
-        (void)hipFree(cache_[big].ptr);
+        free_root(cache_[big].root);
         cache_.erase(cache_.begin() + (long)big);
+        return true;
     }
     void drop_cache() {
         if (cache_.empty()) return;
         HIP_CHECK(hipDeviceSynchronize());
-        for (auto &b : cache_) (void)hipFree(b.ptr);
-        cache_.clear();
+        std::vector<Buf> keep;
+        for (auto &b : cache_) {
+            if (whole(b)) free_root(b.root);
+            else keep.push_back(b);
+        }
+        cache_.swap(keep);
     }
     // end of a build: free the kept blocks no get() took during it (released in an earlier build and
     // idle since), so a big build's blocks do not pin HBM for the life of the constructor; the blocks
     // this build gave back stay for the next build of the same shape
     void end_build() {
         bool any = false;
-        for (const auto &b : cache_) any |= b.age > 0;
+        for (const auto &b : cache_) any |= b.age > 0 && whole(b);
         if (any) {
             HIP_CHECK(hipDeviceSynchronize());
             std::vector<Buf> keep;
             for (auto &b : cache_) {
-                if (b.age > 0) (void)hipFree(b.ptr);
+                if (b.age > 0 && whole(b)) free_root(b.root);
                 else keep.push_back(b);
             }
             cache_.swap(keep);
@@ -206,6 +218,8 @@ class Workspace {
         for (auto &b : cache_) b.age = 1;
     }
     uint64_t held_slot(Slot s) const { return bufs_[s].cap; }
+    uint64_t carves() const { return carves_; }
+    bool carve_always = false;  // MTG_WS_CARVE=1
     const void *peek(Slot s) const { return bufs_[s].ptr; }
     // bumped whenever the slot's buffer changes (regrown or released): a block given back may be
     // handed to another slot, so a pointer comparison alone cannot tell that the data is still there
@@ -216,23 +230,81 @@ class Workspace {
         void *ptr = nullptr;
         size_t cap = 0;
         uint32_t age = 0;  // kept blocks: builds ended since it was given back (end_build)
+        int root = -1;     // the device block (roots_) it is, or is a piece of
     };
+    struct Root {
+        void *base = nullptr;  // hipMalloc'ed, hipFree'd once when no piece of it is in use
+        size_t cap = 0;
+    };
+    bool whole(const Buf &b) const { return b.root >= 0 && b.ptr == roots_[b.root].base && b.cap == roots_[b.root].cap; }
+    bool try_malloc(void **p, size_t cap, int *root) {
+        if (hipMalloc(p, cap) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        size_t i = 0;
+        while (i < roots_.size() && roots_[i].base) ++i;
+        if (i == roots_.size()) roots_.emplace_back();
+        roots_[i] = Root{*p, cap};
+        *root = (int)i;
+        return true;
+    }
+    void free_root(int r) {
+        (void)hipFree(roots_[r].base);
+        roots_[r] = Root{};
+    }
+    // a slot's buffer back to the kept list, merged with the kept pieces of its block next to it (a
+    // block whose pieces are all back is whole again: the next build of the same shape takes it whole)
+    void give_back(Buf b) {
+        b.age = 0;
+        for (bool merged = true; merged;) {
+            merged = false;
+            for (size_t i = 0; i < cache_.size(); ++i) {
+                Buf &o = cache_[i];
+                if (o.root != b.root || b.root < 0) continue;
+                if ((char *)o.ptr + o.cap == (char *)b.ptr) {
+                    b.ptr = o.ptr, b.cap += o.cap;
+                } else if ((char *)b.ptr + b.cap == (char *)o.ptr) {
+                    b.cap += o.cap;
+                } else {
+                    continue;
+                }
+                cache_.erase(cache_.begin() + (long)i);
+                merged = true;
+                break;
+            }
+        }
+        cache_.push_back(b);
+    }
     // the smallest kept block of at least `bytes` and at most about twice that (a far bigger block
-    // stays for the request it was made for); any: no upper bound (the device has no room left)
-    void *take_cached(size_t bytes, size_t *cap, bool any = false) {
+    // stays for the request it was made for); carve (the device has no room left): the smallest kept
+    // block or piece that holds `bytes`, its front handed out and its rest kept when that is 256 MiB+
+    void *take_cached(size_t bytes, size_t *cap, int *root, bool carve = false) {
         size_t best = cache_.size();
         for (size_t i = 0; i < cache_.size(); ++i)
-            if (cache_[i].cap >= bytes && (any || cache_[i].cap <= 2 * bytes + (64u << 20)) &&
+            if (cache_[i].cap >= bytes && (carve || cache_[i].cap <= 2 * bytes + (64u << 20)) &&
                 (best == cache_.size() || cache_[i].cap < cache_[best].cap))
                 best = i;
         if (best == cache_.size()) return nullptr;
-        void *p = cache_[best].ptr;
-        *cap = cache_[best].cap;
+        Buf &k = cache_[best];
+        void *p = k.ptr;
+        *root = k.root;
+        const size_t piece = (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);  // 2 MiB aligned
+        if (carve && k.cap >= piece + (256u << 20)) {
+            *cap = piece;
+            k.ptr = (char *)k.ptr + piece;
+            k.cap -= piece;
+            k.age = 0;
+            return p;
+        }
+        *cap = k.cap;
         cache_.erase(cache_.begin() + (long)best);
         return p;
     }
     Buf bufs_[NSLOTS];
     uint64_t gen_[NSLOTS] = {};
+    std::vector<Root> roots_;
+    uint64_t carves_ = 0;
 
   public:
     bool trace = false;  // MTG_TRACE: report every fresh allocation of 256 MiB or more
@@ -349,10 +421,21 @@ struct Ctx {
         const uint64_t *start = nullptr;
     } gidx;
     bool want_gidx = false;  // the next msd_sort_unique's output feeds the fused rc merge
+    // a batched collect round's share of the canonical set's bucket index (collect_rounds_fused): the
+    // speculative final level's gather writes entries [lo, hi) of `start` (2^bits buckets) as positions
+    // + off in the whole set, and says so in `written`
+    struct RoundIndex {
+        uint64_t *start = nullptr;
+        unsigned bits = 0;
+        uint64_t off = 0, lo = 0, hi = 0;
+        bool written = false;
+    } ridx;
+    bool round_index = true;  // MTG_ROUND_INDEX=0: the canonical set's index by a bucket_index pass
     // where the next msd_sort_unique's final gather writes its compact distinct keys (and counts) instead of
     // *keys (the exchange pieces append each piece's keys in place: routed_pieces); *keys then points there
     void *sort_out = nullptr;
     uint32_t *sort_out_vals = nullptr;
+    uint64_t sort_out_cap = ~0ull;  // keys sort_out holds (more distinct keys: the usual gather into *keys)
     // the single build's canonical set left in the speculative level's bucket layout (no
     // group_gather_kernel): bucket g's keys at keys[bstart[g] ..), compact at ustart[g] ..
     // (ustart[g + 1] - ustart[g] keys).  rc_map and the fused rc merge read it there;
@@ -373,7 +456,19 @@ struct Ctx {
     // step overflowed into the exact level, sort 30.3 -> 38.9 ms; level 3 now samples every tile's
     // first eighth.)
     bool spec3 = true;
-    bool rounds_one_b = false;  // MTG_ROUNDS_ONE_B=1: two collect rounds share one pass B (collect_rounds_fused)
+    // the speculative final level's local unique writes over its own buckets (each group is read whole
+    // before it writes): one slack-sized buffer instead of two.  MTG_SPEC_INPLACE=0: two
+    bool spec_inplace = true;
+    // a free buffer the speculative final level of a 3-level sort may partition into (the batched
+    // collect's level-1 array, sized for it, free once level 2 has moved the keys out): no third block
+    void *spec_into = nullptr;
+    uint64_t spec_into_bytes = 0;
+    // a collect round whose keys are sparse in the plan's final buckets (it spans more level-1 buckets
+    // than its share: canonical k-mers crowd the small prefixes) takes one final bit fewer, so its local
+    // unique runs fuller groups (configs[3]'s second round: 2.95 M groups of ~390 distinct keys, 25.7 vs
+    // 20.6 ms for the first round's 1.25 M).  MTG_ROUND_BITS=0: the plan's bits in every round
+    bool round_bits = true;
+    bool rounds_one_b = true;  // two collect rounds share one pass B (collect_rounds_fused); MTG_ROUNDS_ONE_B=0: not
     // MTG_DIST_PIECES=n: the routed multi-GPU collect sends exchange 1 in n pieces on the exchange stream,
     // each sorted by its owner while the next one is in flight (routed_pieces); 1 = one exchange, then the sort
     uint32_t dist_pieces = 4;
@@ -437,7 +532,11 @@ static void load_knobs(Ctx &c) {
     c.defer_gather = !is("MTG_DEFER_GATHER", "0");
     c.spec_rc = !is("MTG_SPEC_RC", "0");
     c.spec3 = !is("MTG_SPEC3", "0");
-    c.rounds_one_b = is("MTG_ROUNDS_ONE_B", "1");
+    c.rounds_one_b = !is("MTG_ROUNDS_ONE_B", "0");
+    c.ws.carve_always = is("MTG_WS_CARVE", "1");
+    c.spec_inplace = !is("MTG_SPEC_INPLACE", "0");
+    c.round_bits = !is("MTG_ROUND_BITS", "0");
+    c.round_index = !is("MTG_ROUND_INDEX", "0");
     if (const char *e = getenv("MTG_DIST_PIECES")) {
         c.dist_pieces = (uint32_t)std::max(1L, std::min(16L, atol(e)));
         c.dist_pieces_set = true;
@@ -773,7 +872,8 @@ static void ensure_compact(Ctx &c) {
 template <int L, bool COUNTED>
 static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_t n, unsigned nbits, unsigned bp,
                                  unsigned bb, uint32_t cmax, bool distinct, RcMerge<L> *rm,
-                                 const Ctx::GroupIndex &cidx, bool fine = false) {
+                                 const Ctx::GroupIndex &cidx, bool fine = false, Key<L> *spare = nullptr) {
+    // spare (c.spec_into, uncounted): a free buffer of c.spec_into_bytes the buckets may take instead of SPEC_A
     // COUNTED: the counts travel with their keys (SPEC_AC / SPEC_BC) and add with saturation in the
     // local pass, as in the exact level (configs[4]'s counted route)
     if constexpr (L != 1) {
@@ -797,10 +897,15 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // tile-granular sample sized the buckets badly (overflow at 2 M reads)
         if (g1) fine = true;
         const uint64_t nb = 1ull << bb;
-        // the two slack-sized buffers must fit next to everything else
-        {
+        // the deferred gather (the fused rc merge follows) leaves the distinct keys in their own buckets
+        // (SPEC_B); otherwise the local unique writes over its input buckets (in place: one buffer)
+        const bool gap_out = !COUNTED && c.defer_gather_req && c.defer_gather && c.want_gidx;
+        const bool inplace = !rm && c.spec_inplace && !gap_out;
+        if (COUNTED) spare = nullptr;
+        // the slack-sized buffers must fit next to everything else
+        if (!spare) {
             const uint64_t fr = c.ws.free_bytes();
-            if ((double)n * KB * 1.4 * 2.0 > 0.5 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
+            if ((double)n * KB * 1.4 * (inplace ? 1.0 : 2.0) > 0.5 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
                                                   (double)c.ws.held_slot(Workspace::SPEC_B) +
                                                   (double)c.ws.held_slot(Workspace::SPEC_AC) +
                                                   (double)c.ws.held_slot(Workspace::SPEC_BC))
@@ -840,9 +945,10 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             HIP_CHECK(hipGetLastError());
         }
         const uint64_t C = read_u64(c, (const unsigned long long *)(bstart + nb));
-        {  // the capacity is known now: both slack-sized buffers (one for the fused rc merge) must fit
+        if (spare && C * sizeof(Key<L>) > c.spec_into_bytes) spare = nullptr;
+        if (!spare) {  // the capacity is known now: both slack-sized buffers (one: fused rc merge, in place) must fit
             const uint64_t fr = c.ws.free_bytes();
-            const double need = (double)C * KB * (rm ? 1.0 : 2.0);
+            const double need = (double)C * KB * (rm || inplace ? 1.0 : 2.0);
             const double have = 0.9 * (double)fr + (double)c.ws.held_slot(Workspace::SPEC_A) +
                                 (double)c.ws.held_slot(Workspace::SPEC_AC) +
                                 (rm ? 0.0 : (double)c.ws.held_slot(Workspace::SPEC_B) +
@@ -853,7 +959,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
                 return ~0ull;
             }
         }
-        Key<L> *sa = (Key<L> *)c.ws.get(Workspace::SPEC_A, C * sizeof(Key<L>));
+        Key<L> *sa = spare ? spare : (Key<L> *)c.ws.get(Workspace::SPEC_A, C * sizeof(Key<L>));
         uint32_t *sac = COUNTED ? (uint32_t *)c.ws.get(Workspace::SPEC_AC, C * 4) : nullptr;
         auto *cur = (unsigned long long *)c.ws.get(Workspace::SPEC_CUR, nb * 8);
         HIP_CHECK(hipMemcpyAsync(cur, bstart, nb * 8, hipMemcpyDeviceToDevice, c.stream));
@@ -976,8 +1082,8 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             return n;
         }
         // every bucket one group: [bstart[b], cur[b])
-        Key<L> *sb = (Key<L> *)c.ws.get(Workspace::SPEC_B, C * sizeof(Key<L>));
-        uint32_t *sbc = COUNTED ? (uint32_t *)c.ws.get(Workspace::SPEC_BC, C * 4) : nullptr;
+        Key<L> *sb = inplace ? sa : (Key<L> *)c.ws.get(Workspace::SPEC_B, C * sizeof(Key<L>));
+        uint32_t *sbc = !COUNTED ? nullptr : inplace ? sac : (uint32_t *)c.ws.get(Workspace::SPEC_BC, C * 4);
         uint32_t *ucount = (uint32_t *)c.ws.get(Workspace::MSD_UCOUNT, (nb + 1) * 4);
         uint32_t *ovf = (uint32_t *)c.ws.get(Workspace::MSD_OVF, nb * 4);
         HIP_CHECK(hipMemsetAsync(ovf, 0, nb * 4, c.stream));
@@ -1042,16 +1148,19 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
             return u;
         }
         const bool index = c.want_gidx;
-        uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8) : nullptr;
-        if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
-        if (c.sort_out) {  // (the caller's destination: the input is no longer read)
-            *keys = (Key<L> *)c.sort_out;
+        // a collect round's share of the whole set's index (Ctx::ridx), its buckets 2^(bits - bb) a group
+        const bool rindex = !index && c.ridx.start && bb <= c.ridx.bits;
+        uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8) : rindex ? c.ridx.start : nullptr;
+        const unsigned ib = rindex ? c.ridx.bits : bb;
+        if (index || rindex) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
+        if (c.sort_out && (c.sort_out_cap == ~0ull || read_u64(c, (const unsigned long long *)(ustart + nb)) <= c.sort_out_cap)) {
+            *keys = (Key<L> *)c.sort_out;  // (the caller's destination: the input is no longer read)
             if (COUNTED) *vals = c.sort_out_vals;
         }
         bucket_pieces(0, nb, [&](uint64_t g0, unsigned cnt) {
             group_gather_kernel<L, COUNTED><<<dim3(cnt), dim3(256), 0, c.stream>>>(
-                sb, sbc, bstart, ustart, *keys, COUNTED ? *vals : nullptr, nullptr, nbits - bb, gi, &c.small->gidx_bad,
-                g0);
+                sb, sbc, bstart, ustart, *keys, COUNTED ? *vals : nullptr, nullptr, nbits - ib, gi, &c.small->gidx_bad,
+                g0, ib - bb, rindex ? c.ridx.off : 0, rindex ? c.ridx.lo : 0, rindex ? c.ridx.hi : ~0ull);
             HIP_CHECK(hipGetLastError());
         });
         uint64_t u = 0;
@@ -1060,10 +1169,11 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         if (index) {
             HIP_CHECK(hipMemcpyAsync(gi + nb, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
             HIP_CHECK(hipMemcpyAsync(gi + nb + 1, ustart + nb, 8, hipMemcpyDeviceToDevice, c.stream));
-            HIP_CHECK(hipMemcpyAsync(&ibad, &c.small->gidx_bad, 4, hipMemcpyDeviceToHost, c.stream));
         }
+        if (index || rindex) HIP_CHECK(hipMemcpyAsync(&ibad, &c.small->gidx_bad, 4, hipMemcpyDeviceToHost, c.stream));
         HIP_CHECK(hipStreamSynchronize(c.stream));
         if (index && !ibad) c.gidx = Ctx::GroupIndex{*keys, u, bb, nbits, gi};
+        if (rindex) c.ridx.written = !ibad;
         consumed_gap1();
         ++c.timings.spec_levels;
         if (fine) ++c.timings.spec_fine_levels;
@@ -1203,8 +1313,11 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                 // a 10-bit level 1 on a small input (a tile-granular sample of ~30 tiles a bucket missed
                 // by up to ~25 %)
                 const bool fine = lev >= 3 || (n >> digit_end[lev - 1]) < 64ull * MsdTraits<L>::TILE;
+                // the caller's spare buffer (c.spec_into) once level 2 has moved the keys out of it
+                Key<L> *spare = lev >= 3 && c.spec_into && c.spec_into != (void *)*keys ? (Key<L> *)c.spec_into : nullptr;
                 const uint64_t u = spec_final_level<L, COUNTED>(c, keys, vals, n, nbits, digit_end[lev - 1],
-                                                                digit_end[lev], cmax, distinct, rm, saved_gidx, fine);
+                                                                digit_end[lev], cmax, distinct, rm, saved_gidx, fine,
+                                                                spare);
                 if (u != ~0ull) return u;
             }
             run_level(lev);
@@ -1442,8 +1555,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         const bool index = c.want_gidx && gbucket_out && b > 0;
         uint64_t *gi = index ? (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nbuckets + 2) * 8) : nullptr;
         if (index) HIP_CHECK(hipMemsetAsync(&c.small->gidx_bad, 0, 4, c.stream));
-        if (c.sort_out) {  // (the caller's destination: the gather reads *alt only)
-            *keys = (Key<L> *)c.sort_out;
+        if (c.sort_out &&
+            (c.sort_out_cap == ~0ull || read_u64(c, (const unsigned long long *)(ustart + ngroups)) <= c.sort_out_cap)) {
+            *keys = (Key<L> *)c.sort_out;  // (the caller's destination: the gather reads *alt only)
             if (COUNTED) *vals = c.sort_out_vals;
         }
         bucket_pieces(0, ngroups, [&](uint64_t g0, unsigned cnt) {
@@ -2261,23 +2375,39 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         for (uint64_t b = bb[r]; b < bb[r + 1]; ++b) nr[r] += h1[b];
         nmax = std::max(nmax, nr[r]);
     }
-    // one pass B for every round (MTG_ROUNDS_ONE_B=0: a pass B per round) when the whole level-1 layout
-    // (N keys) fits in KA beside one round's partition buffer and the canonical set: the rounds then
-    // sort their slices of it, and the reads are scanned once instead of R times (configs[3]'s share:
-    // two 40 ms pass-B scans)
-    // MTG_ROUNDS_ONE_B=1: two rounds of the u64 pass B (configs[3]'s share) become one when both rounds'
-    // keys fit beside the partition buffer and the canonical set: the pass writes round 0's buckets into
-    // KA and round 1's into KA2 (per-bucket destinations, bdelta), so the reads are scanned once (pass B
-    // 2 x 40 -> 48.7 ms).  Off by default: the third ~64 GB block fragments the workspace for the later
-    // stages (their 4-20 GB requests were handed the idle 64 GB blocks once HBM ran out, and the emit
-    // ran out of memory at configs[3]'s share; gpurun_out/r5p), and freeing it costs ~12 ms per GB
+    // two rounds of the u64 pass B (configs[3]'s share) become one when both rounds' keys fit beside the
+    // partition buffer and the canonical set: the pass writes round 0's buckets into KA and round 1's into
+    // KA2 (per-bucket destinations, bdelta), so the reads are scanned once (pass B 2 x 40 -> 45 ms).
+    // MTG_ROUNDS_ONE_B=0: a pass B per round.  (Round 5 kept it off: the third ~64 GB block left the later
+    // stages no room -- their 4-20 GB requests each took a whole idle 64 GB block -- until the workspace
+    // learned to carve pieces off its kept blocks, Workspace::take_cached)
     bool one_b = false;
     if (R == 2 && c.rounds_one_b && L == 1 && !COUNTED && K <= 32) {
         const double kb = (double)sizeof(K2);
         const double need = ((double)N + (double)nmax) * kb + u_est * 1.25 * kb + (double)(1ull << 30);
         one_b = need <= budget;
     }
-    K2 *ka = (K2 *)c.ws.get(Workspace::KA, (one_b ? nr[0] : nmax) * sizeof(K2));
+    // a 3-level plan's speculative level 3 partitions into KA, which level 2 has emptied by then (the
+    // round's keys in KB; with one pass B, round 1's in KA2): KA is sized for the level's slack-sized
+    // buckets -- 1.2 n + 512 a bucket (spec_caps_kernel), +5 % -- when that fits the budget, so the level
+    // needs no third round-sized block and its histogram pass goes (configs[3]'s share: levels 2 and 3
+    // were both exact, a 60 GB read each per round)
+    uint64_t ka_keys = one_b ? nr[0] : nmax;
+    struct SpareGuard {  // never left set past this function (a thrown build included)
+        Ctx &c;
+        ~SpareGuard() { c.spec_into = nullptr, c.spec_into_bytes = 0; }
+    } spare_guard{c};
+    if (L == 1 && !COUNTED && plan.levels == 3 && c.spec3 && c.spec_final && c.spec_inplace && !c.use_lsd) {
+        double fmax = 0;
+        for (uint32_t r = 0; r < R; ++r) fmax = std::max(fmax, (double)(bb[r + 1] - bb[r]) / (double)nb1);
+        const double cap = (1.2 * (double)nmax + 512.0 * (double)(1ull << plan.digit_end[3]) * fmax) * 1.05 + 65536.0;
+        const double kb = (double)sizeof(K2);
+        const double need = (cap + (one_b ? (double)nr[1] : 0.0) + (double)nmax) * kb + u_est * 1.25 * kb +
+                            (double)(1ull << 30);
+        if (cap > (double)ka_keys && need <= budget) ka_keys = (uint64_t)cap;
+    }
+    K2 *ka = (K2 *)c.ws.get(Workspace::KA, ka_keys * sizeof(K2));
+    if (L == 1 && ka_keys > (one_b ? nr[0] : nmax)) c.spec_into = ka, c.spec_into_bytes = ka_keys * sizeof(K2);
     K2 *ka2 = one_b ? (K2 *)c.ws.get(Workspace::KA2, std::max<uint64_t>(nr[1], 1) * sizeof(K2)) : nullptr;
     K2 *kb = (K2 *)c.ws.get(Workspace::KB, nmax * sizeof(K2));
     uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nmax * 4) : nullptr;
@@ -2310,7 +2440,40 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     *out = nullptr;
     *outc = nullptr;
     bool first = true;
+    // the canonical set sized from pass A's duplication estimate up front, so that every round's final
+    // gather writes its distinct keys straight into it (c.sort_out) instead of into the round buffer and a
+    // copy after (a 19 GB copy per configs[3] round); a round that finds more falls back to that copy
+    if (R > 1 && !COUNTED) {
+        cap = (uint64_t)u_est + 65536;
+        *out = (K2 *)c.ws.get(Workspace::CANON, cap * sizeof(K2));
+    }
+    struct SortOutGuard {
+        Ctx &c;
+        ~SortOutGuard() { c.sort_out = nullptr, c.sort_out_vals = nullptr, c.sort_out_cap = ~0ull, c.ridx = Ctx::RoundIndex{}; }
+    } sort_out_guard{c};
+    // the rc stage reads the canonical set through a bucket index over the rc sort's final bits (its plan
+    // for the set's size, estimated here from pass A's duplication): each round's speculative gather writes
+    // its buckets' entries (Ctx::ridx) instead of a bucket_index pass over the whole set after the rounds
+    // (5.6 ms at configs[3]'s share); a round that takes another path leaves it to that pass
+    unsigned fb_est = 0;
+    uint64_t *rgi = nullptr;
+    bool rgi_ok = false;
+    if (canonical && !COUNTED && c.round_index) {
+        const MsdPlan rp = msd_plan<L>(c, std::max<uint64_t>(1, (uint64_t)((double)N / A.dup)), 2 * K, 1.0);
+        fb_est = rp.levels ? rp.digit_end[rp.levels] : 0;
+        if (fb_est >= b1 && fb_est <= 26) {
+            rgi = (uint64_t *)c.ws.get(Workspace::CANON_IDX, ((1ull << fb_est) + 2) * 8);
+            rgi_ok = true;
+        }
+    }
     for (uint32_t r = 0; r < R; ++r) {
+        if (rgi_ok && !nr[r]) {  // no keys: the round's index entries all point at the set's next position
+            const uint64_t lo = bb[r] << (fb_est - b1), hi = bb[r + 1] << (fb_est - b1);
+            if (lo < hi)
+                fill_u64_kernel<<<dim3((unsigned)std::min<uint64_t>(ceil_div(hi - lo, 256), 4096)), dim3(256), 0, c.stream>>>(
+                    rgi, lo, hi, off);
+            HIP_CHECK(hipGetLastError());
+        }
         if (!nr[r]) continue;
         const uint32_t *dh1 = nullptr;
         uint64_t n = 0;
@@ -2333,8 +2496,24 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
             tr("rounds: pass B", r, n);
         }
         c.track_partition = first;  // the roofline's partition pass: the first round's level 2
+        MsdPlan rplan = plan;
+        if (L == 1 && c.round_bits && plan.levels >= 2) {
+            // keys per final bucket in this round against the whole input's average (Ctx::round_bits)
+            const unsigned T = plan.digit_end[plan.levels], bp = plan.digit_end[plan.levels - 1];
+            const double nbk = (double)(bb[r + 1] - bb[r]) * (double)(1ull << (T - b1));
+            const double rho = ((double)n / nbk) / ((double)N / (double)(1ull << T));
+            if (rho < 0.75 && T >= bp + 2) rplan.digit_end[plan.levels] = T - 1;
+        }
+        if (*out && off < cap && (!COUNTED || *outc)) {
+            c.sort_out = *out + off, c.sort_out_cap = cap - off;
+            c.sort_out_vals = COUNTED ? *outc + off : nullptr;  // (the counts travel with their keys)
+        }
+        if (rgi_ok) c.ridx = Ctx::RoundIndex{rgi, fb_est, off, bb[r] << (fb_est - b1), bb[r + 1] << (fb_est - b1), false};
         const uint64_t U = msd_sort_unique<L, COUNTED>(c, &xa, &xb, &xac, &xbc, n, 2 * K, cmax, A.dup, dh1, false,
-                                                       nullptr, true, nullptr, &plan);
+                                                       nullptr, true, nullptr, &rplan);
+        rgi_ok = rgi_ok && c.ridx.written;
+        c.ridx = Ctx::RoundIndex{};
+        c.sort_out = nullptr, c.sort_out_vals = nullptr, c.sort_out_cap = ~0ull;
         c.track_partition = false;
         first = false;
         tr("rounds: sort", r, U);
@@ -2347,8 +2526,10 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
             *out = (K2 *)c.ws.get(Workspace::CANON, cap * sizeof(K2), off * sizeof(K2), c.stream);
             if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, cap * 4, off * 4, c.stream);
         }
-        HIP_CHECK(hipMemcpyAsync(*out + off, xa, U * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
-        if (COUNTED) HIP_CHECK(hipMemcpyAsync(*outc + off, xac, U * 4, hipMemcpyDeviceToDevice, c.stream));
+        if (xa != *out + off) {  // (gathered into the round buffer, not straight into the set)
+            HIP_CHECK(hipMemcpyAsync(*out + off, xa, U * sizeof(K2), hipMemcpyDeviceToDevice, c.stream));
+            if (COUNTED) HIP_CHECK(hipMemcpyAsync(*outc + off, xac, U * 4, hipMemcpyDeviceToDevice, c.stream));
+        }
         off += U;
         if (c.debug)
             fprintf(stderr, "[mtg debug]   round %u: buckets [%lu, %lu) n=%lu -> %lu distinct\n", r,
@@ -2359,6 +2540,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, 4);
     }
     debug_check_sorted(c, "canonical rounds", *out, off);
+    c.spec_into = nullptr, c.spec_into_bytes = 0;
     // the round buffers (sized for the largest round) go; the rc stage takes KB and SPEC_A again at
     // its own size
     for (auto sl : {Workspace::KA, Workspace::KA2, Workspace::CA, Workspace::KB, Workspace::CB, Workspace::SPEC_A,
@@ -2373,9 +2555,16 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         if (fb && fb <= 26) {
             const uint64_t nb = 1ull << fb;
             uint64_t *gi = (uint64_t *)c.ws.get(Workspace::CANON_IDX, (nb + 2) * 8);
-            bucket_index<L>(c, *out, off, 2 * K - fb, nb, gi);
-            HIP_CHECK(hipMemcpyAsync(gi + nb + 1, gi + nb, 8, hipMemcpyDeviceToDevice, c.stream));
+            if (rgi_ok && fb == fb_est && gi == rgi) {  // written by the rounds' gathers: its two end entries
+                fill_u64_kernel<<<dim3(1), dim3(256), 0, c.stream>>>(gi, nb, nb + 2, off);
+                HIP_CHECK(hipGetLastError());
+                if (c.debug) fprintf(stderr, "[mtg debug] canonical rounds: bucket index from the rounds' gathers\n");
+            } else {
+                bucket_index<L>(c, *out, off, 2 * K - fb, nb, gi);
+                HIP_CHECK(hipMemcpyAsync(gi + nb + 1, gi + nb, 8, hipMemcpyDeviceToDevice, c.stream));
+            }
             c.gidx = Ctx::GroupIndex{*out, off, fb, 2 * K, gi};
+
         }
     }
     *U_out = off;

@@ -914,6 +914,9 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             if (COUNTED) sscr[p] = s_sum[i];
         }
         __syncthreads();
+        // (a 9-bit counting sort -- half the sub-bucket scans, its fill counters in the gathered slot list's
+        // words -- measured even, 7.90-7.94 vs 7.94-7.96 ms sort stage in round 6; 10 bits cost occupancy:
+        // 8.57 ms)
         // (staging the sorted run in LDS for one coalesced store halves the HBM write bytes -- PMC
         // WRITE_SIZE 2.89 GB for 1.5 GB of keys stored one by one at their ranks -- but the extra
         // barrier cost more: sort stage 10.5 -> 11.0 ms)
@@ -1186,31 +1189,52 @@ __global__ __launch_bounds__(256) void group_gather_kernel(
     const uint64_t *__restrict__ gstart, const uint64_t *__restrict__ ustart,
     Key<L> *__restrict__ out, uint32_t *__restrict__ ocnt, const uint64_t *__restrict__ gbucket = nullptr,
     unsigned ishift = 0, uint64_t *__restrict__ istart = nullptr, uint32_t *__restrict__ ibad = nullptr,
-    uint64_t g_base = 0) {
+    uint64_t g_base = 0, unsigned gshift = 0, uint64_t ioff = 0, uint64_t ilo = 0, uint64_t ihi = ~0ull) {
     // a run of more than IRUN empty buckets between two keys would be one thread's serial loop:
     // the index is abandoned (*ibad) and the caller builds it with bucket_index_kernel
+    // gshift: a group covers 2^gshift index buckets; ioff: added to every index entry (the output's place
+    // in a bigger array); only index entries in [ilo, ihi) are written (a batched collect's round owns those)
     constexpr uint64_t IRUN = 4096;
     const uint64_t g = g_base + blockIdx.x;
     const uint64_t src = gstart[g], dst = ustart[g], m = ustart[g + 1] - dst;
     // gbucket == nullptr: one bucket per group (the speculative final level)
-    const uint64_t gb0 = istart ? (gbucket ? gbucket[g] : g) : 0;
-    const uint64_t gb1 = istart ? (gbucket ? gbucket[g + 1] : g + 1) : 0;
+    const uint64_t gb0 = istart ? (gbucket ? gbucket[g] : g) << gshift : 0;
+    const uint64_t gb1 = istart ? (gbucket ? gbucket[g + 1] : g + 1) << gshift : 0;
     bool bad = false;
+    // one bucket a group (gbucket == nullptr, the speculative final level): its 2^gshift index buckets
+    // start at the group's first key at or above each -- a binary search per bucket, no per-key work
+    // (the per-key walk below re-reads every key's predecessor: ~2 ms a configs[3] round)
+    const bool per_key = istart && gbucket;
     for (uint64_t i = threadIdx.x; i < m; i += 256) {
         const Key<L> key = tmp[src + i];
         out[dst + i] = key;
         if (COUNTED) ocnt[dst + i] = tcnt[src + i];
-        if (istart) {  // buckets (previous key's, this key's] start here
+        if (per_key) {  // buckets (previous key's, this key's] start here
             const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
             const uint64_t pb = i == 0 ? gb0 - 1 : bits_at(shr(tmp[src + i - 1], ishift), 0, 32);
             if (kb - pb > IRUN) bad = true;
-            else for (uint64_t x = pb + 1; x <= kb; ++x) istart[x] = dst + i;
+            else
+                for (uint64_t x = pb + 1; x <= kb; ++x)
+                    if (x >= ilo && x < ihi) istart[x] = ioff + dst + i;
         }
     }
-    if (istart) {  // the group's buckets after its last key start at its end
+    if (istart && !gbucket) {
+        for (uint64_t t = threadIdx.x; t < gb1 - gb0; t += 256) {
+            const uint64_t x = gb0 + t;
+            uint64_t lo = 0, hi = t ? m : 0;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (bits_at(shr(tmp[src + mid], ishift), 0, 32) < x) lo = mid + 1;
+                else hi = mid;
+            }
+            if (x >= ilo && x < ihi) istart[x] = ioff + dst + lo;
+        }
+    } else if (istart) {  // the group's buckets after its last key start at its end
         const uint64_t lb = m ? bits_at(shr(tmp[src + m - 1], ishift), 0, 32) : gb0 - 1;
         if (gb1 - (lb + 1) > 256 * IRUN) bad = true;
-        else for (uint64_t x = lb + 1 + threadIdx.x; x < gb1; x += 256) istart[x] = dst + m;
+        else
+            for (uint64_t x = lb + 1 + threadIdx.x; x < gb1; x += 256)
+                if (x >= ilo && x < ihi) istart[x] = ioff + dst + m;
         if (bad) atomicOr(ibad, 1u);
     }
 }

@@ -59,7 +59,7 @@ def test_rounds_random_reads(small_fused, rounds, k):
 @pytest.mark.parametrize("k", [20, 31])
 def test_rounds_pass_b_per_round_knob(small_fused, k):
     # two rounds of the u64 pass B run as one pass writing each round's buckets into its own buffer;
-    # (MTG_ROUNDS_ONE_B=1, opt-in); 0: a pass B per round (the masked scan)
+    # (the default; MTG_ROUNDS_ONE_B=1); 0: a pass B per round (the masked scan)
     small_fused.setenv("MTG_RANGES", "2")
     reads = _random_reads(3000 + k, 400, 150, 5000, n_rate=0.005, lower=True)
     for one_b in ("1", "0"):
@@ -68,6 +68,24 @@ def test_rounds_pass_b_per_round_knob(small_fused, k):
             for bits in (0, 8):
                 _, t = _check(k, reads, canonical, bits)
                 assert t.collect_mode == ROUNDS and t.n_batches == 2, (t.collect_mode, t.n_batches)
+
+
+@pytest.mark.parametrize("knob", ["MTG_ROUND_INDEX", "MTG_ROUND_BITS", "MTG_ROUNDS_ONE_B"])
+def test_rounds_2m_knobs_off(monkeypatch, knob):
+    # the batched collect's defaults each switched off in turn on 2 M genome reads of 3 MSD levels in 2
+    # rounds: the canonical set's bucket index written by the rounds' gathers (MTG_ROUND_INDEX), one final
+    # bit fewer in a sparse round (MTG_ROUND_BITS), one pass B for both rounds (MTG_ROUNDS_ONE_B)
+    monkeypatch.setenv("MTG_RANGES", "2")
+    monkeypatch.setenv("MTG_MSD_LEVELS", "3")
+    monkeypatch.setenv(knob, "0")
+    asc = bench.make_reads_host_codes(2_000_000, 150, 4242, "genome", 10.0)
+    ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, num_threads=8)
+    ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)
+    got = ctor.build_chunk()
+    t = ctor.timings()
+    assert t.collect_mode == ROUNDS and t.n_batches == 2
+    reads = [asc[i].tobytes() for i in range(len(asc))]
+    assert_same(got, O.build_chunk(30, reads, canonical=True), "2M reads k=31, 2 rounds, %s=0" % knob)
 
 
 def test_rounds_counts_saturate(small_fused):
@@ -124,22 +142,37 @@ def test_rounds_bench_generator_2m(monkeypatch, canonical, bits):
     assert_same(got, want, "2M reads k=31 canonical=%s bits=%d, 3 rounds" % (canonical, bits))
 
 
-# a 3-level plan in every round (configs[3]'s share plans 7 + 8 + 7 bits): forced on 2 M reads
-@pytest.mark.parametrize("spec3", ["0", "1"])
+# a 3-level plan in every round (configs[3]'s share plans 10 + 16 + 22 bits): forced on 2 M reads.  The
+# speculative level 3 partitions into the rounds' level-1 array (c.spec_into) and its local unique writes
+# over its own buckets; MTG_SPEC_INPLACE=0 gives it two buffers of its own, MTG_WS_CARVE=1 makes every
+# workspace request a piece carved off a kept block where one holds it (the allocator's no-room path)
+@pytest.mark.parametrize("spec3,knobs", [("0", {}), ("1", {}), ("1", {"MTG_WS_CARVE": "1"}),
+                                         ("1", {"MTG_SPEC_INPLACE": "0"})])
 @pytest.mark.parametrize("canonical", [False, True])
-def test_rounds_three_msd_levels(monkeypatch, canonical, spec3):
+def test_rounds_three_msd_levels(monkeypatch, canonical, spec3, knobs):
+    if knobs and not canonical:
+        pytest.skip("the knob cases run on the canonical build")
     monkeypatch.setenv("MTG_RANGES", "3")
     monkeypatch.setenv("MTG_MSD_LEVELS", "3")
     monkeypatch.setenv("MTG_SPEC3", spec3)
+    for name, v in knobs.items():
+        monkeypatch.setenv(name, v)
     asc = bench.make_reads_host_codes(2_000_000, 150, 12345, "genome", 10.0)
     ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=canonical, num_threads=8)
     ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)
     got = ctor.build_chunk()
     t = ctor.timings()
     assert t.collect_mode == ROUNDS and t.n_batches == 3
+    if spec3 == "1":  # every round's level 3 speculative, none fell back
+        assert t.spec_levels >= 3 and t.spec_fallbacks == 0, (t.spec_levels, t.spec_fallbacks)
     reads = [asc[i].tobytes() for i in range(len(asc))]
     want = O.build_chunk(30, reads, canonical=canonical)
-    assert_same(got, want, "2M reads k=31 canonical=%s, 3 rounds of 3 MSD levels, MTG_SPEC3=%s" % (canonical, spec3))
+    assert_same(got, want, "2M reads k=31 canonical=%s, 3 rounds of 3 MSD levels, MTG_SPEC3=%s %s" %
+                (canonical, spec3, knobs))
+    if knobs:  # a second build on the same constructor: the kept (and carved) blocks handed out again
+        ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)  # (a build consumes its reads)
+        again = ctor.build_chunk()
+        assert_same(again, want, "the same constructor's second build, %s" % knobs)
 
 
 # configs[3]'s shape at a size the oracle finishes: 20 M genome-sampled reads (2.4e9 windows) under a
