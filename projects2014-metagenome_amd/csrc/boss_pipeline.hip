@@ -66,7 +66,7 @@ class Workspace {
         SK_OWN, SK_TCNT, SK_TOFF, SK_WORDS, SK_LENS, SK_CNT, SK_RWORDS, SK_RLENS, SK_RCNT, SK_NW, SK_WOFF, SK_SEQ,
         SK_STARTS, SK_RID, CANON_IDX, SPEC_A, SPEC_B, SPEC_CAP, SPEC_CUR, GAP_BSTART, GAP_USTART, CANON, CANONC,
         FUSED_SEL, WN, SPEC_AC, SPEC_BC, SPEC1_CAPS, SPEC1_START, SPEC1_TV, QINDEX, DBITMAP, RC_L1START, RC_L1CUR, RC_TILEG,
-        KA2, ROUND_DELTA, XA2, XAC2, CA2, NSLOTS
+        KA2, ROUND_DELTA, XA2, XAC2, CA2, SPEC_MID_TV, NSLOTS
     };
     ~Workspace() {
         // every device block once, by its base (a slot or kept entry may be a piece of one: carve)
@@ -81,7 +81,7 @@ class Workspace {
             int root = -1;
             void *p = take_cached(bytes, &cap, &root);
             if (!p) {
-                cap = bytes + bytes / 8;
+                cap = bytes + std::min<size_t>(bytes / 8, 1ull << 30);
                 const auto t0 = std::chrono::steady_clock::now();
                 bool dropped = false, carved = false;
                 if (carve_always) {
@@ -99,7 +99,7 @@ class Workspace {
                     carved = p != nullptr;
                     while (!p && !cache_.empty() && drop_largest()) {
                         dropped = true;
-                        cap = bytes + bytes / 8;
+                        cap = bytes + std::min<size_t>(bytes / 8, 1ull << 30);
                         if (!try_malloc(&p, cap, &root)) p = nullptr;
                     }
                     if (!p && !try_malloc(&p, cap, &root)) {
@@ -493,6 +493,14 @@ struct Ctx {
     // positions, tile t of the level-2 tiling holding keys in its first gap1_tv[t] positions
     uint64_t gap1_n = 0;
     const uint32_t *gap1_tv = nullptr;
+    // the previous-level buckets a padded input's keys occupy, [gap1_lo, gap1_hi) (spec_mid_level; 0 / 0:
+    // unknown, every bucket)
+    uint64_t gap1_lo = 0, gap1_hi = 0;
+    // a 3-level sort's speculative middle level (spec_mid_level) partitions into this buffer (the batched
+    // collect's KB, sized for it); MTG_SPEC_MID=0: the exact middle level
+    void *spec_mid_into = nullptr;
+    uint64_t spec_mid_bytes = 0;
+    bool spec_mid = true;
     // bucket index over the real edges, built by the dummy stage and reused by the split emit
     const void *bidx_keys = nullptr;
     uint64_t bidx_n = 0;
@@ -537,6 +545,7 @@ static void load_knobs(Ctx &c) {
     c.spec_inplace = !is("MTG_SPEC_INPLACE", "0");
     c.round_bits = !is("MTG_ROUND_BITS", "0");
     c.round_index = !is("MTG_ROUND_INDEX", "0");
+    c.spec_mid = !is("MTG_SPEC_MID", "0");
     if (const char *e = getenv("MTG_DIST_PIECES")) {
         c.dist_pieces = (uint32_t)std::max(1L, std::min(16L, atol(e)));
         c.dist_pieces_set = true;
@@ -821,13 +830,34 @@ struct RcMerge {
 // of slack (a bucket of ~4600 keys overflows with probability ~1e-10 at a 1/8 sample)
 // (buckets outside [blo, bhi) -- below the input's first or above its last previous-level prefix --
 // hold no key and get no slack: a round of a batched collect fills a fraction of the buckets)
+// align (a speculative middle level): capacities rounded up to whole tiles of the next level's tiling
 __global__ void spec_caps_kernel(const uint32_t *__restrict__ sample, uint64_t nb, uint32_t stride,
-                                 uint32_t *__restrict__ cap, bool tiny, uint64_t blo, uint64_t bhi) {
+                                 uint32_t *__restrict__ cap, bool tiny, uint64_t blo, uint64_t bhi,
+                                 uint32_t align = 0) {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
-    if (b < blo || b >= bhi) cap[b] = 0;
-    else cap[b] = tiny ? (uint32_t)(((uint64_t)sample[b] * stride) / 2)
-                       : (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
+    if (b < blo || b >= bhi) {
+        cap[b] = 0;
+        return;
+    }
+    uint32_t v = tiny ? (uint32_t)(((uint64_t)sample[b] * stride) / 2)
+                      : (uint32_t)(((uint64_t)sample[b] * stride * 6) / 5) + 512u;
+    if (align) v = (v + align - 1) / align * align;
+    cap[b] = v;
+}
+
+// the tile fill of a speculative middle level's output (tile-aligned buckets [bstart[b], bstart[b + 1]),
+// keys up to cur[b]): tile t holds keys in its first tv[t] positions -- the padded-input convention of
+// the next level's kernels (Ctx::gap1_tv)
+__global__ void spec_tile_fill_kernel(const uint64_t *__restrict__ bstart, const unsigned long long *__restrict__ cur,
+                                      uint64_t nb, uint32_t tile, uint32_t *__restrict__ tv) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const uint64_t s = bstart[b], e = bstart[b + 1], k = cur[b];
+    for (uint64_t t = s / tile; t < e / tile; ++t) {
+        const uint64_t t0 = t * tile;
+        tv[t] = (uint32_t)(k <= t0 ? 0 : min<uint64_t>(tile, k - t0));
+    }
 }
 
 // The final MSD level of the main sort (level 2 after the fused K1's level 1) without its exact
@@ -922,7 +952,10 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // the buckets the keys can occupy: those under the previous level's first and last prefix
         // (a padded input's ends are not keys: every bucket)
         uint64_t blo = 0, bhi = nb;
-        if (bp && !g1) {
+        if (g1 && c.gap1_hi > c.gap1_lo) {  // a speculative middle level's output: its key range is known
+            blo = c.gap1_lo << (bb - bp);
+            bhi = std::min<uint64_t>(nb, c.gap1_hi << (bb - bp));
+        } else if (bp && !g1) {
             Key<L> ends[2];
             HIP_CHECK(hipMemcpyAsync(&ends[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
             HIP_CHECK(hipMemcpyAsync(&ends[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
@@ -988,7 +1021,7 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
         // g1: the padded input stays marked (Ctx::gap1_n) until this level succeeds -- a local pass that
         // overflows below returns ~0 and the caller's exact level must read the padded array again
         auto consumed_gap1 = [&]() {
-            if (g1) c.gap1_n = 0, c.gap1_tv = nullptr;  // the buckets below are compact per bucket
+            if (g1) c.gap1_n = 0, c.gap1_tv = nullptr, c.gap1_lo = c.gap1_hi = 0;  // the buckets below are compact per bucket
         };
         if (rm) {  // the fused rc merge over the speculative buckets
             uint32_t *cnt = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
@@ -1184,6 +1217,85 @@ static uint64_t spec_final_level(Ctx &c, Key<L> **keys, uint32_t **vals, uint64_
     }
 }
 
+// The middle level of a 3-level sort without its exact histogram pass (a 60 GB read per configs[3]
+// round): the level-2 buckets are sized from a sample with slack and rounded up to whole tiles of the
+// level-3 tiling, the keys go from *keys into them in *alt (the caller's buffer of c.spec_mid_bytes,
+// Ctx::spec_mid_into), and the padded result is marked for level 3 as the speculative level-1 layout is
+// for level 2 (Ctx::gap1_n / gap1_tv: tile t holds keys in its first tv[t] positions), with the
+// level-2 prefix range of the keys (gap1_lo / gap1_hi) for level 3's bucket range.  False (nothing the
+// caller needs touched) when it does not fit or a bucket overflowed: the exact level then.
+template <int L, bool COUNTED>
+static bool spec_mid_level(Ctx &c, Key<L> **keys, Key<L> **alt, uint64_t n, unsigned nbits, unsigned bp, unsigned bb) {
+    if constexpr (L != 1 || COUNTED) {
+        return false;
+    } else {
+        constexpr int TILE = MsdTraits<L>::TILE;
+        constexpr uint32_t SS = 8;
+        const uint64_t tiles = ceil_div(n, TILE);
+        if (c.use_lsd || !c.spec_final || tiles < 64 * SS || bb - bp > 9 || bb > 24 || !bp) return false;
+        const uint64_t nb = 1ull << bb;
+        uint32_t *h = (uint32_t *)c.ws.get(Workspace::MSD_COUNTS, nb * 4);
+        HIP_CHECK(hipMemsetAsync(h, 0, nb * 4, c.stream));
+        // every 8th tile (level-1 buckets span hundreds of tiles here)
+        msd_hist_kernel<L><<<dim3((unsigned)ceil_div(tiles, SS)), dim3(MSD_BLOCK), 0, c.stream>>>(*keys, n, nbits, bb, bp, h,
+                                                                                                SS, 1, 1, nullptr);
+        HIP_CHECK(hipGetLastError());
+        Key<L> ends[2];
+        HIP_CHECK(hipMemcpyAsync(&ends[0], *keys, sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipMemcpyAsync(&ends[1], *keys + (n - 1), sizeof(Key<L>), hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        const uint64_t lo1 = ends[0].w[0] >> (nbits - bp), hi1 = ends[1].w[0] >> (nbits - bp);
+        const uint64_t blo = lo1 << (bb - bp), bhi = std::min<uint64_t>(nb, (hi1 + 1) << (bb - bp));
+        uint32_t *cap = (uint32_t *)c.ws.get(Workspace::SPEC_CAP, nb * 4);
+        spec_caps_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(h, nb, SS, cap, c.spec_tiny, blo,
+                                                                                        bhi, (uint32_t)TILE);
+        HIP_CHECK(hipGetLastError());
+        uint64_t *bstart = (uint64_t *)c.ws.get(Workspace::MSD_BSTART, (nb + 1) * 8);
+        {
+            uint32_t ep;
+            const uint64_t st = ceil_div(nb, 4096);
+            uint64_t *desc = acquire_desc(c, st, &ep);
+            HIP_CHECK(hipMemsetAsync(&c.small->counter, 0, 4, c.stream));
+            scan_counts_kernel<<<dim3((unsigned)st), dim3(512), 0, c.stream>>>(cap, nb, bstart, desc, ep,
+                                                                              &c.small->counter, &c.small->error);
+            HIP_CHECK(hipGetLastError());
+        }
+        const uint64_t C = read_u64(c, (const unsigned long long *)(bstart + nb));
+        if (C * sizeof(Key<L>) > c.spec_mid_bytes) {
+            if (c.debug) fprintf(stderr, "[mtg debug] speculative middle level: capacity %lu does not fit\n", (unsigned long)C);
+            return false;
+        }
+        auto *cur = (unsigned long long *)c.ws.get(Workspace::SPEC_CUR, nb * 8);
+        HIP_CHECK(hipMemcpyAsync(cur, bstart, nb * 8, hipMemcpyDeviceToDevice, c.stream));
+        HIP_CHECK(hipMemsetAsync(&c.small->spec_ovf, 0, 4, c.stream));
+        msd_partition_kernel<L, false><<<dim3((unsigned)xcd_grid(tiles)), dim3(MSD_BLOCK), 0, c.stream>>>(
+            *keys, *alt, nullptr, nullptr, n, nbits, bb, bp, cur, 1, (const unsigned long long *)(bstart + 1),
+            &c.small->spec_ovf, nullptr);
+        HIP_CHECK(hipGetLastError());
+        const uint64_t ntv = C / TILE;
+        uint32_t *tv = (uint32_t *)c.ws.get(Workspace::SPEC_MID_TV, std::max<uint64_t>(ntv, 1) * 4);
+        spec_tile_fill_kernel<<<dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, c.stream>>>(bstart, cur, nb, TILE, tv);
+        HIP_CHECK(hipGetLastError());
+        uint32_t povf = 0;
+        HIP_CHECK(hipMemcpyAsync(&povf, &c.small->spec_ovf, 4, hipMemcpyDeviceToHost, c.stream));
+        HIP_CHECK(hipStreamSynchronize(c.stream));
+        if (povf) {
+            if (c.debug) fprintf(stderr, "[mtg debug] speculative middle level: a bucket overflowed, exact level\n");
+            ++c.timings.spec_fallbacks;
+            return false;
+        }
+        std::swap(*keys, *alt);
+        c.gap1_n = C;
+        c.gap1_tv = tv;
+        c.gap1_lo = blo, c.gap1_hi = bhi;
+        ++c.timings.spec_levels;
+        if (c.debug)
+            fprintf(stderr, "[mtg debug] speculative middle level: n=%lu capacity=%lu (%.2fx)\n", (unsigned long)n,
+                    (unsigned long)C, (double)C / (double)n);
+        return true;
+    }
+}
+
 template <int L, bool COUNTED>
 static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **vals,
                                 uint32_t **valt, uint64_t n, unsigned nbits, uint32_t cmax,
@@ -1220,8 +1332,9 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
         const unsigned bb = digit_end[lev], bp = digit_end[lev - 1];
         nbuckets = 1ull << bb;
         const uint32_t *cnt = hist1;
-        // level 2 after a speculative level-1 layout reads the padded array (c.gap1_n positions)
-        const bool g1 = lev == 2 && level1_done && c.gap1_n;
+        // level 2 after a speculative level-1 layout reads the padded array (c.gap1_n positions), and so
+        // does level 3 after a speculative middle level (spec_mid_level)
+        const bool g1 = c.gap1_n && (lev == 2 ? level1_done : lev == 3);
         const uint64_t npos = g1 ? c.gap1_n : n, ltiles = g1 ? ceil_div(npos, TILE) : tiles;
         const uint32_t *tv = g1 ? c.gap1_tv : nullptr;
         if (lev != 1 || !hist1) {
@@ -1266,7 +1379,7 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
             *keys, *alt, COUNTED ? *vals : nullptr, COUNTED ? *valt : nullptr, npos, nbits, bb, bp, cur, 1, nullptr,
             nullptr, tv);
         HIP_CHECK(hipGetLastError());
-        if (g1) c.gap1_n = 0, c.gap1_tv = nullptr;  // compact from here on
+        if (g1) c.gap1_n = 0, c.gap1_tv = nullptr, c.gap1_lo = c.gap1_hi = 0;  // compact from here on
         tm.mark();
         if (c.track_partition && c.radix_launches == 0) {  // first partition launch of the sort
             HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -1319,6 +1432,13 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                                                                 digit_end[lev], cmax, distinct, rm, saved_gidx, fine,
                                                                 spare);
                 if (u != ~0ull) return u;
+            }
+            // a 3-level sort's middle level without its histogram pass, into the caller's buffer
+            if (lev == 2 && levels == 3 && level1_done && !c.gap1_n && c.spec_mid && c.spec3 && *alt &&
+                c.spec_mid_into == (void *)*alt &&
+                spec_mid_level<L, COUNTED>(c, keys, alt, n, nbits, digit_end[1], digit_end[2])) {
+                b = digit_end[2];
+                continue;
             }
             run_level(lev);
         }
@@ -2090,6 +2210,7 @@ static bool stage_extract_fused(Ctx &c, unsigned K, bool canonical, uint32_t cma
         const bool spec1 = !COUNTED && K <= 32 && c.spec_l1 && npos >= c.spec_l1_min;
         c.gap1_n = 0;
         c.gap1_tv = nullptr;
+        c.gap1_lo = c.gap1_hi = 0;
         if (spec1) {
             fused_pass_a(c, K, canonical, in, &A, c.spec_l1_sample);
             const MsdPlan plan = fused_plan(c, A.N, 2 * K, A.dup, true);
@@ -2140,7 +2261,7 @@ static uint64_t stage_collect(Ctx &c, unsigned K, uint32_t cmax, Key<L2> **ka, K
                               const uint32_t *hist1 = nullptr, const MsdPlan *plan = nullptr) {
     // hist1 != nullptr: *ka is already scattered by the level-1 digit (stage_extract_fused)
     uint64_t U = 0;
-    if (!hist1) c.gap1_n = 0, c.gap1_tv = nullptr;
+    if (!hist1) c.gap1_n = 0, c.gap1_tv = nullptr, c.gap1_lo = c.gap1_hi = 0;
     if (c.use_lsd) {
         radix_sort<L2, COUNTED>(c, ka, kb, ca, cb, N, 2 * K, track);
         reset_small(c);
@@ -2395,7 +2516,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     uint64_t ka_keys = one_b ? nr[0] : nmax;
     struct SpareGuard {  // never left set past this function (a thrown build included)
         Ctx &c;
-        ~SpareGuard() { c.spec_into = nullptr, c.spec_into_bytes = 0; }
+        ~SpareGuard() { c.spec_into = nullptr, c.spec_into_bytes = 0, c.spec_mid_into = nullptr, c.spec_mid_bytes = 0; }
     } spare_guard{c};
     if (L == 1 && !COUNTED && plan.levels == 3 && c.spec3 && c.spec_final && c.spec_inplace && !c.use_lsd) {
         double fmax = 0;
@@ -2409,7 +2530,21 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     K2 *ka = (K2 *)c.ws.get(Workspace::KA, ka_keys * sizeof(K2));
     if (L == 1 && ka_keys > (one_b ? nr[0] : nmax)) c.spec_into = ka, c.spec_into_bytes = ka_keys * sizeof(K2);
     K2 *ka2 = one_b ? (K2 *)c.ws.get(Workspace::KA2, std::max<uint64_t>(nr[1], 1) * sizeof(K2)) : nullptr;
-    K2 *kb = (K2 *)c.ws.get(Workspace::KB, nmax * sizeof(K2));
+    // ... and the speculative middle level (spec_mid_level) partitions into KB: sized for its tile-aligned
+    // slack buckets -- 1.2 n + 512 keys and up to one tile a bucket -- when that fits too
+    uint64_t kb_keys = nmax;
+    if (L == 1 && c.spec_into && c.spec_mid && plan.levels == 3) {
+        double fmax = 0;
+        for (uint32_t r = 0; r < R; ++r) fmax = std::max(fmax, (double)(bb[r + 1] - bb[r]) / (double)nb1);
+        const double mcap = 1.2 * (double)nmax * 1.05 +
+                            (512.0 + MsdTraits<L>::TILE) * (double)(1ull << plan.digit_end[2]) * fmax + 65536.0;
+        const double kbb = (double)sizeof(K2);
+        const double need = ((double)ka_keys + (one_b ? (double)nr[1] : 0.0) + mcap) * kbb + u_est * 1.25 * kbb +
+                            (double)(1ull << 30);
+        if (need <= budget) kb_keys = (uint64_t)mcap;
+    }
+    K2 *kb = (K2 *)c.ws.get(Workspace::KB, kb_keys * sizeof(K2));
+    if (kb_keys > nmax) c.spec_mid_into = kb, c.spec_mid_bytes = kb_keys * sizeof(K2);
     uint32_t *ca = COUNTED ? (uint32_t *)c.ws.get(Workspace::CA, nmax * 4) : nullptr;
     uint32_t *cb = COUNTED ? (uint32_t *)c.ws.get(Workspace::CB, nmax * 4) : nullptr;
     tr("rounds: buffers", R, nmax);
@@ -2540,7 +2675,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         if (COUNTED) *outc = (uint32_t *)c.ws.get(Workspace::CANONC, 4);
     }
     debug_check_sorted(c, "canonical rounds", *out, off);
-    c.spec_into = nullptr, c.spec_into_bytes = 0;
+    c.spec_into = nullptr, c.spec_into_bytes = 0, c.spec_mid_into = nullptr, c.spec_mid_bytes = 0;
     // the round buffers (sized for the largest round) go; the rc stage takes KB and SPEC_A again at
     // its own size
     for (auto sl : {Workspace::KA, Workspace::KA2, Workspace::CA, Workspace::KB, Workspace::CB, Workspace::SPEC_A,

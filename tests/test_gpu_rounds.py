@@ -70,14 +70,17 @@ def test_rounds_pass_b_per_round_knob(small_fused, k):
                 assert t.collect_mode == ROUNDS and t.n_batches == 2, (t.collect_mode, t.n_batches)
 
 
-@pytest.mark.parametrize("knob", ["MTG_ROUND_INDEX", "MTG_ROUND_BITS", "MTG_ROUNDS_ONE_B"])
-def test_rounds_2m_knobs_off(monkeypatch, knob):
+@pytest.mark.parametrize("knob,value", [("MTG_ROUND_INDEX", "0"), ("MTG_ROUND_BITS", "0"), ("MTG_ROUNDS_ONE_B", "0"),
+                                         ("MTG_SPEC_MID", "0"), ("MTG_SPEC_CAPS", "tiny")])
+def test_rounds_2m_knobs_off(monkeypatch, knob, value):
     # the batched collect's defaults each switched off in turn on 2 M genome reads of 3 MSD levels in 2
     # rounds: the canonical set's bucket index written by the rounds' gathers (MTG_ROUND_INDEX), one final
-    # bit fewer in a sparse round (MTG_ROUND_BITS), one pass B for both rounds (MTG_ROUNDS_ONE_B)
+    # bit fewer in a sparse round (MTG_ROUND_BITS), one pass B for both rounds (MTG_ROUNDS_ONE_B), the
+    # speculative middle level (MTG_SPEC_MID); halved speculative capacities (MTG_SPEC_CAPS=tiny) make the
+    # middle and final levels overflow and fall back to the exact ones
     monkeypatch.setenv("MTG_RANGES", "2")
     monkeypatch.setenv("MTG_MSD_LEVELS", "3")
-    monkeypatch.setenv(knob, "0")
+    monkeypatch.setenv(knob, value)
     asc = bench.make_reads_host_codes(2_000_000, 150, 4242, "genome", 10.0)
     ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, num_threads=8)
     ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)
@@ -85,7 +88,9 @@ def test_rounds_2m_knobs_off(monkeypatch, knob):
     t = ctor.timings()
     assert t.collect_mode == ROUNDS and t.n_batches == 2
     reads = [asc[i].tobytes() for i in range(len(asc))]
-    assert_same(got, O.build_chunk(30, reads, canonical=True), "2M reads k=31, 2 rounds, %s=0" % knob)
+    assert_same(got, O.build_chunk(30, reads, canonical=True), "2M reads k=31, 2 rounds, %s=%s" % (knob, value))
+    if knob == "MTG_SPEC_CAPS":
+        assert t.spec_fallbacks > 0, t.spec_fallbacks
 
 
 def test_rounds_counts_saturate(small_fused):
