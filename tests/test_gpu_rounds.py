@@ -73,7 +73,7 @@ def test_rounds_pass_b_per_round_knob(small_fused, k):
 @pytest.mark.parametrize("knob,value", [("MTG_ROUND_INDEX", "0"), ("MTG_ROUND_BITS", "0"), ("MTG_ROUNDS_ONE_B", "0"),
                                          ("MTG_SPEC_MID", "0"), ("MTG_SPEC_CAPS", "tiny")])
 def test_rounds_2m_knobs_off(monkeypatch, knob, value):
-    # the batched collect's defaults each switched off in turn on 2 M genome reads of 3 MSD levels in 2
+    # the batched collect's defaults each switched off in turn on 1 M genome reads of 3 MSD levels in 2
     # rounds: the canonical set's bucket index written by the rounds' gathers (MTG_ROUND_INDEX), one final
     # bit fewer in a sparse round (MTG_ROUND_BITS), one pass B for both rounds (MTG_ROUNDS_ONE_B), the
     # speculative middle level (MTG_SPEC_MID); halved speculative capacities (MTG_SPEC_CAPS=tiny) make the
@@ -81,14 +81,14 @@ def test_rounds_2m_knobs_off(monkeypatch, knob, value):
     monkeypatch.setenv("MTG_RANGES", "2")
     monkeypatch.setenv("MTG_MSD_LEVELS", "3")
     monkeypatch.setenv(knob, value)
-    asc = bench.make_reads_host_codes(2_000_000, 150, 4242, "genome", 10.0)
+    asc = bench.make_reads_host_codes(1_000_000, 150, 4242, "genome", 10.0)
     ctor = boss.IBOSSChunkConstructor.initialize(30, both_strands=True, num_threads=8)
     ctor.add_packed(asc.reshape(-1), np.arange(len(asc) + 1, dtype=np.uint64) * 150)
     got = ctor.build_chunk()
     t = ctor.timings()
     assert t.collect_mode == ROUNDS and t.n_batches == 2
     reads = [asc[i].tobytes() for i in range(len(asc))]
-    assert_same(got, O.build_chunk(30, reads, canonical=True), "2M reads k=31, 2 rounds, %s=%s" % (knob, value))
+    assert_same(got, O.build_chunk(30, reads, canonical=True), "1M reads k=31, 2 rounds, %s=%s" % (knob, value))
     if knob == "MTG_SPEC_CAPS":
         assert t.spec_fallbacks > 0, t.spec_fallbacks
 
