@@ -2011,6 +2011,12 @@ struct BucketSel {
     }
 };
 
+// the u128 pass B as the packed-word kernel (extract_partition_fast2_kernel): uncounted basic / canonical
+template <int L, bool COUNTED>
+static inline bool fast2_applies(const Ctx &c, unsigned K, bool canonical) {
+    return L == 2 && !COUNTED && c.fast2 && K > 32 && K <= 64 && cmode(c, canonical) <= 1;
+}
+
 // pass B: the k-mers whose level-1 bucket (top b1 bits) is in `sel` (nullptr: every bucket)
 // scattered into ka by that bucket; returns their number and their level-1 counts in *dh1 (device;
 // zero outside `sel`)
@@ -2018,8 +2024,9 @@ template <int L, bool COUNTED>
 static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, const BuildInput &in,
                              const FusedA &A, unsigned b1, const BucketSel *sel, Key<L> *ka, uint32_t *ca,
                              const uint32_t **dh1_out, const long long *bdelta = nullptr) {
-    // bdelta (the u64 pass B only): per level-1 bucket, where its keys go relative to ka (elements) --
-    // the collect rounds' one pass B writes each round's buckets into that round's own buffer
+    // bdelta (the u64 pass B and the u128 packed-word one): per level-1 bucket, where its keys go relative
+    // to ka (elements) -- the collect rounds' one pass B writes each round's buckets into that round's own
+    // buffer
     const uint32_t nb1 = 1u << b1;
     const unsigned hb = FUSED_HB;
     if (sel && nb1 > 32 * FUSED_SEL_WORDS) throw std::runtime_error("collect round mask: level-1 digit too wide");
@@ -2057,22 +2064,23 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
     EventTimer tm(c.stream);
     tm.mark();
     const bool fast_b = L == 1 && !COUNTED && K <= 32;
-    if (bdelta && !fast_b) throw std::runtime_error("per-bucket destinations need the u64 pass B");
+    if (bdelta && !fast_b && !fast2_applies<L, COUNTED>(c, K, canonical))
+        throw std::runtime_error("per-bucket destinations need the u64 or the packed-word u128 pass B");
     if constexpr (L == 2) {
         // u128 windows (K <= 64): pass B on 256-thread tiles (A was made for them); uncounted canonical /
         // basic builds take the packed-word kernel (MTG_FAST2=0: the generic one)
         constexpr int B = fused_block<2>();
         if (b1 > 9) throw std::runtime_error("the u128 pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, B>::TILE);
-        if (!COUNTED && c.fast2 && K > 32 && K <= 64 && cmode(c, canonical) <= 1) {
+        if (fast2_applies<L, COUNTED>(c, K, canonical)) {
             if (K == 63 && c.kspec)
                 extract_partition_fast2_kernel<B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
                     in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
-                    (const uint32_t *)dsel);
+                    (const uint32_t *)dsel, bdelta);
             else
                 extract_partition_fast2_kernel<B><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
                     in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
-                    (const uint32_t *)dsel);
+                    (const uint32_t *)dsel, bdelta);
         } else if (K == 63 && c.kspec)
             extract_partition_kernel<2, COUNTED, B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
                 in.seq, in.seq_len, K, cmode(c, canonical), in.read_starts, in.read_counts, in.n_reads, in.rid_at, cmax, b1,
@@ -2496,14 +2504,15 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
         for (uint64_t b = bb[r]; b < bb[r + 1]; ++b) nr[r] += h1[b];
         nmax = std::max(nmax, nr[r]);
     }
-    // two rounds of the u64 pass B (configs[3]'s share) become one when both rounds' keys fit beside the
+    // two rounds of pass B (configs[3]'s share; configs[2]'s u128 rounds) become one when both rounds' keys fit beside the
     // partition buffer and the canonical set: the pass writes round 0's buckets into KA and round 1's into
     // KA2 (per-bucket destinations, bdelta), so the reads are scanned once (pass B 2 x 40 -> 45 ms).
     // MTG_ROUNDS_ONE_B=0: a pass B per round.  (Round 5 kept it off: the third ~64 GB block left the later
     // stages no room -- their 4-20 GB requests each took a whole idle 64 GB block -- until the workspace
     // learned to carve pieces off its kept blocks, Workspace::take_cached)
     bool one_b = false;
-    if (R == 2 && c.rounds_one_b && L == 1 && !COUNTED && K <= 32) {
+    // (u128, configs[2]: both rounds' keys, 141 GB, beside KB and the canonical set -- ~255 of the 309 GB)
+    if (R == 2 && c.rounds_one_b && ((L == 1 && !COUNTED && K <= 32) || fast2_applies<L, COUNTED>(c, K, canonical))) {
         const double kb = (double)sizeof(K2);
         const double need = ((double)N + (double)nmax) * kb + u_est * 1.25 * kb + (double)(1ull << 30);
         one_b = need <= budget;

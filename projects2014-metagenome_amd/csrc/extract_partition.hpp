@@ -555,7 +555,9 @@ template <int BLOCK, int KC = 0>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
-    Key<2> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr) {
+    Key<2> *__restrict__ kout, uint32_t *__restrict__ error, const uint32_t *__restrict__ sel = nullptr,
+    const long long *__restrict__ bdelta = nullptr) {
+    // bdelta: as in extract_partition_fast_kernel (the collect rounds' one pass B for configs[2]'s two rounds)
     const unsigned K = KC ? (unsigned)KC : K_;
     constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 5;  // +5 words: a thread's windows reach 15 + 63 chars on
     constexpr int NBMAX = 512;
@@ -691,6 +693,8 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
             if (c[q] && g + c[q] > be[q]) {  // pass A counted this bucket differently: never
                 atomicOr(error, 2u);          // write past its range
                 g = ~0ull;
+            } else if (bdelta) {
+                g += (unsigned long long)bdelta[i];
             }
             s_gbase[i] = g;
         }

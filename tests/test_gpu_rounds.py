@@ -227,6 +227,21 @@ def test_rounds_u128_random_reads(small_fused, rounds, k):
             assert t.collect_mode == ROUNDS and t.n_batches == rounds, (t.collect_mode, t.n_batches)
 
 
+@pytest.mark.parametrize("k", [33, 62, 63])
+def test_rounds_u128_pass_b_per_round_knob(small_fused, k):
+    # configs[2]'s two u128 rounds share one packed-word pass B (extract_partition_fast2_kernel with per-bucket
+    # destinations: round 1's buckets into KA2); MTG_ROUNDS_ONE_B=0: a pass B per round.  Counted builds take
+    # the generic pass B, one per round
+    small_fused.setenv("MTG_RANGES", "2")
+    reads = _random_reads(7000 + k, 300, 150, 6000, n_rate=0.005, lower=True)
+    for one_b in ("1", "0"):
+        small_fused.setenv("MTG_ROUNDS_ONE_B", one_b)
+        for canonical in (False, True):
+            for bits in (0, 16):
+                _, t = _check(k, reads, canonical, bits)
+                assert t.collect_mode == ROUNDS and t.n_batches == 2, (t.collect_mode, t.n_batches)
+
+
 @pytest.mark.parametrize("k", [32, 47, 62, 63])
 def test_rounds_u128_generic_pass_b(small_fused, k):
     # MTG_FAST2=0: the uncounted u128 rounds' pass B as the generic extract_partition_kernel<2> (slide_windows)
