@@ -393,6 +393,8 @@ struct Ctx {
     unsigned fused_b1 = 0;         // MTG_FUSED_B1=n: the fused K1's level-1 digit forced to n bits (A/B runs)
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
     bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
+    bool fast2_ppt8 = true;        // MTG_FAST2_PPT8=0: the u128 packed-word pass B at 16 windows a thread (256 threads)
+    bool lu_wpe2 = true;           // MTG_LU_WPE2=0: the u128 local unique compiled for 1 wave per SIMD (no VGPR cap)
     bool fast2 = true;             // MTG_FAST2=0: the u128 rounds' pass B as the generic extract_partition_kernel
     int canon_mode = 1;            // the single-build extraction's canonical representative (cmode); the
                                    // super-k-mer owners of a multi-GPU build extract with 2
@@ -533,6 +535,8 @@ static void load_knobs(Ctx &c) {
     c.wide_b1 = !is("MTG_WIDE_B1", "0");
     c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
     c.lu_fast = !is("MTG_LU_FAST", "0");
+    c.lu_wpe2 = !is("MTG_LU_WPE2", "0");
+    c.fast2_ppt8 = !is("MTG_FAST2_PPT8", "0");
     c.fast2 = !is("MTG_FAST2", "0");
     if (const char *e = getenv("MTG_MERGE_IT")) c.merge_it = (uint32_t)std::max(1L, std::min(64L, atol(e)));
     if (const char *v = getenv("MTG_FUSED_B1")) c.fused_b1 = (unsigned)std::min(10, std::max(0, atoi(v)));
@@ -1567,6 +1571,17 @@ static uint64_t msd_sort_unique(Ctx &c, Key<L> **keys, Key<L> **alt, uint32_t **
                             return;
                         }
                     }
+                    // u128 keys (configs[2]): the state-word table at <= 80 VGPRs, so three workgroups fit a CU
+                    // (the LDS allows three; 93 VGPRs allowed two)
+                    if constexpr (L == 2 && !KC && !ND && !COUNTED) {
+                        if (c.lu_wpe2) {
+                            local_unique_kernel<L, COUNTED, KC, 512, SL, ND, 6><<<dim3(cnt), dim3(512), 0, c.stream>>>(
+                                *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits,
+                                *alt, COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax, nullptr,
+                                glist ? 0 : g0);
+                            return;
+                        }
+                    }
                     local_unique_kernel<L, COUNTED, KC, 512, SL, ND, WPE><<<dim3(cnt), dim3(512), 0, c.stream>>>(
                         *keys, COUNTED ? *vals : nullptr, gstart, glist ? glist + g0 : nullptr, nbits, b, sbits, *alt,
                         COUNTED ? *valt : nullptr, ucount, ovf, &c.small->counter, cmax, nullptr, glist ? 0 : g0);
@@ -2073,7 +2088,17 @@ static uint64_t fused_pass_b(Ctx &c, unsigned K, bool canonical, uint32_t cmax, 
         if (b1 > 9) throw std::runtime_error("the u128 pass B takes at most 9 bits");
         const uint64_t ftiles = ceil_div(A.npos, FusedTraits<COUNTED, B>::TILE);
         if (fast2_applies<L, COUNTED>(c, K, canonical)) {
-            if (K == 63 && c.kspec)
+            // the same 4096-window tiles as 512 threads of 8 windows (twice the waves a CU at the same LDS)
+            static_assert(FusedTraits<COUNTED, B>::TILE == 512 * 8, "a pass-B tile = 512 threads x 8 windows");
+            if (c.fast2_ppt8 && K == 63 && c.kspec)
+                extract_partition_fast2_kernel<512, 63, 8><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+                    in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
+                    (const uint32_t *)dsel, bdelta);
+            else if (c.fast2_ppt8)
+                extract_partition_fast2_kernel<512, 0, 8><<<dim3((unsigned)xcd_grid(ftiles)), dim3(512), 0, c.stream>>>(
+                    in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
+                    (const uint32_t *)dsel, bdelta);
+            else if (K == 63 && c.kspec)
                 extract_partition_fast2_kernel<B, 63><<<dim3((unsigned)xcd_grid(ftiles)), dim3(B), 0, c.stream>>>(
                     in.seq, in.seq_len, K, cmode(c, canonical), b1, A.per_stripe, scur, send, (Key<2> *)ka, &c.small->error,
                     (const uint32_t *)dsel, bdelta);

@@ -551,7 +551,11 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast_kernel(
 // puts it in the label; validity is the K-bit field of the 80-bit invalid mask.  Same k-mers as
 // slide_windows<2> (forward and rc plain words, plain_to_boss, rc < fwd picks rc), so the same output as
 // extract_partition_kernel<2>.  canonical: 0 / 1 only (the routed u128 collect is not fused).
-template <int BLOCK, int KC = 0>
+// PPT = 8 (round 6): 8 windows a thread on 512-thread tiles of the same 4096 windows -- a thread starts at
+// char 8 t, half-way into a packed word, so its five words are funnel-shifted by 16 bits from six.  Twice the
+// waves per CU at the same LDS (the tile's 64 KB of staged keys held 16 windows a thread at 256 threads:
+// 8 waves a CU; configs[2]'s pass B ran at 2.1 TB/s of writes)
+template <int BLOCK, int KC = 0, int PPT_ = 16>
 __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
     const uint8_t *__restrict__ seq, uint64_t seq_len, unsigned K_, int canonical, unsigned b,
     uint64_t per_stripe, unsigned long long *__restrict__ cursor, const unsigned long long *__restrict__ bend,
@@ -559,7 +563,8 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
     const long long *__restrict__ bdelta = nullptr) {
     // bdelta: as in extract_partition_fast_kernel (the collect rounds' one pass B for configs[2]'s two rounds)
     const unsigned K = KC ? (unsigned)KC : K_;
-    constexpr int PPT = 16, TILE = BLOCK * PPT, NW = BLOCK + 5;  // +5 words: a thread's windows reach 15 + 63 chars on
+    static_assert(PPT_ == 16 || PPT_ == 8, "16 or 8 windows a thread");
+    constexpr int PPT = PPT_, TILE = BLOCK * PPT, NW = TILE / 16 + 5;  // +5 words: a thread's windows reach 15 + 63 chars on
     constexpr int NBMAX = 512;
     constexpr int PER = NBMAX / BLOCK > 0 ? NBMAX / BLOCK : 1;
     static_assert(TILE <= 65536, "u16 in-tile offsets");
@@ -589,12 +594,28 @@ __global__ __launch_bounds__(BLOCK) void extract_partition_fast2_kernel(
     __syncthreads();
 
     uint32_t w[5];
+    uint64_t invlo, invhi;
+    if constexpr (PPT == 16) {
 #pragma unroll
-    for (int q = 0; q < 5; ++q) w[q] = s_pack[tid + q];
-    const uint64_t invlo = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) | ((uint64_t)s_inv[tid + 2] << 32) |
-                           ((uint64_t)s_inv[tid + 3] << 48);
-    const uint64_t invhi = s_inv[tid + 4];
-    const uint64_t p0 = base + 16ull * tid;
+        for (int q = 0; q < 5; ++q) w[q] = s_pack[tid + q];
+        invlo = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) | ((uint64_t)s_inv[tid + 2] << 32) |
+                ((uint64_t)s_inv[tid + 3] << 48);
+        invhi = s_inv[tid + 4];
+    } else {
+        // the thread's chars start at 8 t: word t / 2, char 8 (t & 1) -- five words from six, shifted by hc chars
+        const uint32_t wi = tid >> 1, hc = 8u * (tid & 1u);
+        uint32_t x[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) x[q] = s_pack[wi + q];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) w[q] = __builtin_amdgcn_alignbit(x[q + 1], x[q], 2 * hc);
+        const uint64_t a = (uint64_t)s_inv[wi] | ((uint64_t)s_inv[wi + 1] << 16) | ((uint64_t)s_inv[wi + 2] << 32) |
+                           ((uint64_t)s_inv[wi + 3] << 48);
+        const uint64_t bh = (uint64_t)s_inv[wi + 4] | ((uint64_t)s_inv[wi + 5] << 16);
+        invlo = hc ? (a >> hc) | (bh << (64 - hc)) : a;
+        invhi = hc ? bh >> hc : bh;
+    }
+    const uint64_t p0 = base + (uint64_t)PPT * tid;
     const uint32_t nwin = p0 < npos ? (uint32_t)min<uint64_t>(PPT, npos - p0) : 0u;
     const uint64_t maskK = K >= 64 ? ~0ull : (1ull << K) - 1;
     const unsigned hb = 2 * K - 64;                                   // bits of the high half (2 .. 64)

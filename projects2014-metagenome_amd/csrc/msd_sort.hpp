@@ -597,9 +597,9 @@ __global__ __launch_bounds__(LB) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         // 8.56 -> 8.29-8.38 ms in round 4, the 6-key batch spilled 16-20 bytes per lane to scratch);
         // MTG_LU_BATCH overrides it at build time for A/B runs
 #ifdef MTG_LU_BATCH
-        constexpr int BATCH = (KEYCAS && !COUNTED && !NODUP ? MTG_LU_BATCH : (LB >= 1024 ? 12 : WPE >= 8 ? 4 : 8)) / PAIR;
+        constexpr int BATCH = (KEYCAS && !COUNTED && !NODUP ? MTG_LU_BATCH : (LB >= 1024 ? 12 : WPE >= 6 ? 4 : 8)) / PAIR;
 #else
-        constexpr int BATCH = (LB >= 1024 ? 12 : WPE >= 8 ? 4 : 8) / PAIR;
+        constexpr int BATCH = (LB >= 1024 ? 12 : WPE >= 6 ? 4 : 8) / PAIR;
 #endif
         const uint64_t a0 = PAIR == 2 ? (g0 & ~1ull) : g0;
         for (uint64_t ib = a0 + (uint64_t)tid * PAIR; ib < g1 && !ovf; ib += (uint64_t)LB * BATCH * PAIR) {
