@@ -394,6 +394,7 @@ struct Ctx {
     bool wide_b1 = true;           // MTG_WIDE_B1=0: no 10-bit level 1 (fused_plan)
     bool lu_fast = true;           // MTG_LU_FAST=0: local_unique_kernel's per-key list positions (A/B)
     bool fast2_ppt8 = true;        // MTG_FAST2_PPT8=0: the u128 packed-word pass B at 16 windows a thread (256 threads)
+    bool rc_wide = true;           // MTG_RC_WIDE=0: the u128 rc sort planned like the unique (half-full merge groups)
     bool lu_wpe2 = true;           // MTG_LU_WPE2=0: the u128 local unique compiled for 1 wave per SIMD (no VGPR cap)
     bool fast2 = true;             // MTG_FAST2=0: the u128 rounds' pass B as the generic extract_partition_kernel
     int canon_mode = 1;            // the single-build extraction's canonical representative (cmode); the
@@ -536,6 +537,7 @@ static void load_knobs(Ctx &c) {
     c.kmc_mirror = !is("MTG_KMC_MIRROR", "0");
     c.lu_fast = !is("MTG_LU_FAST", "0");
     c.lu_wpe2 = !is("MTG_LU_WPE2", "0");
+    c.rc_wide = !is("MTG_RC_WIDE", "0");
     c.fast2_ppt8 = !is("MTG_FAST2_PPT8", "0");
     c.fast2 = !is("MTG_FAST2", "0");
     if (const char *e = getenv("MTG_MERGE_IT")) c.merge_it = (uint32_t)std::max(1L, std::min(64L, atol(e)));
@@ -816,6 +818,15 @@ static MsdPlan msd_plan(const Ctx &c, uint64_t n, unsigned nbits, double dup) {
 }
 
 static void note_bucket_index(Ctx &c, const void *keys, uint64_t n, const uint64_t *start, unsigned shift);
+
+// The plan of the rc sort fused with the merge (and of the canonical set's bucket index it reads): u128 keys
+// take one final bit fewer than the unique's plan, so a merge group holds ~480 rc + ~480 canonical keys in
+// its 1024-key LDS arrays instead of ~240 + 240 -- the per-group cost (barriers, table setup) then spreads
+// over twice the keys (configs[2]: 2.03e9 rc keys over 2^22 buckets, not 2^23)
+template <int L>
+static MsdPlan rc_plan(const Ctx &c, uint64_t n, unsigned nbits) {
+    return msd_plan<L>(c, L == 2 && c.rc_wide ? std::max<uint64_t>(1, n / 2) : n, nbits, 1.0);
+}
 
 // the rc sort's local pass fused with the merge into the real edges (local_merge_kernel)
 template <int L>
@@ -2628,7 +2639,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     uint64_t *rgi = nullptr;
     bool rgi_ok = false;
     if (canonical && !COUNTED && c.round_index) {
-        const MsdPlan rp = msd_plan<L>(c, std::max<uint64_t>(1, (uint64_t)((double)N / A.dup)), 2 * K, 1.0);
+        const MsdPlan rp = rc_plan<L>(c, std::max<uint64_t>(1, (uint64_t)((double)N / A.dup)), 2 * K);
         fb_est = rp.levels ? rp.digit_end[rp.levels] : 0;
         if (fb_est >= b1 && fb_est <= 26) {
             rgi = (uint64_t *)c.ws.get(Workspace::CANON_IDX, ((1ull << fb_est) + 2) * 8);
@@ -2719,7 +2730,7 @@ static bool collect_rounds_fused(Ctx &c, unsigned K, bool canonical, uint32_t cm
     // bits (a one-pass build gets it from its own sort's groups)
     c.gidx = Ctx::GroupIndex{};
     if (canonical && off && !COUNTED) {
-        const MsdPlan rp = msd_plan<L>(c, off, 2 * K, 1.0);
+        const MsdPlan rp = rc_plan<L>(c, off, 2 * K);
         const unsigned fb = rp.levels ? rp.digit_end[rp.levels] : 0;
         if (fb && fb <= 26) {
             const uint64_t nb = 1ull << fb;
@@ -2754,10 +2765,13 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
     uint64_t Urc = U;
     uint32_t *rc_hist = nullptr;
     bool rc_level1 = false;  // buf already partitioned by the rc sort's level-1 digit
+    // the fused merge's plan (rc_plan: u128 merge groups twice as full); the plain sort plans its own
+    const bool own_plan = rm && L2 == 2 && c.rc_wide;
+    const MsdPlan rcp = own_plan ? rc_plan<L2>(c, U, 2 * K) : MsdPlan{};
     if (K & 1) {
         unsigned rc_hist_bits = 0;
         if (!c.use_lsd && sort) {
-            const MsdPlan plan = msd_plan<L2>(c, U, 2 * K, 1.0);
+            const MsdPlan plan = own_plan ? rcp : msd_plan<L2>(c, U, 2 * K, 1.0);
             if (plan.levels) {
                 rc_hist_bits = plan.digit_end[1];
                 rc_hist = (uint32_t *)c.ws.get(Workspace::HIST1, (1u << rc_hist_bits) * 4);
@@ -2828,7 +2842,7 @@ static uint64_t stage_rc(Ctx &c, unsigned K, unsigned cbits, uint32_t cmax, Key<
     uint32_t *rca = bufc, *rcb = COUNTED ? (uint32_t *)c.ws.get(Workspace::RC_ALTC, Urc * 4) : nullptr;
     if (c.use_lsd) radix_sort<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, false);
     else Urc = msd_sort_unique<L2, COUNTED>(c, &ra, &rb, &rca, &rcb, Urc, 2 * K, cmax, 1.0, rc_hist, true, nullptr,
-                                            rc_level1, rm);
+                                            rc_level1, rm, own_plan && rcp.levels ? &rcp : nullptr);
     *rk = ra;
     *rkc = rca;
     return Urc;
