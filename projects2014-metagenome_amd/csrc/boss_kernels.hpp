@@ -1618,9 +1618,30 @@ __global__ __launch_bounds__(SplitEmitTraits<L2>::BLOCK) void split_emit_kernel(
             if (qq < ns && g >= 0 && g < (int64_t)na) s_a[qq] = st[q];
         }
     } else {
-        for (uint32_t q = tid; q < ns; q += BLOCK) {
-            const int64_t g = g0 + q;
-            if (g >= 0 && g < (int64_t)na) s_a[q] = a[g];
+        // wider keys: three loads in flight per thread at a time (configs[2]'s u128 edges), held limb by limb
+        // (an array of keys went to scratch memory)
+        constexpr int CH = 3;
+        for (uint32_t b0 = 0; b0 < ns; b0 += CH * BLOCK) {
+            uint64_t st[CH * L2];
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+                const uint32_t qq = b0 + tid + q * BLOCK;
+                const int64_t g = g0 + qq;
+                if (qq < ns && g >= 0 && g < (int64_t)na) {
+                    const Key<L2> v = a[g];
+#pragma unroll
+                    for (int w = 0; w < L2; ++w) st[q * L2 + w] = v.w[w];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+                const uint32_t qq = b0 + tid + q * BLOCK;
+                const int64_t g = g0 + qq;
+                if (qq < ns && g >= 0 && g < (int64_t)na) {
+#pragma unroll
+                    for (int w = 0; w < L2; ++w) s_a[qq].w[w] = st[q * L2 + w];
+                }
+            }
         }
     }
     for (uint32_t q = tid; q < TILE / 32; q += BLOCK) s_bm[q] = 0;

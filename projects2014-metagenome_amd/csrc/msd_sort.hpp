@@ -1019,20 +1019,23 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
 #pragma unroll
     for (int q = 0; q < PR; ++q) {
         const uint32_t i = tid + q * LB;
+        rk[q] = Key<L>::zero();  // (defined on every lane: a partly written key array went to scratch)
         if (i < nr) {
             rk[q] = keys[g0 + i];
             if (COUNTED) rv[q] = vals[g0 + i];
         }
     }
     const uint64_t cr = cgap ? cgap[gb0] : c0;
-    if constexpr (L == 1) {
+    if constexpr (L <= 2) {
         // the canonical keys' loads all in flight with the rc keys' before the LDS stores (a rolled loop
-        // waited for each load before issuing the next; u64 keys only, the wider ones' registers spill)
+        // waited for each load before issuing the next; u64 and u128 keys -- PR = 2 for u128 -- the wider
+        // ones' registers spill)
         Key<L> ckr[PR];
         uint32_t cvr[PR];
 #pragma unroll
         for (int q = 0; q < PR; ++q) {
             const uint32_t i = tid + q * LB;
+            ckr[q] = Key<L>::zero();
             if (i < nc) {
                 ckr[q] = ck[cr + i];
                 if (COUNTED) cvr[q] = cv[cr + i];
@@ -1141,14 +1144,21 @@ __global__ __launch_bounds__(LB) void local_merge_kernel(
     Key<L> ha = s_r[min(i, (uint32_t)CAP - 1)], hc = s_c[min(j, (uint32_t)CAP - 1)];
     for (uint32_t o = o0; o < o1; ++o) {
         const bool take_r = (i < nr) & ((j >= nc) | (ha < hc));  // (no short-circuit: no exec mask)
-        const Key<L> key = take_r ? ha : hc;
+        // (limb by limb: a select of whole u128 keys went through scratch memory -- the two heads stored,
+        // the taken one reloaded by address, every output key)
+        Key<L> key;
+#pragma unroll
+        for (int w = 0; w < L; ++w) key.w[w] = take_r ? ha.w[w] : hc.w[w];
         out[base + o] = key;
         if (COUNTED) outc[base + o] = *(take_r ? s_rv + i : s_cv + j);
         i += take_r ? 1u : 0u;
         j += take_r ? 0u : 1u;
         const Key<L> nx = *(take_r ? s_r + min(i, (uint32_t)CAP - 1) : s_c + min(j, (uint32_t)CAP - 1));
-        ha = take_r ? nx : ha;
-        hc = take_r ? hc : nx;
+#pragma unroll
+        for (int w = 0; w < L; ++w) {
+            ha.w[w] = take_r ? nx.w[w] : ha.w[w];
+            hc.w[w] = take_r ? hc.w[w] : nx.w[w];
+        }
         if (istart) {
             const uint64_t kb = bits_at(shr(key, ishift), 0, 32);
             uint32_t q = NGAP;
