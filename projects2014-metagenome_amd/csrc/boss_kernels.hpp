@@ -911,9 +911,47 @@ __global__ __launch_bounds__(256) void dummy_sink_kernel(
         }
     }
     __syncthreads();
+    if constexpr (L != 1) {
+        // (round 6) the staged classes fill s_r[0 .. sum of their counts) one after another: a thread's
+        // positions tid + 256 k are mapped to their class and loaded all at once, limb by limb (a rolled
+        // loop per class waited for each 16-byte load before issuing the next: configs[2]'s sink pass)
+        if (!(ABL & 4)) {
+            constexpr int NJ = (T::CAP + 255) / 256;
+            uint64_t lv[NJ * L];
+            uint32_t okm = 0;
+#pragma unroll
+            for (int k2 = 0; k2 < NJ; ++k2) {
+                const uint32_t p = tid + 256u * k2;
+                uint64_t idx = 0;
+                bool ok = false;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t o = s_off[c];
+                    if (o != ~0u && p >= o && p - o < s_cnt[c]) {
+                        ok = true;
+                        idx = s_lo[c] + (p - o);
+                    }
+                }
+#pragma unroll
+                for (int w = 0; w < L; ++w) lv[k2 * L + w] = 0;
+                if (ok) {
+                    okm |= 1u << k2;
+                    const Key<L> v = look[idx];
+#pragma unroll
+                    for (int w = 0; w < L; ++w) lv[k2 * L + w] = v.w[w];
+                }
+            }
+#pragma unroll
+            for (int k2 = 0; k2 < NJ; ++k2)
+                if ((okm >> k2) & 1u) {
+#pragma unroll
+                    for (int w = 0; w < L; ++w) s_r[tid + 256u * k2].w[w] = lv[k2 * L + w];
+                }
+        }
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        if (ABL & 4) break;
+        if (L != 1 || (ABL & 4)) break;  // (u64: the per-wave classes above; wider keys: the flat staging)
         if (s_off[c] == ~0u) continue;
         const uint64_t a = s_lo[c];
         const uint32_t off = s_off[c], cnt = s_cnt[c];
